@@ -1,0 +1,140 @@
+/*
+ * vihmc.h -- C-ABI of libvihmc.so, the MI355X (gfx950) log-posterior + gradient engine for VI-HMC.
+ *
+ * It replaces the reference's log-probability closure: the Python callable returned by
+ * `define_model_log_prob` and handed to hamiltorch's sampler.
+ *   - DeepONet VI-HMC:  Operator_network/VI_HMC/main_VI_HMC_burgers.py:27-180
+ *                       (log_prob_func :86-178, Functional_DeepONet my_make_func.py:44-83)
+ *   - DeepONet full HMC / splitting shards: Operator_network/HMC/main_HMC_splitting.py:79-258
+ *   - BNN VI-HMC:       Neural_network/VI_HMC/main_VI_HMC.py:28-153 (Functional_Net my_make_func.py:52-73)
+ *   - BNN full HMC:     hamiltorch.define_model_log_prob as called by
+ *                       Neural_network/HMC/main_regression_hmc.py:124-127 (same function, 'regression' loss)
+ * and the forward used by `predict_model` (main_VI_HMC_burgers.py:183-241, main_VI_HMC.py:156-259).
+ *
+ * Where the reference evaluates ONE parameter vector per call through PyTorch autograd, a plan here
+ * evaluates C chains at once: theta is [C, K] (K = number of sampled / "sensitive" parameters),
+ * logp is [C] and grad is [C, K]. All three are DEVICE pointers on the plan's device; inputs given
+ * at plan creation are HOST pointers and are copied (the plan owns its device copies).
+ *
+ * Conventions
+ *   - every function returns 0 on success, a nonzero code on failure; vihmc_last_error() gives a
+ *     thread-local message. A non-finite log-probability is NOT an error: it is returned as is and
+ *     the caller treats it as a rejection (reference: util.LogProbError, util.py:107-119).
+ *   - `stream` is a hipStream_t passed as void* (0 = the null stream). Calls only enqueue work;
+ *     there is no host synchronisation inside vihmc_logp_grad / vihmc_forward.
+ *   - results are deterministic: fixed-order reductions, no floating-point atomics.
+ *   - a plan is bound to one device and used from one host thread.
+ */
+#ifndef VIHMC_H
+#define VIHMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vihmc_plan vihmc_plan;
+
+enum vihmc_act  { VIHMC_ACT_IDENTITY = 0, VIHMC_ACT_TANH = 1, VIHMC_ACT_RELU = 2, VIHMC_ACT_SINE = 3 };
+enum vihmc_loss { VIHMC_LOSS_NLL = 0,       /* GaussianNLLLoss(sum), tau_out = variance  (:83-84,162-163) */
+                  VIHMC_LOSS_REGRESSION = 1 /* -0.5*tau_out*sum(r^2), tau_out = precision (:157-159)     */ };
+
+/* One nn.Linear: weight[n_out, n_in] at w_off and bias[n_out] at b_off (-1: no bias) in the flat
+ * parameter vector (util.unflatten order, Operator_network/VI_HMC/util.py:141-152). `act` is the
+ * activation applied to this layer's output (VIHMC_ACT_IDENTITY for the last layer of each MLP). */
+typedef struct {
+    int64_t w_off, b_off;
+    int32_t n_out, n_in, act, _pad;
+} vihmc_linear;
+
+/* Gaussian log-likelihood + Gaussian prior shared by both model kinds. */
+typedef struct {
+    int32_t loss;          /* enum vihmc_loss                                                     */
+    float   tau_out;       /* variance (NLL) or precision (regression)                            */
+    float   prior_scale;   /* prior divided by this (splitting shards: num_splits, :253-254)      */
+    int32_t _pad;
+} vihmc_lik_desc;
+
+/* DeepONet: `branch` and `trunk` are the layer tables of DeepONet's b1 / b2 Sequentials
+ * (Operator_network/VI_HMC/model.py:42-62); the scalar output bias b sits at flat index 0.
+ * Trunk inputs are given already mapped to features (my_make_func.py:63-65, theta-independent). */
+typedef struct {
+    int32_t n_branch_layers, n_trunk_layers;
+    const vihmc_linear* branch;
+    const vihmc_linear* trunk;
+    int64_t n_params;      /* D                                   */
+    int32_t N;             /* branch rows (functions)             */
+    int32_t P;             /* trunk rows (space-time points)      */
+    int32_t in_branch;     /* branch input width                  */
+    int32_t in_trunk;      /* trunk feature width                 */
+    int32_t K;             /* sampled parameters per chain        */
+    int32_t max_chains;    /* largest C ever passed to this plan  */
+    vihmc_lik_desc lik;
+} vihmc_deeponet_desc;
+
+/* BNN MLP (Neural_network/VI_HMC/main_VI_HMC.py:297-334): layers in Sequential order. */
+typedef struct {
+    int32_t n_layers;
+    int32_t _pad0;
+    const vihmc_linear* layers;
+    int64_t n_params;      /* D                       */
+    int32_t N;             /* data rows               */
+    int32_t in_dim;        /* input width             */
+    int32_t out_dim;       /* output width            */
+    int32_t K;
+    int32_t max_chains;
+    int32_t _pad1;
+    vihmc_lik_desc lik;
+} vihmc_mlp_desc;
+
+/* Create a DeepONet plan.
+ *   x_branch [N, in_branch] fp32, trunk_feat [P, in_trunk] fp32, y [N, P] fp32,
+ *   frozen [D] fp32: the weights that are not sampled (mu_VI; `sampled_weights` at my_make_func.py:21,48),
+ *   sens_idx [K] int64: sorted indices of the sampled parameters (gradient_indices_*.npy); K == D with
+ *            sens_idx = 0..D-1 is full-parameter HMC (mus=None branch, my_make_func.py:45-46),
+ *   prior_mu [K], prior_sd [K] fp32: Normal(prior_mu, prior_sd) per sampled parameter (:74-81,96-102).
+ * Replaces: define_model_log_prob(...) (main_VI_HMC_burgers.py:27-84), incl. the torch.load of mu/sigma. */
+int vihmc_deeponet_plan_create(vihmc_plan** out, const vihmc_deeponet_desc* d,
+                               const float* x_branch, const float* trunk_feat, const float* y,
+                               const float* frozen, const int64_t* sens_idx,
+                               const float* prior_mu, const float* prior_sd, int device);
+
+/* Create a BNN plan (x [N, in_dim], y [N, out_dim]). Replaces Neural_network/VI_HMC/main_VI_HMC.py:28-95;
+ * prior_mu/prior_sd already expanded per sampled parameter with the reference's per-tensor slicing
+ * (main_VI_HMC.py:107-112). */
+int vihmc_mlp_plan_create(vihmc_plan** out, const vihmc_mlp_desc* d,
+                          const float* x, const float* y,
+                          const float* frozen, const int64_t* sens_idx,
+                          const float* prior_mu, const float* prior_sd, int device);
+
+/* log p(theta_c) and d log p / d theta_c for C <= max_chains chains.
+ * Replaces: log_prob_func(params) + torch.autograd.grad(log_prob, params) [hamiltorch params_grad],
+ * main_VI_HMC_burgers.py:86-178 / main_VI_HMC.py:96-151. grad may be NULL (value only). */
+int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, void* stream);
+
+/* Forward only: logp [C] and the network output out [C, N, P] (DeepONet) or [C, N, out_dim] (BNN).
+ * Replaces log_prob_func(..., predict=True) -> (logp, output) (main_VI_HMC_burgers.py:175-176). */
+int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* out, void* stream);
+
+/* Plan introspection: 0 = DeepONet, 1 = MLP; D; K; max_chains; device bytes owned. */
+int     vihmc_plan_kind(const vihmc_plan* p);
+int64_t vihmc_plan_n_params(const vihmc_plan* p);
+int     vihmc_plan_K(const vihmc_plan* p);
+int     vihmc_plan_max_chains(const vihmc_plan* p);
+int64_t vihmc_plan_device_bytes(const vihmc_plan* p);
+
+/* Kernel-level timing hook for the roofline: HIP events bracket every launch of kernel `which`
+ * (0 = fused contraction, owner=trunk) on the plan's stream when enabled; the accumulated time in ms
+ * and launch count are read back with vihmc_timing_read (this syncs the events). */
+int vihmc_timing_enable(vihmc_plan* p, int which, int on);
+int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches);
+
+void        vihmc_plan_destroy(vihmc_plan* p);
+const char* vihmc_last_error(void);
+const char* vihmc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VIHMC_H */

@@ -1,0 +1,254 @@
+"""Generate the golden vectors that pin the oracle, by running the REFERENCE's own log-prob code.
+
+Run in the build container only (it reads /root/reference, which the GPU box does not have):
+
+    python tests/golden/make_golden.py
+
+The reference is imported as-is (read-only, no bytecode written) with an empty stub for the
+un-vendored third-party ``hamiltorch`` package, which the log-prob closures never call
+(SURVEY.md §8c). Its ``define_model_log_prob`` closures are evaluated with torch.autograd on the CPU
+on seeded synthetic inputs, and the outputs are written as small .npz fixtures next to this file:
+
+* ``bnn_*.npz``        Neural_network/VI_HMC/main_VI_HMC.py:28-153 on the shipped Neural_network/Data
+* ``deeponet_*.npz``   Operator_network/VI_HMC/main_VI_HMC_burgers.py:27-180 (VI-HMC closure) and
+                       Operator_network/HMC/main_HMC_splitting.py:79-258 (full-parameter split closures)
+
+Small cases store every input; the full Burgers-shape case stores the generator seed plus SHA-256 of
+the regenerated inputs (vihmc.data.deeponet_problem, pure numpy) and the outputs.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+import tempfile
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(ROOT, "vi-hmc_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from vihmc.data import deeponet_problem, save_vi_artefacts  # noqa: E402
+from vihmc.layout import DeepONetSpec  # noqa: E402
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def stub_hamiltorch():
+    ht = types.ModuleType("hamiltorch")
+    ht.samplers = types.ModuleType("hamiltorch.samplers")
+    ht.util = types.ModuleType("hamiltorch.util")
+    sys.modules["hamiltorch"] = ht
+    sys.modules["hamiltorch.samplers"] = ht.samplers
+    sys.modules["hamiltorch.util"] = ht.util
+
+
+def import_ref(subdir: str, main: str):
+    """Import reference modules of one directory (util/config/model/my_make_func clash across dirs)."""
+    for m in ("util", "config", "config_splitting", "model", "my_make_func", main):
+        sys.modules.pop(m, None)
+    d = os.path.join(REF, subdir)
+    sys.path.insert(0, d)
+    try:
+        mod = __import__(main)
+    finally:
+        sys.path.remove(d)
+    return mod
+
+
+def ref_logp_grad(fn, theta: np.ndarray):
+    p = torch.tensor(theta, dtype=torch.float32).requires_grad_()
+    lp = fn(p)
+    g, = torch.autograd.grad(lp.sum(), p)
+    return np.float64(lp.detach().sum().item()), g.numpy().astype(np.float32)
+
+
+# ------------------------------------------------------------------------------------------------
+# BNN (Neural_network/VI_HMC)
+# ------------------------------------------------------------------------------------------------
+def bnn_cases(out):
+    cwd = os.getcwd()
+    os.chdir(os.path.join(REF, "Neural_network", "VI_HMC"))   # get_data reads ../Data
+    try:
+        M = import_ref("Neural_network/VI_HMC", "main_VI_HMC")
+        cfg = M.cfg
+        x_tr, y_tr, x_val, y_val = M.get_data()
+    finally:
+        os.chdir(cwd)
+    np.savez(os.path.join(out, "bnn_data.npz"), x_train=x_tr.numpy(), y_train=y_tr.numpy(),
+             x_val=x_val.numpy(), y_val=y_val.numpy())
+    tmp = tempfile.mkdtemp()
+    cases = {
+        # configs 2-3: NLL variance 0.0025, prior_var 1, sensitive subset
+        "bnn_vi_hmc": dict(loss="NLL", tau_out=0.0025, prior_var=1.0, K=90, load_prior=False, seed=11),
+        # config 1: hamiltorch define_model_log_prob == regression, precision 400, tau 1, all params
+        "bnn_hmc_regression": dict(loss="regression", tau_out=400.0, prior_var=1.0, K=None, load_prior=False, seed=12),
+        # load_prior: Normal(mu_VI[idx], sigma_VI[idx]) (main_VI_HMC.py:87-88,357-363)
+        "bnn_load_prior": dict(loss="NLL", tau_out=0.0025, prior_var=1.0, K=60, load_prior=True, seed=13),
+        # non-uniform per-tensor prior variances exercise the slicing quirk (main_VI_HMC.py:107-112)
+        "bnn_tensor_prior": dict(loss="NLL", tau_out=0.01, prior_var=[0.5, 2.0, 1.5, 0.25, 3.0, 1.0], K=120,
+                                 load_prior=False, seed=14),
+    }
+    for name, c in cases.items():
+        torch.manual_seed(c["seed"])
+        cfg.loss, cfg.tau_out, cfg.load_prior = c["loss"], c["tau_out"], c["load_prior"]
+        cfg.prior_file, cfg.prior_uid = tmp, name
+        net = M.get_model(cfg.bias)
+        flat = torch.cat([p.detach().flatten() for p in net.parameters()]).numpy()
+        rng = np.random.default_rng(c["seed"])
+        D = flat.size
+        mu = (flat + 0.05 * rng.standard_normal(D)).astype(np.float32)
+        sd = (0.1 * np.abs(mu) + 0.01).astype(np.float32)
+        idx = np.arange(D) if c["K"] is None else np.sort(rng.choice(D, c["K"], replace=False))
+        save_vi_artefacts(tmp, name, mu, sd, idx)
+        shapes = [p.shape for p in net.parameters()]
+        sizes = [p.nelement() for p in net.parameters()]
+        if c["load_prior"]:
+            prior_list = [torch.from_numpy(mu[idx]), torch.from_numpy(sd[idx])]
+        else:
+            pv = c["prior_var"] if isinstance(c["prior_var"], list) else [c["prior_var"]] * len(sizes)
+            prior_list = [torch.tensor(float(v)) for v in pv]
+        fn = M.define_model_log_prob(net, c["loss"], x_tr, y_tr, sizes, shapes, prior_list, c["tau_out"],
+                                     grad_ind=idx)
+        fnp = M.define_model_log_prob(net, c["loss"], x_val, y_val, sizes, shapes, prior_list, c["tau_out"],
+                                      grad_ind=idx, predict=True)
+        thetas = [mu[idx], mu[idx] + 0.1 * rng.standard_normal(idx.size).astype(np.float32)]
+        res = {}
+        for t, th in enumerate(thetas):
+            lp, g = ref_logp_grad(fn, th)
+            res[f"logp{t}"], res[f"grad{t}"], res[f"theta{t}"] = lp, g, th
+            with torch.no_grad():
+                lpv, pred = fnp(torch.tensor(th))
+            res[f"val_logp{t}"], res[f"val_pred{t}"] = np.float64(lpv.sum().item()), pred.numpy()
+        prior_var = np.asarray(c["prior_var"] if isinstance(c["prior_var"], list) else [c["prior_var"]] * len(sizes))
+        np.savez(os.path.join(out, f"{name}.npz"), mu=mu, sd=sd, grad_ind=idx.astype(np.int64), loss=c["loss"],
+                 tau_out=c["tau_out"], prior_var=prior_var, load_prior=c["load_prior"], **res)
+        print(name, "logp0", res["logp0"], "logp1", res["logp1"])
+
+
+# ------------------------------------------------------------------------------------------------
+# DeepONet (Operator_network/VI_HMC, Operator_network/HMC)
+# ------------------------------------------------------------------------------------------------
+def deeponet_vihmc(M, spec: DeepONetSpec, prob, name, out, thetas, load_prior=False, store_inputs=True,
+                   grad_subsample=None, seed_meta=None, with_predict=True):
+    cfg = M.cfg
+    tmp = tempfile.mkdtemp()
+    cfg.branch_depth, cfg.trunk_depth, cfg.activation = spec.depth_branch, spec.depth_trunk, spec.activation
+    cfg.load_prior, cfg.sample_data = load_prior, False
+    cfg.prior_file, cfg.prior_uid = tmp, name
+    save_vi_artefacts(tmp, name, prob.mu, prob.sigma, prob.grad_ind)
+    net = M.DeepONet(spec.width_branch, spec.width_trunk, spec.in_branch, spec.in_trunk, spec.depth_branch,
+                     spec.depth_trunk, spec.activation, spec.output_neurons)
+    idx = prob.grad_ind
+    if load_prior:
+        tau_list = [torch.from_numpy(prob.mu[idx]), torch.from_numpy(prob.sigma[idx])]
+    else:
+        tau_list = [torch.tensor(cfg.prior_var)]
+    tr = (torch.from_numpy(prob.branch_in), torch.from_numpy(prob.trunk_in), torch.from_numpy(prob.y))
+    fn = M.define_model_log_prob(net, cfg.loss, tr, tau_list, cfg.tau_out, device="cpu")
+    res = {}
+    for t, th in enumerate(thetas):
+        lp, g = ref_logp_grad(fn, th)
+        res[f"logp{t}"] = lp
+        if grad_subsample is None:
+            res[f"grad{t}"], res[f"theta{t}"] = g, th
+        else:
+            res[f"grad{t}_sub"] = g[grad_subsample]
+            res[f"grad{t}_norm"] = np.float64(np.linalg.norm(g.astype(np.float64)))
+            res[f"theta{t}_sha"] = sha(th)
+        if with_predict:
+            fnp = M.define_model_log_prob(net, cfg.loss, tr, tau_list, cfg.tau_out, predict=True, device="cpu")
+            with torch.no_grad():
+                lpv, pred = fnp(torch.tensor(th))
+            res[f"pred{t}"] = pred.numpy()
+        print(name, t, "logp", lp)
+    meta = dict(spec=np.array([spec.width_branch, spec.width_trunk, spec.in_branch, spec.in_trunk, spec.depth_branch,
+                               spec.depth_trunk, spec.out]),
+                loss=cfg.loss, tau_out=cfg.tau_out, prior_var=cfg.prior_var, load_prior=load_prior)
+    if store_inputs:
+        meta.update(branch_in=prob.branch_in, trunk_in=prob.trunk_in, y=prob.y, mu=prob.mu, sigma=prob.sigma,
+                    grad_ind=prob.grad_ind)
+    else:
+        meta.update(seed_meta, sha_branch=sha(prob.branch_in), sha_trunk=sha(prob.trunk_in), sha_y=sha(prob.y),
+                    sha_mu=sha(prob.mu), sha_idx=sha(prob.grad_ind), grad_subsample=grad_subsample)
+    np.savez_compressed(os.path.join(out, f"{name}.npz"), **meta, **res)
+
+
+def refshape_theta1(th0):
+    return (th0 + 0.01 * np.random.default_rng(7).standard_normal(th0.size)).astype(np.float32)
+
+
+def deeponet_cases(out, full_size=True):
+    M = import_ref("Operator_network/VI_HMC", "main_VI_HMC_burgers")
+    small = DeepONetSpec(width_branch=16, width_trunk=16, in_branch=12, in_trunk=5, depth_branch=3, depth_trunk=3)
+    prob = deeponet_problem(seed=3, n=6, nt=5, nx=7, spec=small, k=300)
+    rng = np.random.default_rng(3)
+    th0 = prob.mu[prob.grad_ind]
+    th1 = (th0 + 0.05 * rng.standard_normal(th0.size)).astype(np.float32)
+    deeponet_vihmc(M, small, prob, "deeponet_small", out, [th0, th1])
+    deeponet_vihmc(M, small, prob, "deeponet_small_loadprior", out, [th0, th1], load_prior=True)
+    # odd widths exercise the kernels' padding paths (non-multiples of 4 and 16)
+    odd = DeepONetSpec(width_branch=37, width_trunk=37, in_branch=19, in_trunk=5, depth_branch=4, depth_trunk=2,
+                       output_neurons=21)
+    probo = deeponet_problem(seed=4, n=45, nt=7, nx=9, spec=odd, k=None)
+    th0 = probo.mu[probo.grad_ind]
+    th1 = (th0 + 0.02 * rng.standard_normal(th0.size)).astype(np.float32)
+    deeponet_vihmc(M, odd, probo, "deeponet_odd_full", out, [th0, th1])
+    # reference network shape (width 100, depth 9, 101 branch inputs), reduced N/P, K = 17240
+    ref = DeepONetSpec()
+    probr = deeponet_problem(seed=5, n=8, nt=11, nx=11, spec=ref, k=17240)
+    th0 = probr.mu[probr.grad_ind]
+    th1 = refshape_theta1(th0)
+    sub = np.sort(np.random.default_rng(5).choice(17240, 2048, replace=False))
+    deeponet_vihmc(M, ref, probr, "deeponet_refshape", out, [th0, th1], store_inputs=False, grad_subsample=sub,
+                   seed_meta=dict(seed=5, n=8, nt=11, nx=11, k=17240, theta1_seed=7), with_predict=False)
+    if full_size:
+        probf = deeponet_problem(seed=0)
+        th0 = probf.mu[probf.grad_ind]
+        subf = np.sort(np.random.default_rng(0).choice(probf.K, 2048, replace=False))
+        deeponet_vihmc(M, ref, probf, "deeponet_burgers", out, [th0], store_inputs=False, grad_subsample=subf,
+                       seed_meta=dict(seed=0, n=1000, nt=101, nx=101, k=17240), with_predict=False)
+    return probr, th1
+
+
+def deeponet_split_cases(out):
+    """Full-parameter split closures (Operator_network/HMC/main_HMC_splitting.py:79-258)."""
+    M = import_ref("Operator_network/HMC", "main_HMC_splitting")
+    cfg = M.cfg
+    small = DeepONetSpec(width_branch=16, width_trunk=16, in_branch=12, in_trunk=5, depth_branch=3, depth_trunk=3)
+    cfg.branch_depth, cfg.trunk_depth, cfg.activation, cfg.load_prior, cfg.sample_data = 3, 3, "tanh", False, False
+    cfg.dataset = "Burgers"
+    prob = deeponet_problem(seed=6, n=8, nt=5, nx=7, spec=small, k=None)
+    net = M.DeepONet(16, 16, 12, 5, 3, 3, "tanh", None)
+    shards = []
+    for i in range(2):
+        sl = slice(4 * i, 4 * (i + 1))
+        shards.append((torch.from_numpy(prob.branch_in[sl]), torch.from_numpy(prob.trunk_in),
+                       torch.from_numpy(prob.y[sl])))
+    fns = M.define_split_model_log_prob(net, cfg.loss, shards, 2, [torch.tensor(cfg.prior_var)], cfg.tau_out,
+                                        device="cpu", verbose=False)
+    rng = np.random.default_rng(6)
+    th = (prob.mu + 0.01 * rng.standard_normal(prob.mu.size)).astype(np.float32)
+    res = {}
+    for m, fn in enumerate(fns):
+        lp, g = ref_logp_grad(fn, th)
+        res[f"logp_shard{m}"], res[f"grad_shard{m}"] = lp, g
+        print("split shard", m, lp)
+    np.savez_compressed(os.path.join(out, "deeponet_split.npz"), branch_in=prob.branch_in, trunk_in=prob.trunk_in,
+                        y=prob.y, theta=th, prior_var=cfg.prior_var, tau_out=cfg.tau_out, loss=cfg.loss,
+                        spec=np.array([16, 16, 12, 5, 3, 3, 16]), **res)
+
+
+if __name__ == "__main__":
+    stub_hamiltorch()
+    torch.set_num_threads(8)
+    bnn_cases(HERE)
+    deeponet_cases(HERE, full_size="--no-full" not in sys.argv)
+    deeponet_split_cases(HERE)

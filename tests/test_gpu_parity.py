@@ -1,0 +1,148 @@
+"""HIP path vs oracle / reference goldens, through the C-ABI (libvihmc.so via vihmc.engine).
+
+Tolerances (fp32 kernels, different summation order from torch's CPU kernels):
+  logp: |Δ| <= 2e-5·|logp| + 1e-3 (DeepONet: per-lane fp64 accumulation of r² keeps this tight)
+  grad: ||Δ|| <= 2e-4·||grad|| and elementwise atol 1e-4·max|grad|
+  predictions: rtol 1e-4, atol 1e-4·max|pred|
+"""
+import numpy as np
+import pytest
+import torch
+
+from goldens import BNN_CASES, DEEPONET_CASES, bnn_case, deeponet_case, load, spec_of
+from oracle.deeponet_ref import deeponet_layout, np_logp_grad
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_norm(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def engine_for(c, max_chains=4, device="cuda:0"):
+    from vihmc.engine import DeepONetEngine, trunk_features
+    p = c.prob
+    return DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
+                          c.prior_sd, c.loss, c.tau_out, max_chains=max_chains, device=device)
+
+
+def check_logp(lp, ref):
+    assert abs(lp - ref) <= 2e-5 * abs(ref) + 1e-3, (lp, ref)
+
+
+def check_grad(g, ref):
+    assert rel_norm(g, ref) < 2e-4
+    np.testing.assert_allclose(g, ref, rtol=2e-3, atol=1e-4 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("name", DEEPONET_CASES + ["deeponet_burgers"])
+def test_deeponet_engine_matches_golden(name, cuda_device):
+    c = deeponet_case(name)
+    eng = engine_for(c, max_chains=len(c.thetas))
+    th = torch.tensor(np.stack(c.thetas), device=cuda_device)
+    lp, g = eng.logp_grad(th)
+    lp, g = lp.cpu().numpy(), g.cpu().numpy()
+    for t in range(len(c.thetas)):
+        check_logp(float(lp[t]), float(c.g[f"logp{t}"]))
+        if f"grad{t}" in c.g:
+            check_grad(g[t], c.g[f"grad{t}"])
+        else:
+            sub = c.g["grad_subsample"]
+            gs = c.g[f"grad{t}_sub"]
+            np.testing.assert_allclose(g[t][sub], gs, rtol=2e-3, atol=2e-4 * np.abs(gs).max())
+            assert np.linalg.norm(g[t].astype(np.float64)) == pytest.approx(float(c.g[f"grad{t}_norm"]), rel=2e-4)
+        if f"pred{t}" in c.g:
+            lpf, out = eng.forward(th[t:t + 1])
+            pred = c.g[f"pred{t}"]
+            np.testing.assert_allclose(out[0].cpu().numpy(), pred, rtol=1e-4, atol=1e-4 * np.abs(pred).max())
+            check_logp(float(lpf[0]), float(c.g[f"logp{t}"]))
+
+
+@pytest.mark.parametrize("name", ["deeponet_small", "deeponet_odd_full"])
+def test_deeponet_engine_vs_fp64_oracle_many_chains(name, cuda_device):
+    """C chains with independent thetas in one launch == each chain against the fp64 oracle."""
+    c = deeponet_case(name)
+    rng = np.random.default_rng(42)
+    C = 7
+    base = c.thetas[0]
+    thetas = np.stack([base + 0.03 * rng.standard_normal(base.size).astype(np.float32) for _ in range(C)])
+    eng = engine_for(c, max_chains=C)
+    lp, g = eng.logp_grad(torch.tensor(thetas, device=cuda_device))
+    lay = deeponet_layout(c.spec.in_branch, c.spec.width_branch, c.spec.depth_branch, c.spec.in_trunk,
+                          c.spec.width_trunk, c.spec.depth_trunk, c.spec.out)
+    p = c.prob
+    for i in range(C):
+        rl, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, thetas[i], c.prior_mu,
+                                 c.prior_sd, c.loss, c.tau_out, full=c.full)
+        check_logp(float(lp[i]), rl)
+        check_grad(g[i].cpu().numpy(), rg)
+    # a smaller C on the same plan only touches the first C chains and agrees bit for bit
+    lp2, g2 = eng.logp_grad(torch.tensor(thetas[:3], device=cuda_device))
+    assert torch.equal(lp2, lp[:3]) and torch.equal(g2, g[:3])
+
+
+def test_deeponet_engine_deterministic(cuda_device):
+    c = deeponet_case("deeponet_refshape")
+    eng = engine_for(c, max_chains=2)
+    th = torch.tensor(np.stack(c.thetas), device=cuda_device)
+    a = eng.logp_grad(th)
+    b = eng.logp_grad(th)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert torch.equal(eng.logp(th), a[0])
+
+
+def test_deeponet_split_shards_engine(cuda_device):
+    from vihmc.engine import DeepONetEngine, trunk_features
+    g = load("deeponet_split")
+    spec = spec_of(g)
+    th = torch.tensor(g["theta"], device=cuda_device)[None]
+    for m in range(2):
+        sl = slice(4 * m, 4 * (m + 1))
+        eng = DeepONetEngine(spec, g["branch_in"][sl], trunk_features(g["trunk_in"]), g["y"][sl], g["theta"],
+                             np.arange(spec.n_params), 0.0, float(np.sqrt(g["prior_var"])), str(g["loss"]),
+                             float(g["tau_out"]), prior_scale=2.0, device=cuda_device)
+        lp, gr = eng.logp_grad(th)
+        check_logp(float(lp[0]), float(g[f"logp_shard{m}"]))
+        check_grad(gr[0].cpu().numpy(), g[f"grad_shard{m}"])
+
+
+def test_deeponet_nonfinite_is_not_an_error(cuda_device):
+    c = deeponet_case("deeponet_small")
+    eng = engine_for(c, max_chains=2)
+    th = np.stack(c.thetas)
+    th[1, 3] = np.nan
+    lp, g = eng.logp_grad(torch.tensor(th, device=cuda_device))
+    lp = lp.cpu().numpy()
+    check_logp(float(lp[0]), float(c.g["logp0"]))
+    assert not np.isfinite(lp[1])
+
+
+def test_engine_rejects_bad_shapes(cuda_device):
+    c = deeponet_case("deeponet_small")
+    eng = engine_for(c, max_chains=2)
+    with pytest.raises(ValueError):
+        eng.logp_grad(torch.zeros(3, eng.K, device=cuda_device))
+    with pytest.raises(ValueError):
+        eng.logp_grad(torch.zeros(1, eng.K + 1, device=cuda_device))
+
+
+@pytest.mark.parametrize("name", BNN_CASES)
+def test_bnn_engine_matches_golden(name, cuda_device):
+    from vihmc.engine import MLPEngine
+    c = bnn_case(name)
+    g = c.g
+    eng = MLPEngine(c.spec, c.data["x_train"], c.data["y_train"], g["mu"], c.idx, c.prior_mu, c.prior_sd, c.loss,
+                    c.tau_out, max_chains=2, device=cuda_device)
+    th = torch.tensor(np.stack(c.thetas), device=cuda_device)
+    lp, gr = eng.logp_grad(th)
+    for t in range(2):
+        check_logp(float(lp[t]), float(g[f"logp{t}"]))
+        check_grad(gr[t].cpu().numpy(), g[f"grad{t}"])
+    val = MLPEngine(c.spec, c.data["x_val"], c.data["y_val"], g["mu"], c.idx, c.prior_mu, c.prior_sd, c.loss,
+                    c.tau_out, max_chains=2, device=cuda_device)
+    lpv, pred = val.forward(th)
+    for t in range(2):
+        check_logp(float(lpv[t]), float(g[f"val_logp{t}"]))
+        np.testing.assert_allclose(pred[t].cpu().numpy(), g[f"val_pred{t}"], rtol=1e-4, atol=1e-4)

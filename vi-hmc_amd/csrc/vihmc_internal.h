@@ -1,0 +1,107 @@
+// Internal declarations shared by the kernels (vihmc_kernels.hip) and the plan / C-ABI layer
+// (vihmc_plan.hip). Nothing here crosses the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace vihmc {
+
+enum { ACT_ID = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SINE = 3 };
+enum { MODE_FWD = 0, MODE_BWD = 1 };
+
+// ---------------------------------------------------------------------------------------------
+// Row-dot GEMM: O[m][n] = epilogue( sum_k A[m][k] * B[n][k] ), both operands row-major with the
+// contraction index contiguous. Used for every forward layer (A = activations, B = W[n_out][n_in])
+// and for the backward input-gradient (A = delta, B = W^T[n_in][n_out]).
+//   FWD epilogue: O = act(acc + bias[n])
+//   BWD epilogue: O = acc * act'(H[m][n])      (H = the stored activation of the layer below)
+// Columns [Nn, ldo) of O are written as zeros so the next GEMM can read whole 4-float groups.
+// ---------------------------------------------------------------------------------------------
+struct RowdotProb {
+    const float* A; int64_t a_cs; int32_t lda;
+    const float* B; int64_t b_cs; int32_t ldb;
+    float* O;       int64_t o_cs; int32_t ldo;
+    const float* bias; int64_t bias_cs;
+    const float* H; int64_t h_cs; int32_t ldh;
+    int32_t M, Nn, K, act;
+    int32_t tiles;          // ceil(M / (16*MS))
+};
+struct RowdotArgs {
+    RowdotProb p[2];
+    int32_t nprob, C;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Column-sum GEMM for weight gradients: part[chunk][n][j] = sum_{m in chunk} D[m][n] * H[m][j],
+// plus the bias gradient part[chunk][n_out*ldh + n] = sum_m D[m][n]. One partial per row chunk,
+// reduced in fixed order by k_reduce_partials (deterministic, no atomics).
+// ---------------------------------------------------------------------------------------------
+struct ColsumProb {
+    const float* D; int64_t d_cs; int32_t ldd;
+    const float* H; int64_t h_cs; int32_t ldh;
+    float* part;    int64_t part_cs;   // per chain: n_chunks * (n_out*ldh + n_out_pad)
+    int32_t M, n_out, n_in, rows_per_chunk, n_chunks, n_pairs, part_stride;
+};
+struct ColsumArgs {
+    ColsumProb p[2];
+    int32_t nprob, C;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Fused branch x trunk contraction with the Gaussian likelihood, owner form.
+//   S[q][o] = sum_k Q[q][k] * Own[o][k] + b0;  r = S - Y[q][o];  G = gscale * r
+//   dOwn[o][j] = sum_q G[q][o] * Q[q][j]            (WITH_GRAD)
+// The wave owns 32 rows of `Own` and streams `Q` in 16-row steps; S is never stored.
+// Side A: Own = Z_trunk [P], Q = Z_branch [N], Y = y [N][P]   -> dZ_trunk (complete) + sum r^2, sum G
+// Side B: Own = Z_branch [N], Q = Z_trunk chunk, Y = y^T [P][N] -> dZ_branch partial per chunk
+// Forward-only (predict) writes out[q][o] = S into `out` (side A, o = p contiguous).
+// ---------------------------------------------------------------------------------------------
+struct ContractProb {
+    const float* Own; int64_t own_cs; int32_t ldown;
+    const float* Q;   int64_t q_cs;   int32_t ldq;
+    const float* Y;   int32_t ldy;
+    const float* b0;  int64_t b0_cs;
+    float* out;       int64_t out_cs; int32_t ldout; int64_t out_chunk_stride;
+    double* stats;    int64_t stats_cs;   // 2 doubles per wave (sum r^2, sum G) when with_stats
+    int32_t Mo, Mq, W;
+    int32_t o_tiles, q_chunks, q_per_chunk;
+    int32_t with_stats, write_s;
+    float gscale;
+};
+
+// launchers (vihmc_kernels.hip)
+hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s);
+hipError_t launch_colsum(const ColsumArgs& a, int jt, hipStream_t s);
+hipError_t launch_contract(const ContractProb& p, int C, bool with_grad, hipStream_t s);
+hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* frozen, const int32_t* map_w,
+                              const int32_t* map_wt, int64_t D, hipStream_t s);
+hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, int K, const int32_t* smap_w,
+                          const int32_t* smap_wt, hipStream_t s);
+// Sum `n_parts` partial slabs of `len` floats (slab stride `part_stride`, chain stride `in_cs`) into
+// dst[c*dst_cs + e] (e < len), fixed order.
+struct ReduceJob {
+    const float* src; int64_t in_cs; int64_t part_stride; int32_t n_parts; int32_t len;
+    float* dst; int64_t dst_cs;
+};
+hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s);
+hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_waves, int C, float* lik,
+                                 float* gp, int64_t gp_cs, double count, int loss, float tau_out, hipStream_t s);
+hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
+                               const float* prior_mu, const float* prior_inv_var, double prior_const,
+                               float prior_scale, const float* lik, int C, float* logp, float* grad,
+                               hipStream_t s);
+
+// BNN: one wave per chain, everything in registers / LDS.
+struct MlpLayer { int32_t w_off, b_off, n_out, n_in, act; };
+struct MlpArgs {
+    MlpLayer L[6];
+    int32_t n_layers, D, K, N, in_dim, out_dim;
+    const float* x; const float* y; const float* frozen; const int32_t* idx;
+    const float* prior_mu; const float* prior_inv_var;
+    double prior_const; float prior_scale; int32_t loss; float tau_out;
+    const float* theta; float* logp; float* grad; float* out;
+};
+hipError_t launch_mlp(const MlpArgs& a, int C, int maxw, hipStream_t s);
+size_t mlp_lds_bytes(int D, int n_layers, int maxw);
+
+}  // namespace vihmc

@@ -1,0 +1,763 @@
+// Plan management and the extern "C" boundary of libvihmc.so (declared in include/vihmc.h).
+//
+// A DeepONet plan owns, per chain c < max_chains:
+//   packed weights  [dp]   : b0 slot, then per layer  Wp[n_out][ldi] | bias[n_out] | WT[n_in][ldo]
+//                            (ld* = round_up(.,4) so every row is 16-B aligned for float4 operand loads;
+//                            padding stays zero), initialised once from the frozen vector (mu_VI);
+//                            each evaluation only scatters theta into the K sampled positions.
+//   activations     per net: h_j [rows][ldo_j] for every layer j (needed by the backward)
+//   deltas          per net: 2 ping-pong buffers [rows][max ldo]
+//   gradient        [dp]   : packed layout (Wp | bias) + slot 0 for db0, gathered at the sampled indices
+//   partial slabs   side-B contraction partials and per-row-chunk dW/db partials (fixed-order reduce)
+// Shared across chains: branch input [N][ldxb], trunk features [P][ldxt], y [N][P] and y^T [P][N].
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vihmc.h"
+#include "vihmc_internal.h"
+
+using namespace vihmc;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& msg, int code = 1) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return fail(std::string(#expr) + ": " + hipGetErrorString(e_), (int)e_); \
+    } while (0)
+
+inline int64_t r4(int64_t x) { return (x + 3) & ~int64_t(3); }
+inline int64_t r64(int64_t x) { return (x + 63) & ~int64_t(63); }
+inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+struct LayerPk {
+    int n_out, n_in, ldi, ldo, act;
+    int64_t wp, bias, wt;
+    // dW partials
+    int n_chunks;
+    int64_t part_off, part_stride;
+};
+
+struct Net {
+    std::vector<LayerPk> L;
+    int rows = 0, ld_in = 0;
+    float* input = nullptr;       // shared [rows][ld_in]
+    float* act = nullptr;         // per chain
+    int64_t act_cs = 0;
+    std::vector<int64_t> h_off;
+    float* delta[2] = {nullptr, nullptr};
+    int64_t delta_cs = 0;
+    float* dwpart = nullptr;
+    int64_t dwpart_cs = 0;
+    int rows_per_chunk = 256;
+};
+
+}  // namespace
+
+struct vihmc_plan {
+    int kind = 0;  // 0 DeepONet, 1 MLP
+    int device = 0;
+    int64_t D = 0;
+    int K = 0, maxC = 0;
+    vihmc_lik_desc lik{};
+    std::vector<void*> allocs;
+    int64_t bytes = 0;
+
+    int32_t* smap_w = nullptr;
+    int32_t* smap_wt = nullptr;
+    float* prior_mu = nullptr;
+    float* prior_iv = nullptr;
+    double prior_const = 0.0;
+    float* lik_buf = nullptr;
+
+    // DeepONet
+    int N = 0, P = 0, W = 0, ldz = 0;
+    Net nets[2];
+    float* packed = nullptr;
+    float* gp = nullptr;
+    int64_t dp = 0;
+    float *y = nullptr, *yT = nullptr;
+    float* partB = nullptr;
+    int64_t partB_cs = 0;
+    int qchunksB = 1, qperB = 16;
+    double* stats = nullptr;
+    int64_t stats_cs = 0;
+    int nwavesA = 0;
+    ReduceJob* jobsB = nullptr;
+    ReduceJob* jobsW = nullptr;
+    int n_jobsW = 0, max_lenW = 0, lenB = 0;
+
+    // MLP
+    MlpArgs mlp{};
+    int maxw = 0;
+
+    // timing hook
+    int timing_on = 0, timing_which = 0;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+
+    template <typename T>
+    int alloc(T** p, int64_t n) {
+        void* v = nullptr;
+        const size_t sz = std::max<int64_t>(n, 1) * sizeof(T);
+        hipError_t e = hipMalloc(&v, sz);
+        if (e != hipSuccess) return fail(std::string("hipMalloc(") + std::to_string(sz) + "): " + hipGetErrorString(e), (int)e);
+        e = hipMemset(v, 0, sz);
+        if (e != hipSuccess) return fail(std::string("hipMemset: ") + hipGetErrorString(e), (int)e);
+        allocs.push_back(v);
+        bytes += sz;
+        *p = static_cast<T*>(v);
+        return 0;
+    }
+    template <typename T>
+    int upload(T** p, const T* host, int64_t n) {
+        if (int rc = alloc(p, n)) return rc;
+        HIPCHK(hipMemcpy(*p, host, n * sizeof(T), hipMemcpyHostToDevice));
+        return 0;
+    }
+    ~vihmc_plan() {
+        for (void* p : allocs) (void)hipFree(p);
+        for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+    }
+
+    int timing_begin(int which, hipStream_t s, hipEvent_t* stop) {
+        *stop = nullptr;
+        if (!timing_on || which != timing_which) return 0;
+        while (ev_pool.size() < ev_used + 2) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            ev_pool.push_back(e);
+        }
+        HIPCHK(hipEventRecord(ev_pool[ev_used], s));
+        *stop = ev_pool[ev_used + 1];
+        ev_used += 2;
+        return 0;
+    }
+};
+
+namespace {
+
+int prior_setup(vihmc_plan* p, const float* prior_mu, const float* prior_sd) {
+    std::vector<float> iv(p->K);
+    double cst = 0.0;
+    const double half_log_2pi = 0.5 * std::log(2.0 * M_PI);
+    for (int k = 0; k < p->K; ++k) {
+        const double sd = prior_sd[k];
+        if (!(sd > 0.0)) return fail("prior_sd must be > 0 (index " + std::to_string(k) + ")");
+        iv[k] = (float)(1.0 / (sd * sd));
+        cst += -std::log(sd) - half_log_2pi;
+    }
+    p->prior_const = cst;
+    if (int rc = p->upload(&p->prior_mu, prior_mu, p->K)) return rc;
+    if (int rc = p->upload(&p->prior_iv, iv.data(), p->K)) return rc;
+    return 0;
+}
+
+int check_lik(const vihmc_lik_desc& l) {
+    if (l.loss != VIHMC_LOSS_NLL && l.loss != VIHMC_LOSS_REGRESSION) return fail("unsupported loss kind");
+    if (!(l.prior_scale > 0.f)) return fail("prior_scale must be > 0");
+    return 0;
+}
+
+int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb, const float* tf, const float* y,
+                   const float* frozen, const int64_t* idx, const float* prior_mu, const float* prior_sd) {
+    if (d->n_branch_layers < 1 || d->n_trunk_layers < 1) return fail("empty branch or trunk");
+    if (d->N < 1 || d->P < 1 || d->K < 1 || d->max_chains < 1) return fail("N, P, K, max_chains must be >= 1");
+    if (int rc = check_lik(d->lik)) return rc;
+    p->kind = 0;
+    p->D = d->n_params;
+    p->K = d->K;
+    p->maxC = d->max_chains;
+    p->lik = d->lik;
+    p->N = d->N;
+    p->P = d->P;
+
+    // ---- layer tables + packed layout --------------------------------------------------------
+    std::vector<int32_t> map_w(p->D, -1), map_wt(p->D, -1);
+    if (p->D < 1) return fail("n_params must be >= 1");
+    map_w[0] = 0;  // scalar output bias b (model.py:26) -> packed slot 0
+    int64_t off = 4;
+    const vihmc_linear* tabs[2] = {d->branch, d->trunk};
+    const int nl[2] = {d->n_branch_layers, d->n_trunk_layers};
+    const int in_w[2] = {d->in_branch, d->in_trunk};
+    const int rows[2] = {d->N, d->P};
+    for (int net = 0; net < 2; ++net) {
+        Net& n = p->nets[net];
+        n.rows = rows[net];
+        n.ld_in = (int)r4(in_w[net]);
+        int prev = in_w[net];
+        for (int j = 0; j < nl[net]; ++j) {
+            const vihmc_linear& l = tabs[net][j];
+            if (l.n_in != prev) return fail("layer fan-in does not match the previous fan-out");
+            if (l.n_out < 1 || l.n_out > 128 || l.n_in < 1 || l.n_in > 128)
+                return fail("layer widths must be in [1, 128]");
+            if (l.act < 0 || l.act > 2 || (j == nl[net] - 1 && l.act != VIHMC_ACT_IDENTITY) ||
+                (j < nl[net] - 1 && l.act == VIHMC_ACT_IDENTITY))
+                return fail("DeepONet layers: tanh/relu hidden activations, identity last layer");
+            if (l.b_off < 0) return fail("DeepONet layers need a bias");
+            LayerPk L{};
+            L.n_out = l.n_out;
+            L.n_in = l.n_in;
+            L.ldi = (int)r4(l.n_in);
+            L.ldo = (int)r4(l.n_out);
+            L.act = l.act;
+            L.wp = off;
+            off += (int64_t)L.n_out * L.ldi;
+            L.bias = off;
+            off += r4(L.n_out);
+            L.wt = off;
+            off += (int64_t)L.n_in * L.ldo;
+            for (int r = 0; r < l.n_out; ++r) {
+                for (int c = 0; c < l.n_in; ++c) {
+                    const int64_t f = l.w_off + (int64_t)r * l.n_in + c;
+                    if (f < 0 || f >= p->D || map_w[f] != -1) return fail("weight offsets overlap or exceed n_params");
+                    map_w[f] = (int32_t)(L.wp + (int64_t)r * L.ldi + c);
+                    map_wt[f] = (int32_t)(L.wt + (int64_t)c * L.ldo + r);
+                }
+                const int64_t fb = l.b_off + r;
+                if (fb < 0 || fb >= p->D || map_w[fb] != -1) return fail("bias offsets overlap or exceed n_params");
+                map_w[fb] = (int32_t)(L.bias + r);
+            }
+            n.L.push_back(L);
+            prev = l.n_out;
+        }
+    }
+    for (int64_t i = 0; i < p->D; ++i)
+        if (map_w[i] < 0) return fail("layer table does not cover parameter " + std::to_string(i));
+    if (p->nets[0].L.back().n_out != p->nets[1].L.back().n_out)
+        return fail("branch and trunk output widths differ");
+    p->W = p->nets[0].L.back().n_out;
+    p->ldz = (int)r4(p->W);
+    p->dp = r64(off);
+    if (p->dp >= (int64_t(1) << 31)) return fail("packed layout too large");
+
+    std::vector<int32_t> sw(p->K), swt(p->K);
+    for (int k = 0; k < p->K; ++k) {
+        const int64_t i = idx[k];
+        if (i < 0 || i >= p->D) return fail("sensitive index out of range");
+        sw[k] = map_w[i];
+        swt[k] = map_wt[i];
+    }
+    if (int rc = p->upload(&p->smap_w, sw.data(), p->K)) return rc;
+    if (int rc = p->upload(&p->smap_wt, swt.data(), p->K)) return rc;
+    if (int rc = prior_setup(p, prior_mu, prior_sd)) return rc;
+
+    const int C = p->maxC;
+    if (int rc = p->alloc(&p->packed, p->dp * C)) return rc;
+    if (int rc = p->alloc(&p->gp, p->dp * C)) return rc;
+    {
+        float* d_frozen = nullptr;
+        int32_t *d_mw = nullptr, *d_mwt = nullptr;
+        std::vector<void*> tmp;
+        HIPCHK(hipMalloc((void**)&d_frozen, p->D * sizeof(float)));
+        HIPCHK(hipMalloc((void**)&d_mw, p->D * sizeof(int32_t)));
+        HIPCHK(hipMalloc((void**)&d_mwt, p->D * sizeof(int32_t)));
+        HIPCHK(hipMemcpy(d_frozen, frozen, p->D * sizeof(float), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d_mw, map_w.data(), p->D * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(d_mwt, map_wt.data(), p->D * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(launch_init_packed(p->packed, p->dp, C, d_frozen, d_mw, d_mwt, p->D, nullptr));
+        HIPCHK(hipDeviceSynchronize());
+        (void)hipFree(d_frozen);
+        (void)hipFree(d_mw);
+        (void)hipFree(d_mwt);
+    }
+
+    // ---- shared inputs ---------------------------------------------------------------------------
+    const float* inputs[2] = {xb, tf};
+    for (int net = 0; net < 2; ++net) {
+        Net& n = p->nets[net];
+        std::vector<float> pad((size_t)n.rows * n.ld_in, 0.f);
+        for (int r = 0; r < n.rows; ++r)
+            std::memcpy(&pad[(size_t)r * n.ld_in], inputs[net] + (size_t)r * in_w[net], in_w[net] * sizeof(float));
+        if (int rc = p->upload(&n.input, pad.data(), (int64_t)pad.size())) return rc;
+    }
+    const int64_t NP = (int64_t)p->N * p->P;
+    if (int rc = p->upload(&p->y, y, NP)) return rc;
+    {
+        std::vector<float> yt((size_t)NP);
+        for (int64_t n = 0; n < p->N; ++n)
+            for (int64_t q = 0; q < p->P; ++q) yt[(size_t)(q * p->N + n)] = y[n * p->P + q];
+        if (int rc = p->upload(&p->yT, yt.data(), NP)) return rc;
+    }
+
+    // ---- per-chain work buffers ---------------------------------------------------------------------
+    for (int net = 0; net < 2; ++net) {
+        Net& n = p->nets[net];
+        int64_t a = 0;
+        int maxld = 0;
+        for (auto& L : n.L) {
+            n.h_off.push_back(a);
+            a += (int64_t)n.rows * L.ldo;
+            maxld = std::max(maxld, L.ldo);
+        }
+        n.act_cs = r64(a);
+        if (int rc = p->alloc(&n.act, n.act_cs * C)) return rc;
+        n.delta_cs = r64((int64_t)n.rows * maxld);
+        for (int b = 0; b < 2; ++b)
+            if (int rc = p->alloc(&n.delta[b], n.delta_cs * C)) return rc;
+        // weight-gradient partial slabs: one per row chunk
+        n.rows_per_chunk = C >= 8 ? 256 : 64;
+        int64_t po = 0;
+        for (auto& L : n.L) {
+            L.n_chunks = cdiv(n.rows, n.rows_per_chunk);
+            L.part_stride = r4((int64_t)L.n_out * L.ldi + L.n_out);
+            L.part_off = po;
+            po += L.part_stride * L.n_chunks;
+        }
+        n.dwpart_cs = r64(po);
+        if (int rc = p->alloc(&n.dwpart, n.dwpart_cs * C)) return rc;
+    }
+    // contraction side B (branch-owner) partials over trunk chunks
+    {
+        const int waves_a = cdiv(p->P, 32), waves_b = cdiv(p->N, 32);
+        int qc = std::max(1, (int)std::lround((double)waves_a / waves_b));
+        p->qperB = (int)(((int64_t)cdiv(p->P, qc) + 15) / 16 * 16);
+        p->qchunksB = cdiv(p->P, p->qperB);
+        p->partB_cs = r64((int64_t)p->qchunksB * p->N * p->ldz);
+        if (int rc = p->alloc(&p->partB, p->partB_cs * C)) return rc;
+        p->nwavesA = waves_a;
+        p->stats_cs = 2 * (int64_t)waves_a;
+        if (int rc = p->alloc(&p->stats, p->stats_cs * C)) return rc;
+        if (int rc = p->alloc(&p->lik_buf, C)) return rc;
+    }
+    // reduce jobs
+    {
+        ReduceJob jb{};
+        jb.src = p->partB;
+        jb.in_cs = p->partB_cs;
+        jb.part_stride = (int64_t)p->N * p->ldz;
+        jb.n_parts = p->qchunksB;
+        jb.len = p->N * p->ldz;
+        jb.dst = p->nets[0].delta[0];
+        jb.dst_cs = p->nets[0].delta_cs;
+        p->lenB = jb.len;
+        if (int rc = p->upload(&p->jobsB, &jb, 1)) return rc;
+        std::vector<ReduceJob> jw;
+        for (int net = 0; net < 2; ++net) {
+            Net& n = p->nets[net];
+            for (auto& L : n.L) {
+                ReduceJob j{};
+                j.src = n.dwpart + L.part_off;
+                j.in_cs = n.dwpart_cs;
+                j.part_stride = L.part_stride;
+                j.n_parts = L.n_chunks;
+                j.len = L.n_out * L.ldi + L.n_out;
+                j.dst = p->gp + L.wp;
+                j.dst_cs = p->dp;
+                p->max_lenW = std::max(p->max_lenW, j.len);
+                jw.push_back(j);
+            }
+        }
+        p->n_jobsW = (int)jw.size();
+        if (int rc = p->upload(&p->jobsW, jw.data(), (int64_t)jw.size())) return rc;
+    }
+    return 0;
+}
+
+inline int nt_of(int n) { return (n + 15) / 16; }
+
+// Forward through both MLPs (grouped launches: branch + trunk layer j together).
+int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
+    const int maxl = (int)std::max(p->nets[0].L.size(), p->nets[1].L.size());
+    for (int j = 0; j < maxl; ++j) {
+        RowdotArgs a{};
+        a.C = C;
+        int nt = 1;
+        int64_t waves32 = 0;
+        for (int net = 0; net < 2; ++net) {
+            Net& n = p->nets[net];
+            if (j < (int)n.L.size()) waves32 += (int64_t)C * cdiv(n.rows, 32);
+        }
+        const int ms = waves32 >= 2048 ? 2 : 1;
+        for (int net = 0; net < 2; ++net) {
+            Net& n = p->nets[net];
+            if (j >= (int)n.L.size()) continue;
+            const LayerPk& L = n.L[j];
+            RowdotProb& q = a.p[a.nprob++];
+            q.A = j == 0 ? n.input : n.act + n.h_off[j - 1];
+            q.a_cs = j == 0 ? 0 : n.act_cs;
+            q.lda = j == 0 ? n.ld_in : n.L[j - 1].ldo;
+            q.B = p->packed + L.wp;
+            q.b_cs = p->dp;
+            q.ldb = L.ldi;
+            q.O = n.act + n.h_off[j];
+            q.o_cs = n.act_cs;
+            q.ldo = L.ldo;
+            q.bias = p->packed + L.bias;
+            q.bias_cs = p->dp;
+            q.M = n.rows;
+            q.Nn = L.n_out;
+            q.K = L.n_in;
+            q.act = L.act;
+            q.tiles = cdiv(n.rows, 16 * ms);
+            nt = std::max(nt, nt_of(L.n_out));
+        }
+        if (a.nprob == 1) a.p[1] = a.p[0];
+        HIPCHK(launch_rowdot(a, nt, ms, MODE_FWD, s));
+    }
+    return 0;
+}
+
+ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
+    Net& b = p->nets[0];
+    Net& t = p->nets[1];
+    ContractProb q{};
+    q.Own = t.act + t.h_off.back();
+    q.own_cs = t.act_cs;
+    q.ldown = p->ldz;
+    q.Q = b.act + b.h_off.back();
+    q.q_cs = b.act_cs;
+    q.ldq = p->ldz;
+    q.Y = p->y;
+    q.ldy = p->P;
+    q.b0 = p->packed;
+    q.b0_cs = p->dp;
+    if (grad) {
+        q.out = t.delta[0];
+        q.out_cs = t.delta_cs;
+        q.ldout = p->ldz;
+    } else {
+        q.out = out ? out : p->lik_buf;   // dummy when not writing S
+        q.out_cs = out ? (int64_t)p->N * p->P : 0;
+        q.ldout = p->P;
+        q.write_s = out ? 1 : 0;
+    }
+    q.out_chunk_stride = 0;
+    q.stats = p->stats;
+    q.stats_cs = p->stats_cs;
+    q.Mo = p->P;
+    q.Mq = p->N;
+    q.W = p->W;
+    q.o_tiles = cdiv(p->P, 32);
+    q.q_chunks = 1;
+    q.q_per_chunk = p->N;
+    q.with_stats = 1;
+    const float v = std::max(p->lik.tau_out, 1e-6f);
+    q.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
+    (void)C;
+    return q;
+}
+
+int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out, hipStream_t s) {
+    if (C < 1 || C > p->maxC) return fail("C must be in [1, max_chains]");
+    HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s));
+    if (int rc = deeponet_forward_layers(p, C, s)) return rc;
+    const bool want_grad = grad != nullptr && out == nullptr;
+    {
+        ContractProb a = side_a(p, C, want_grad, out);
+        hipEvent_t stop = nullptr;
+        if (int rc = p->timing_begin(0, s, &stop)) return rc;
+        HIPCHK(launch_contract(a, C, want_grad, s));
+        if (stop) HIPCHK(hipEventRecord(stop, s));
+    }
+    HIPCHK(launch_contract_stats(p->stats, p->stats_cs, p->nwavesA, C, p->lik_buf, p->gp, p->dp,
+                                 (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out, s));
+    if (want_grad) {
+        Net& b = p->nets[0];
+        Net& t = p->nets[1];
+        ContractProb q{};
+        q.Own = b.act + b.h_off.back();
+        q.own_cs = b.act_cs;
+        q.ldown = p->ldz;
+        q.Q = t.act + t.h_off.back();
+        q.q_cs = t.act_cs;
+        q.ldq = p->ldz;
+        q.Y = p->yT;
+        q.ldy = p->N;
+        q.b0 = p->packed;
+        q.b0_cs = p->dp;
+        q.out = p->partB;
+        q.out_cs = p->partB_cs;
+        q.ldout = p->ldz;
+        q.out_chunk_stride = (int64_t)p->N * p->ldz;
+        q.stats = p->stats;
+        q.Mo = p->N;
+        q.Mq = p->P;
+        q.W = p->W;
+        q.o_tiles = cdiv(p->N, 32);
+        q.q_chunks = p->qchunksB;
+        q.q_per_chunk = p->qperB;
+        q.with_stats = 0;
+        const float v = std::max(p->lik.tau_out, 1e-6f);
+        q.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
+        hipEvent_t stop = nullptr;
+        if (int rc = p->timing_begin(1, s, &stop)) return rc;
+        HIPCHK(launch_contract(q, C, true, s));
+        if (stop) HIPCHK(hipEventRecord(stop, s));
+        HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s));
+
+        // backward through both MLPs, last layer first
+        int cur[2] = {0, 0};
+        const int maxl = (int)std::max(b.L.size(), t.L.size());
+        for (int i = 0; i < maxl; ++i) {
+            ColsumArgs ca{};
+            ca.C = C;
+            RowdotArgs ra{};
+            ra.C = C;
+            int jt = 1, nt = 1;
+            int64_t waves32 = 0;
+            for (int net = 0; net < 2; ++net) {
+                Net& n = p->nets[net];
+                const int j = (int)n.L.size() - 1 - i;
+                if (j >= 1) waves32 += (int64_t)C * cdiv(n.rows, 32);
+            }
+            const int ms = waves32 >= 2048 ? 2 : 1;
+            for (int net = 0; net < 2; ++net) {
+                Net& n = p->nets[net];
+                const int j = (int)n.L.size() - 1 - i;
+                if (j < 0) continue;
+                const LayerPk& L = n.L[j];
+                ColsumProb& c = ca.p[ca.nprob++];
+                c.D = n.delta[cur[net]];
+                c.d_cs = n.delta_cs;
+                c.ldd = L.ldo;
+                c.H = j == 0 ? n.input : n.act + n.h_off[j - 1];
+                c.h_cs = j == 0 ? 0 : n.act_cs;
+                c.ldh = L.ldi;
+                c.part = n.dwpart + L.part_off;
+                c.part_cs = n.dwpart_cs;
+                c.M = n.rows;
+                c.n_out = L.n_out;
+                c.n_in = L.n_in;
+                c.rows_per_chunk = n.rows_per_chunk;
+                c.n_chunks = L.n_chunks;
+                c.n_pairs = cdiv(L.n_out, 32);
+                c.part_stride = (int32_t)L.part_stride;
+                jt = std::max(jt, nt_of(L.n_in));
+                if (j >= 1) {
+                    const LayerPk& Lp = n.L[j - 1];
+                    RowdotProb& r = ra.p[ra.nprob++];
+                    r.A = n.delta[cur[net]];
+                    r.a_cs = n.delta_cs;
+                    r.lda = L.ldo;
+                    r.B = p->packed + L.wt;
+                    r.b_cs = p->dp;
+                    r.ldb = L.ldo;
+                    r.O = n.delta[cur[net] ^ 1];
+                    r.o_cs = n.delta_cs;
+                    r.ldo = Lp.ldo;
+                    r.H = n.act + n.h_off[j - 1];
+                    r.h_cs = n.act_cs;
+                    r.ldh = Lp.ldo;
+                    r.M = n.rows;
+                    r.Nn = L.n_in;
+                    r.K = L.n_out;
+                    r.act = Lp.act;
+                    r.tiles = cdiv(n.rows, 16 * ms);
+                    nt = std::max(nt, nt_of(L.n_in));
+                }
+            }
+            if (ca.nprob == 1) ca.p[1] = ca.p[0];
+            HIPCHK(launch_colsum(ca, jt, s));
+            if (ra.nprob > 0) {
+                if (ra.nprob == 1) ra.p[1] = ra.p[0];
+                HIPCHK(launch_rowdot(ra, nt, ms, MODE_BWD, s));
+            }
+            for (int net = 0; net < 2; ++net) {
+                const int j = (int)p->nets[net].L.size() - 1 - i;
+                if (j >= 1) cur[net] ^= 1;
+            }
+        }
+        HIPCHK(launch_reduce(p->jobsW, p->n_jobsW, p->max_lenW, C, s));
+    }
+    HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
+                               p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, s));
+    return 0;
+}
+
+int build_mlp(vihmc_plan* p, const vihmc_mlp_desc* d, const float* x, const float* y, const float* frozen,
+              const int64_t* idx, const float* prior_mu, const float* prior_sd) {
+    if (d->n_layers < 2 || d->n_layers > 6) return fail("MLP plan supports 2..6 linear layers");
+    if (d->N < 1 || d->K < 1 || d->max_chains < 1 || d->n_params < 1) return fail("N, K, D, max_chains must be >= 1");
+    if (int rc = check_lik(d->lik)) return rc;
+    p->kind = 1;
+    p->D = d->n_params;
+    p->K = d->K;
+    p->maxC = d->max_chains;
+    p->lik = d->lik;
+    MlpArgs& a = p->mlp;
+    a.n_layers = d->n_layers;
+    a.D = (int32_t)d->n_params;
+    a.K = d->K;
+    a.N = d->N;
+    a.in_dim = d->in_dim;
+    a.out_dim = d->out_dim;
+    int prev = d->in_dim, maxw = std::max(d->in_dim, d->out_dim);
+    std::vector<int> cover(p->D, 0);
+    for (int j = 0; j < d->n_layers; ++j) {
+        const vihmc_linear& l = d->layers[j];
+        if (l.n_in != prev) return fail("layer fan-in does not match the previous fan-out");
+        if (l.act < 0 || l.act > 3) return fail("bad activation code");
+        a.L[j] = MlpLayer{(int32_t)l.w_off, (int32_t)l.b_off, l.n_out, l.n_in, l.act};
+        for (int64_t f = l.w_off; f < l.w_off + (int64_t)l.n_out * l.n_in; ++f) {
+            if (f < 0 || f >= p->D) return fail("weight offsets exceed n_params");
+            cover[f]++;
+        }
+        if (l.b_off >= 0)
+            for (int64_t f = l.b_off; f < l.b_off + l.n_out; ++f) {
+                if (f >= p->D) return fail("bias offsets exceed n_params");
+                cover[f]++;
+            }
+        maxw = std::max(maxw, std::max(l.n_out, l.n_in));
+        prev = l.n_out;
+    }
+    if (prev != d->out_dim) return fail("last layer fan-out != out_dim");
+    for (int64_t i = 0; i < p->D; ++i)
+        if (cover[i] != 1) return fail("layer table must cover every parameter exactly once");
+    if (mlp_lds_bytes((int)p->D, d->n_layers, maxw) > 160 * 1024)
+        return fail("MLP plan keeps weights and per-row activations in LDS: D and widths too large for 160 KiB");
+    p->maxw = maxw;
+    std::vector<int32_t> idx32(p->K);
+    for (int k = 0; k < p->K; ++k) {
+        if (idx[k] < 0 || idx[k] >= p->D) return fail("sensitive index out of range");
+        idx32[k] = (int32_t)idx[k];
+    }
+    float *dx, *dy, *dfz;
+    int32_t* didx;
+    if (int rc = p->upload(&dx, x, (int64_t)d->N * d->in_dim)) return rc;
+    if (int rc = p->upload(&dy, y, (int64_t)d->N * d->out_dim)) return rc;
+    if (int rc = p->upload(&dfz, frozen, p->D)) return rc;
+    if (int rc = p->upload(&didx, idx32.data(), p->K)) return rc;
+    if (int rc = prior_setup(p, prior_mu, prior_sd)) return rc;
+    a.x = dx;
+    a.y = dy;
+    a.frozen = dfz;
+    a.idx = didx;
+    a.prior_mu = p->prior_mu;
+    a.prior_inv_var = p->prior_iv;
+    a.prior_const = p->prior_const;
+    a.prior_scale = p->lik.prior_scale;
+    a.loss = p->lik.loss;
+    a.tau_out = p->lik.tau_out;
+    return 0;
+}
+
+int mlp_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out, hipStream_t s) {
+    if (C < 1 || C > p->maxC) return fail("C must be in [1, max_chains]");
+    MlpArgs a = p->mlp;
+    a.theta = theta;
+    a.logp = logp;
+    a.grad = grad;
+    a.out = out;
+    hipEvent_t stop = nullptr;
+    if (int rc = p->timing_begin(0, s, &stop)) return rc;
+    HIPCHK(launch_mlp(a, C, p->maxw, s));
+    if (stop) HIPCHK(hipEventRecord(stop, s));
+    return 0;
+}
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::exception& e) {
+        return fail(std::string("exception: ") + e.what());
+    } catch (...) {
+        return fail("unknown exception");
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int vihmc_deeponet_plan_create(vihmc_plan** out, const vihmc_deeponet_desc* d, const float* x_branch,
+                               const float* trunk_feat, const float* y, const float* frozen, const int64_t* sens_idx,
+                               const float* prior_mu, const float* prior_sd, int device) {
+    return guarded([&]() -> int {
+        if (!out || !d || !x_branch || !trunk_feat || !y || !frozen || !sens_idx || !prior_mu || !prior_sd)
+            return fail("null argument");
+        *out = nullptr;
+        HIPCHK(hipSetDevice(device));
+        auto* p = new vihmc_plan();
+        p->device = device;
+        if (int rc = build_deeponet(p, d, x_branch, trunk_feat, y, frozen, sens_idx, prior_mu, prior_sd)) {
+            delete p;
+            return rc;
+        }
+        *out = p;
+        return 0;
+    });
+}
+
+int vihmc_mlp_plan_create(vihmc_plan** out, const vihmc_mlp_desc* d, const float* x, const float* y,
+                          const float* frozen, const int64_t* sens_idx, const float* prior_mu, const float* prior_sd,
+                          int device) {
+    return guarded([&]() -> int {
+        if (!out || !d || !x || !y || !frozen || !sens_idx || !prior_mu || !prior_sd || !d->layers)
+            return fail("null argument");
+        *out = nullptr;
+        HIPCHK(hipSetDevice(device));
+        auto* p = new vihmc_plan();
+        p->device = device;
+        if (int rc = build_mlp(p, d, x, y, frozen, sens_idx, prior_mu, prior_sd)) {
+            delete p;
+            return rc;
+        }
+        *out = p;
+        return 0;
+    });
+}
+
+int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, void* stream) {
+    return guarded([&]() -> int {
+        if (!p || !theta || !logp) return fail("null argument");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        return p->kind == 0 ? deeponet_eval(p, theta, C, logp, grad, nullptr, s)
+                            : mlp_eval(p, theta, C, logp, grad, nullptr, s);
+    });
+}
+
+int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* out, void* stream) {
+    return guarded([&]() -> int {
+        if (!p || !theta || !logp || !out) return fail("null argument");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        return p->kind == 0 ? deeponet_eval(p, theta, C, logp, nullptr, out, s)
+                            : mlp_eval(p, theta, C, logp, nullptr, out, s);
+    });
+}
+
+int vihmc_plan_kind(const vihmc_plan* p) { return p ? p->kind : -1; }
+int64_t vihmc_plan_n_params(const vihmc_plan* p) { return p ? p->D : -1; }
+int vihmc_plan_K(const vihmc_plan* p) { return p ? p->K : -1; }
+int vihmc_plan_max_chains(const vihmc_plan* p) { return p ? p->maxC : -1; }
+int64_t vihmc_plan_device_bytes(const vihmc_plan* p) { return p ? p->bytes : -1; }
+
+int vihmc_timing_enable(vihmc_plan* p, int which, int on) {
+    if (!p) return fail("null plan");
+    p->timing_on = on;
+    p->timing_which = which;
+    p->ev_used = 0;
+    return 0;
+}
+
+int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches) {
+    if (!p || !total_ms || !launches) return fail("null argument");
+    double t = 0.0;
+    for (size_t i = 0; i + 1 < p->ev_used; i += 2) {
+        HIPCHK(hipEventSynchronize(p->ev_pool[i + 1]));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, p->ev_pool[i], p->ev_pool[i + 1]));
+        t += ms;
+    }
+    *total_ms = t;
+    *launches = (int64_t)(p->ev_used / 2);
+    p->ev_used = 0;
+    return 0;
+}
+
+void vihmc_plan_destroy(vihmc_plan* p) { delete p; }
+const char* vihmc_last_error(void) { return g_err.c_str(); }
+const char* vihmc_version(void) { return "vihmc 0.1.0 gfx950"; }
+
+}  // extern "C"

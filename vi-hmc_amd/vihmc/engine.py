@@ -1,0 +1,224 @@
+"""Batched log-posterior + gradient engines over libvihmc.so plans.
+
+These are the MI355X replacement of the reference's ``log_prob_func`` + ``torch.autograd.grad``
+pair (Operator_network/VI_HMC/main_VI_HMC_burgers.py:86-178; Neural_network/VI_HMC/
+main_VI_HMC.py:96-151): one call evaluates C chains, theta [C, K] -> (logp [C], grad [C, K]), all
+device-resident, enqueued on torch's current HIP stream with no host synchronisation.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .layout import DeepONetSpec, MLPSpec
+
+LOSS_CODES = {"NLL": 0, "regression": 1}
+
+
+def _c32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _linears(layers) -> ctypes.Array:
+    arr = (_lib.Linear * len(layers))()
+    for i, l in enumerate(layers):
+        arr[i].w_off, arr[i].b_off, arr[i].n_out, arr[i].n_in, arr[i].act = l.w_off, l.b_off, l.n_out, l.n_in, l.act
+    return arr
+
+
+def _lik(loss: str, tau_out: float, prior_scale: float) -> _lib.LikDesc:
+    if loss not in LOSS_CODES:
+        raise NotImplementedError(f"loss {loss!r}: the hot path implements 'NLL' and 'regression'")
+    return _lib.LikDesc(LOSS_CODES[loss], float(tau_out), float(prior_scale), 0)
+
+
+class _Engine:
+    kind = "?"
+
+    def __init__(self, device):
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise RuntimeError("vihmc engines run on a HIP device (torch 'cuda'); there is no CPU fallback")
+        if not torch.cuda.is_available():
+            raise RuntimeError("no HIP device visible: the vihmc engine has no CPU fallback")
+        self.device = torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+        self._plan = ctypes.c_void_p()
+        self.L = _lib.lib()
+
+    # ---- plan lifetime ---------------------------------------------------------------------------
+    def _created(self, rc, what):
+        _lib.check(rc, what)
+        self.K = self.L.vihmc_plan_K(self._plan)
+        self.D = self.L.vihmc_plan_n_params(self._plan)
+        self.max_chains = self.L.vihmc_plan_max_chains(self._plan)
+        self.device_bytes = self.L.vihmc_plan_device_bytes(self._plan)
+
+    def close(self):
+        if getattr(self, "_plan", None) and self._plan.value:
+            self.L.vihmc_plan_destroy(self._plan)
+            self._plan = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- evaluation ------------------------------------------------------------------------------
+    def _theta(self, theta: torch.Tensor) -> torch.Tensor:
+        if theta.dim() == 1:
+            theta = theta.unsqueeze(0)
+        if theta.dim() != 2 or theta.shape[1] != self.K:
+            raise ValueError(f"theta must be [C, {self.K}] (got {tuple(theta.shape)})")
+        if theta.shape[0] > self.max_chains:
+            raise ValueError(f"C={theta.shape[0]} exceeds the plan's max_chains={self.max_chains}")
+        return theta.to(device=self.device, dtype=torch.float32).contiguous()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def logp_grad(self, theta: torch.Tensor, logp: Optional[torch.Tensor] = None,
+                  grad: Optional[torch.Tensor] = None):
+        """theta [C, K] -> (logp [C], grad [C, K]) on the engine's device."""
+        th = self._theta(theta)
+        C = th.shape[0]
+        if logp is None:
+            logp = torch.empty(C, device=self.device, dtype=torch.float32)
+        if grad is None:
+            grad = torch.empty(C, self.K, device=self.device, dtype=torch.float32)
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_logp_grad(self._plan, th.data_ptr(), C, logp.data_ptr(), grad.data_ptr(), self._stream())
+        _lib.check(rc, "vihmc_logp_grad")
+        return logp, grad
+
+    def logp(self, theta: torch.Tensor, logp: Optional[torch.Tensor] = None) -> torch.Tensor:
+        th = self._theta(theta)
+        C = th.shape[0]
+        if logp is None:
+            logp = torch.empty(C, device=self.device, dtype=torch.float32)
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_logp_grad(self._plan, th.data_ptr(), C, logp.data_ptr(), None, self._stream())
+        _lib.check(rc, "vihmc_logp_grad(value)")
+        return logp
+
+    def forward(self, theta: torch.Tensor):
+        """theta [C, K] -> (logp [C], network output [C, *out_shape])."""
+        th = self._theta(theta)
+        C = th.shape[0]
+        logp = torch.empty(C, device=self.device, dtype=torch.float32)
+        out = torch.empty((C,) + tuple(self.out_shape), device=self.device, dtype=torch.float32)
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_forward(self._plan, th.data_ptr(), C, logp.data_ptr(), out.data_ptr(), self._stream())
+        _lib.check(rc, "vihmc_forward")
+        return logp, out
+
+    # ---- kernel timing hook (roofline) -----------------------------------------------------------
+    def timing(self, which: int = 0, on: bool = True):
+        _lib.check(self.L.vihmc_timing_enable(self._plan, which, int(on)), "vihmc_timing_enable")
+
+    def timing_read(self):
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(self.L.vihmc_timing_read(self._plan, ctypes.byref(ms), ctypes.byref(n)), "vihmc_timing_read")
+        return ms.value, n.value
+
+
+def expand_prior(K: int, mu, sd) -> (np.ndarray, np.ndarray):
+    mu = np.broadcast_to(np.asarray(mu, np.float32), (K,)).copy()
+    sd = np.broadcast_to(np.asarray(sd, np.float32), (K,)).copy()
+    return mu, sd
+
+
+class DeepONetEngine(_Engine):
+    """DeepONet VI-HMC / full-HMC log-posterior (Functional_DeepONet + GaussianNLL + Normal prior)."""
+    kind = "deeponet"
+
+    def __init__(self, spec: DeepONetSpec, branch_in, trunk_feat, y, frozen, grad_ind, prior_mu=0.0, prior_sd=0.1,
+                 loss: str = "NLL", tau_out: float = 1.0, prior_scale: float = 1.0, max_chains: int = 1,
+                 device="cuda"):
+        super().__init__(device)
+        xb = _c32(branch_in).reshape(-1, spec.in_branch)
+        tf = _c32(trunk_feat).reshape(-1, spec.in_trunk)
+        yy = _c32(y)
+        N, P = xb.shape[0], tf.shape[0]
+        if yy.shape != (N, P):
+            raise ValueError(f"y must be [N={N}, P={P}] (got {yy.shape})")  # reference: assert at :144
+        fz = _c32(frozen).reshape(-1)
+        if fz.shape[0] != spec.n_params:
+            raise ValueError(f"frozen vector must have D={spec.n_params} entries")
+        idx = np.ascontiguousarray(np.asarray(grad_ind, dtype=np.int64).reshape(-1))
+        K = idx.shape[0]
+        pm, ps = expand_prior(K, prior_mu, prior_sd)
+        self.spec, self.N, self.P = spec, N, P
+        self.out_shape = (N, P)
+        self.grad_ind = idx
+        self._keep = (_linears(spec.branch), _linears(spec.trunk))
+        d = _lib.DeepONetDesc(len(spec.branch), len(spec.trunk), self._keep[0], self._keep[1], spec.n_params, N, P,
+                              spec.in_branch, spec.in_trunk, K, int(max_chains), _lik(loss, tau_out, prior_scale))
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_deeponet_plan_create(ctypes.byref(self._plan), ctypes.byref(d), _lib.fptr(xb),
+                                                   _lib.fptr(tf), _lib.fptr(yy), _lib.fptr(fz), _lib.iptr(idx),
+                                                   _lib.fptr(pm), _lib.fptr(ps), self.device.index)
+        self._created(rc, "vihmc_deeponet_plan_create")
+
+
+class MLPEngine(_Engine):
+    """BNN regression log-posterior (Functional_Net + NLL/regression likelihood + Normal prior)."""
+    kind = "mlp"
+
+    def __init__(self, spec: MLPSpec, x, y, frozen, grad_ind, prior_mu=0.0, prior_sd=1.0, loss: str = "NLL",
+                 tau_out: float = 0.0025, prior_scale: float = 1.0, max_chains: int = 1, device="cuda"):
+        super().__init__(device)
+        xx = _c32(x).reshape(-1, spec.in_dim)
+        yy = _c32(y).reshape(-1, spec.out_dim)
+        N = xx.shape[0]
+        if yy.shape[0] != N:
+            raise ValueError("x and y row counts differ")
+        fz = _c32(frozen).reshape(-1)
+        if fz.shape[0] != spec.n_params:
+            raise ValueError(f"frozen vector must have D={spec.n_params} entries")
+        idx = np.ascontiguousarray(np.asarray(grad_ind, dtype=np.int64).reshape(-1))
+        K = idx.shape[0]
+        pm, ps = expand_prior(K, prior_mu, prior_sd)
+        self.spec, self.N = spec, N
+        self.out_shape = (N, spec.out_dim)
+        self.grad_ind = idx
+        self._keep = _linears(spec.layers)
+        d = _lib.MLPDesc(len(spec.layers), 0, self._keep, spec.n_params, N, spec.in_dim, spec.out_dim, K,
+                         int(max_chains), 0, _lik(loss, tau_out, prior_scale))
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_mlp_plan_create(ctypes.byref(self._plan), ctypes.byref(d), _lib.fptr(xx), _lib.fptr(yy),
+                                              _lib.fptr(fz), _lib.iptr(idx), _lib.fptr(pm), _lib.fptr(ps),
+                                              self.device.index)
+        self._created(rc, "vihmc_mlp_plan_create")
+
+
+def trunk_features(trunk_in) -> np.ndarray:
+    """Trunk feature map computed with torch fp32 CPU ops exactly as the reference does
+    (Operator_network/VI_HMC/my_make_func.py:33-36,63-65): [t, sin2πx, sin4πx, cos2πx, cos4πx].
+    theta-independent, so it is evaluated once per plan."""
+    x2 = torch.as_tensor(np.asarray(trunk_in, dtype=np.float32))
+    if x2.dim() == 2:
+        x2 = x2.unsqueeze(0)
+    xs = x2[:, :, 1]
+    x_bc = torch.stack([torch.sin(2 * np.pi * xs), torch.sin(4 * np.pi * xs), torch.cos(2 * np.pi * xs),
+                        torch.cos(4 * np.pi * xs)], dim=2)
+    x_bc = torch.cat([x2[:, :, 0].unsqueeze(dim=2), x_bc], dim=2)
+    return x_bc[0].numpy()
+
+
+def prior_per_tensor(tensor_sizes: Sequence[int], K: int, stds: Sequence[float]) -> np.ndarray:
+    """Per-sampled-parameter prior std reproducing the reference's per-tensor slicing of the K-vector
+    (Neural_network/VI_HMC/main_VI_HMC.py:107-112: ``w = params[i_prev:index+i_prev]`` walks the
+    *sampled* vector with the full model's tensor sizes)."""
+    sd = np.empty(K, np.float32)
+    i = 0
+    for n, s in zip(tensor_sizes, stds):
+        sd[i:i + n] = s
+        i += n
+        if i >= K:
+            break
+    return sd
