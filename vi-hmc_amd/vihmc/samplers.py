@@ -1,0 +1,415 @@
+"""hamiltorch-compatible HMC sampler, batched over chains and resident on the GPU.
+
+The reference hands a scalar ``log_prob_func`` to the un-vendored ``hamiltorch.samplers.sample``
+(call sites: Operator_network/VI_HMC/main_VI_HMC_burgers.py:286-287,
+Neural_network/VI_HMC/main_VI_HMC.py:379-380, Operator_network/HMC/main_HMC_splitting.py:361-369).
+This module keeps that algorithm -- Gibbs momentum, leapfrog (or Neal's split integrator), Metropolis
+accept, the dual-averaging step size of ``Sampler.HMC_NUTS`` -- and its exact bookkeeping (what is
+stored during / after burn, what a rejection reverts to, ``LogProbError`` = non-finite log-prob =>
+reject without storing), restated in SURVEY.md Appendix A and oracle/hamiltorch_ref.py, but runs C
+chains at once:
+
+* state (theta, logp, grad) lives in [C, K] device tensors; the accept decision is a device-side
+  ``torch.where``, so there is no host synchronisation per sample (except during NUTS burn-in, where
+  the step-size adaptation is host arithmetic per chain, as in hamiltorch);
+* momenta and accept uniforms come from one CPU ``torch.Generator`` per chain (seeded per chain, so a
+  chain's draws do not depend on how chains are sharded over GPUs), drawn in hamiltorch's order
+  (normal(K) then rand(1)); ``rng="global"`` reproduces hamiltorch's use of the global generators;
+* the gradient at the start of a trajectory is the one computed at its end point by the previous
+  trajectory (or at the revert target), which the deterministic HIP engine makes bit-identical to a
+  recomputation: L gradient evaluations per sample instead of hamiltorch's L+1 (reuse_endpoint_grad).
+
+Elementwise updates use the same op sequence as hamiltorch (``p = p + fp32(eps)*g`` as a separate
+multiply and add, no fused FMA), so trajectories match the oracle to the engine's fp32 tolerance.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from enum import Enum
+from typing import Callable, List, Optional, Sequence, Union
+
+import torch
+
+
+class Sampler(Enum):
+    HMC = 1
+    RMHMC = 2
+    HMC_NUTS = 3
+
+
+class Integrator(Enum):
+    EXPLICIT = 1
+    IMPLICIT = 2
+    S3 = 3
+    SPLITTING = 4
+    SPLITTING_RAND = 5
+    SPLITTING_KMID = 6
+
+
+class LogProbError(Exception):
+    """Non-finite log-probability (reference util.py:107-119); the sampler treats it as a rejection."""
+
+
+# ------------------------------------------------------------------------------------------------
+# evaluators: theta [C, K] -> (logp [C], grad [C, K])
+# ------------------------------------------------------------------------------------------------
+class EngineEvaluator:
+    """Batched HIP engine (vihmc.engine.*Engine)."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        self.K = engine.K
+        self.device = engine.device
+        self.n_grad = 0
+        self.n_value = 0
+
+    def logp_grad(self, theta):
+        self.n_grad += theta.shape[0]
+        return self.engine.logp_grad(theta)
+
+    def logp(self, theta):
+        self.n_value += theta.shape[0]
+        return self.engine.logp(theta)
+
+
+class AutogradEvaluator:
+    """Any scalar torch closure ``f(params[K]) -> logp`` (the reference's own contract), one chain
+    at a time through torch.autograd -- the generic fallback for user-defined log-probs."""
+
+    def __init__(self, fn: Callable, K: int, device):
+        self.fn, self.K, self.device = fn, K, torch.device(device)
+        self.n_grad = 0
+        self.n_value = 0
+
+    def logp_grad(self, theta):
+        lps, gs = [], []
+        for c in range(theta.shape[0]):
+            p = theta[c].detach().clone().requires_grad_()
+            lp = self.fn(p)
+            lp = lp.sum() if lp.dim() else lp
+            g, = torch.autograd.grad(lp, p)
+            lps.append(lp.detach().reshape(()))
+            gs.append(g)
+        self.n_grad += theta.shape[0]
+        return torch.stack(lps).to(torch.float32), torch.stack(gs).to(torch.float32)
+
+    def logp(self, theta):
+        with torch.no_grad():
+            out = torch.stack([self.fn(theta[c]).sum().reshape(()) for c in range(theta.shape[0])])
+        self.n_value += theta.shape[0]
+        return out.to(torch.float32)
+
+
+def evaluator_for(log_prob_func, K: int, device) -> Union[EngineEvaluator, AutogradEvaluator]:
+    eng = getattr(log_prob_func, "_vihmc_engine", None)
+    if eng is not None:
+        return EngineEvaluator(eng)
+    return AutogradEvaluator(log_prob_func, K, device)
+
+
+# ------------------------------------------------------------------------------------------------
+# random streams
+# ------------------------------------------------------------------------------------------------
+class ChainRNG:
+    """Momentum (standard normal [C, K]) and log-uniform [C] draws, in hamiltorch's call order."""
+
+    def __init__(self, C: int, K: int, device, seeds: Optional[Sequence[int]] = None, mode: str = "per_chain"):
+        self.C, self.K, self.device, self.mode = C, K, torch.device(device), mode
+        if mode == "global":
+            if C != 1:
+                raise ValueError("rng='global' reproduces hamiltorch's single-chain global-generator stream; C must be 1")
+        elif mode == "per_chain":
+            if seeds is None or len(seeds) != C:
+                raise ValueError("rng='per_chain' needs one seed per chain")
+            self.gens = [torch.Generator().manual_seed(int(s)) for s in seeds]
+            self._zeros = torch.zeros(K)
+            self._ones = torch.ones(K)
+        else:
+            raise ValueError(f"unknown rng mode {mode!r}")
+        self._pin = self.device.type == "cuda"
+
+    def draw_momentum(self) -> torch.Tensor:
+        """Standard-normal momenta [C, K] on the device (hamiltorch gibbs)."""
+        if self.mode == "global":
+            return torch.normal(torch.zeros(self.K, device=self.device), torch.ones(self.K, device=self.device))[None]
+        z = torch.empty(self.C, self.K, pin_memory=self._pin)
+        for c, g in enumerate(self.gens):
+            torch.normal(self._zeros, self._ones, generator=g, out=z[c])
+        return z.to(self.device, non_blocking=True)
+
+    def draw_logu(self, mask=None) -> torch.Tensor:
+        """log(torch.rand(1)) per chain on the device (hamiltorch's accept draw, computed on the CPU);
+        chains with mask[c] False do not consume their stream (value -inf)."""
+        if self.mode == "global":
+            return torch.log(torch.rand(1)).to(self.device)
+        lu = torch.full((self.C,), float("-inf"), pin_memory=self._pin)
+        for c, g in enumerate(self.gens):
+            if mask is None or mask[c]:
+                lu[c] = torch.log(torch.rand(1, generator=g))[0]
+        return lu.to(self.device, non_blocking=True)
+
+    def draw(self):
+        z = self.draw_momentum()
+        return z, self.draw_logu()
+
+
+# ------------------------------------------------------------------------------------------------
+# dual averaging (hamiltorch adaptation, host arithmetic per chain)
+# ------------------------------------------------------------------------------------------------
+def adaptation(rho, t, step_size_init, H_t, eps_bar, desired_accept_rate=0.8):
+    t = t + 1
+    r = torch.tensor([rho])
+    if bool(torch.isnan(r).any()) or bool(torch.isinf(r).any()):
+        alpha = 0
+    else:
+        alpha = min(1., float(torch.exp(torch.FloatTensor([rho]))))
+    mu = float(torch.log(10 * torch.FloatTensor([step_size_init])))
+    gamma, t0, kappa = 0.05, 10, 0.75
+    H_t = (1 - (1 / (t + t0))) * H_t + (1 / (t + t0)) * (desired_accept_rate - alpha)
+    x_new = mu - (t ** 0.5) / gamma * H_t
+    step_size = float(torch.exp(torch.FloatTensor([x_new])))
+    x_new_bar = t ** -kappa * x_new + (1 - t ** -kappa) * torch.log(torch.FloatTensor([eps_bar]))
+    eps_bar = float(torch.exp(x_new_bar))
+    return step_size, eps_bar, H_t
+
+
+# ------------------------------------------------------------------------------------------------
+# batched chains
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class ChainResult:
+    samples: torch.Tensor          # [C, S_cap, K] (rows >= counts[c] are unused)
+    counts: torch.Tensor           # [C] number of stored samples per chain (hamiltorch's len(ret_params))
+    accepted: torch.Tensor         # [C, num_samples] bool
+    logp_trace: torch.Tensor       # [C, num_samples] log-prob of the chain state after each iteration
+    step_size: List[float]         # final step size per chain
+    n_grad_evals: int = 0          # chain-gradient evaluations actually performed
+    n_value_evals: int = 0
+    extra: dict = field(default_factory=dict)
+
+    def chain(self, c: int) -> List[torch.Tensor]:
+        """hamiltorch's return format for chain c: a list of [K] tensors."""
+        return list(self.samples[c, :int(self.counts[c])].unbind(0))
+
+    def stacked(self) -> torch.Tensor:
+        """[C, S, K] when every chain stored the same number of samples."""
+        n = int(self.counts.min())
+        if int(self.counts.max()) != n:
+            raise RuntimeError("chains stored different numbers of samples (LogProbError rejections)")
+        return self.samples[:, :n]
+
+
+def _kinetic(p, inv_mass):
+    return 0.5 * (p * p).sum(1) if inv_mass is None else 0.5 * (p * (inv_mass * p)).sum(1)
+
+
+class HMCRunner:
+    """C independent chains from theta0 [C, K], advanced one HMC iteration per ``step()``.
+
+    ``evaluators`` is one evaluator, or a list of per-shard evaluators for ``Integrator.SPLITTING``
+    (each closure already divides its prior by prior_scale, as define_split_model_log_prob does).
+
+    RNG order: hamiltorch draws the accept uniform only when both Hamiltonians are finite (a
+    ``LogProbError`` skips it). ``strict_rng=True`` reproduces that exactly at the price of one host
+    synchronisation per sample; the default draws every chain's uniform up front (identical streams
+    whenever no log-prob is non-finite) so the whole iteration stays on the device.
+    """
+
+    def __init__(self, evaluators, theta0: torch.Tensor, num_samples: int, num_steps_per_sample: int, step_size,
+                 burn: int = 0, inv_mass: Optional[torch.Tensor] = None, sampler: Sampler = Sampler.HMC,
+                 integrator: Integrator = Integrator.IMPLICIT, desired_accept_rate: float = 0.8,
+                 rng: Optional[ChainRNG] = None, seeds: Optional[Sequence[int]] = None,
+                 reuse_endpoint_grad: bool = True, store: bool = True, strict_rng: bool = False):
+        evs = list(evaluators) if isinstance(evaluators, (list, tuple)) else [evaluators]
+        self.splitting = integrator == Integrator.SPLITTING
+        if self.splitting and len(evs) < 2:
+            raise RuntimeError("For splitting log_prob_func must be list of functions")
+        if not self.splitting and len(evs) != 1:
+            raise RuntimeError("a list of log_prob_funcs needs Integrator.SPLITTING")
+        if sampler == Sampler.RMHMC:
+            raise NotImplementedError("RMHMC is not on the VI-HMC path (no reference call site)")
+        if burn >= num_samples:
+            raise RuntimeError("burn must be less than num_samples.")
+        self.nuts = sampler == Sampler.HMC_NUTS
+        if self.nuts and burn == 0:
+            raise RuntimeError("burn must be greater than 0 for NUTS.")
+        self.evs = evs
+        self.device = device = evs[0].device
+        theta = theta0.to(device=device, dtype=torch.float32).contiguous().clone()
+        if theta.dim() == 1:
+            theta = theta[None]
+        self.C, self.K = C, K = theta.shape
+        self.rng = rng if rng is not None else ChainRNG(C, K, device, seeds if seeds is not None else list(range(C)))
+        self.L, self.M = int(num_steps_per_sample), len(evs)
+        self.num_samples, self.burn = num_samples, burn
+        self.reuse, self.store, self.strict = reuse_endpoint_grad, store, strict_rng
+        self.desired_accept_rate = desired_accept_rate
+        self.inv_mass = self.mass_sqrt = None
+        if inv_mass is not None:
+            self.inv_mass = inv_mass.to(device=device, dtype=torch.float32)
+            if self.inv_mass.dim() != 1:
+                raise NotImplementedError("only a diagonal (1-D) inv_mass is supported on the batched path")
+            self.mass_sqrt = (1 / self.inv_mass) ** 0.5
+        # step sizes: python float (bitwise hamiltorch) or per-chain fp32 column under NUTS adaptation
+        self.eps_host = [float(step_size)] * C
+        self.step_size_init = float(step_size)
+        self.H_t = [0.0] * C
+        self.eps_bar = [1.0] * C
+        # initial state: logp (sum over shards) and the shard-0 gradient that opens a trajectory
+        lp0, g0 = evs[0].logp_grad(theta)
+        for m in range(1, self.M):
+            lp0 = lp0 + evs[m].logp(theta)
+        self.cur = [theta, lp0, g0]
+        self.last_ret = [t.clone() for t in self.cur]
+        self.burn_prev = [t.clone() for t in self.cur]
+        S_cap = num_samples + 2 if store else 2
+        self.samples = torch.empty(C, S_cap, K, device=device)
+        self.samples[:, 0] = theta
+        self.counts = torch.ones(C, dtype=torch.long, device=device)
+        self.accepted = torch.zeros(C, num_samples, dtype=torch.bool, device=device)
+        self.trace = torch.empty(C, num_samples, device=device)
+        self._rows = torch.arange(C, device=device) * S_cap
+        self.n = 0
+
+    def _eps(self):
+        if not self.nuts:
+            return self.eps_host[0]
+        return torch.tensor(self.eps_host, dtype=torch.float32, device=self.device)[:, None]
+
+    def _trajectory(self, th, g, p, eps):
+        evs, L, M, inv_mass = self.evs, self.L, self.M, self.inv_mass
+        if not self.splitting:
+            g_open = g if self.reuse else evs[0].logp_grad(th)[1]
+            p = p + (0.5 * eps) * g_open
+            lp_new = g_new = None
+            for _ in range(L):
+                th = th + eps * p if inv_mass is None else th + eps * inv_mass * p
+                lp_new, g_new = evs[0].logp_grad(th)
+                p = p + eps * g_new
+            p = p - (0.5 * eps) * g_new
+            return th, p, lp_new, g_new
+        sub = eps / (2 * (M - 1))
+        g0_cached = g if self.reuse else None
+        gm = lp0_end = None
+        for _ in range(L):
+            for m in range(M):
+                if m == 0 and g0_cached is not None:
+                    gm = g0_cached
+                else:
+                    _, gm = evs[m].logp_grad(th)
+                p = p + (0.5 * eps) * gm
+                if m < M - 1:
+                    th = th + sub * p
+            for m in reversed(range(M)):
+                if not (m == M - 1 and self.reuse):      # same theta as the forward pass' last shard
+                    lp0_end, gm = evs[m].logp_grad(th)
+                p = p + (0.5 * eps) * gm
+                if m > 0:
+                    th = th + sub * p
+            g0_cached = gm if self.reuse else None
+        lp_sum = lp0_end.clone()
+        for m in range(1, M):
+            lp_sum = lp_sum + evs[m].logp(th)
+        return th, p, lp_sum, gm
+
+    def step(self):
+        """One HMC iteration for every chain (hamiltorch ``sample`` loop body)."""
+        n = self.n
+        if n >= self.num_samples:
+            raise RuntimeError("all samples drawn")
+        rng = self.rng
+        z = rng.draw_momentum()
+        logu = None if self.strict else rng.draw_logu()
+        p = z if self.mass_sqrt is None else z * self.mass_sqrt
+        th, lp, g = self.cur
+        H0 = -lp + _kinetic(p, self.inv_mass)
+        th_new, p, lp_new, g_new = self._trajectory(th, g, p, self._eps())
+        H1 = -lp_new + _kinetic(p, self.inv_mass)
+        d = H0 - H1
+        rho = torch.where(torch.isnan(d), torch.zeros_like(d), torch.clamp(d, max=0.0))
+        ok = torch.isfinite(lp) & torch.isfinite(lp_new)
+        if self.strict:
+            logu = rng.draw_logu(ok.tolist())                      # host sync: hamiltorch skips the draw on error
+        acc = ok & (rho >= logu)
+        err = ~ok
+        new = [th_new, lp_new, g_new]
+
+        def sel(mask, a, b):
+            return torch.where(mask[:, None] if a.dim() == 2 else mask, a, b)
+
+        if n > self.burn:
+            nxt = [sel(acc, nw, lr) for nw, lr in zip(new, self.last_ret)]
+            self.last_ret = nxt
+            if self.store:
+                valid = ~err
+                row = torch.where(valid, self.counts, torch.full_like(self.counts, self.samples.shape[1] - 1))
+                self.samples.view(-1, self.K).index_copy_(0, self._rows + row, nxt[0])
+                self.counts = self.counts + valid.long()
+        else:
+            fallback = [sel(err, lr, bp) for lr, bp in zip(self.last_ret, self.burn_prev)]
+            nxt = [sel(acc, nw, fb) for nw, fb in zip(new, fallback)]
+            self.burn_prev = [sel(acc, nw, bp) for nw, bp in zip(new, self.burn_prev)]
+        self.cur = nxt
+        self.accepted[:, n] = acc
+        self.trace[:, n] = nxt[1]
+        if self.nuts and n <= self.burn:
+            rho_h = torch.where(err, torch.full_like(rho, float("nan")), rho).tolist()   # host sync (burn only)
+            err_h = err.tolist()
+            for c in range(self.C):
+                if n < self.burn or err_h[c]:
+                    self.eps_host[c], self.eps_bar[c], self.H_t[c] = adaptation(
+                        rho_h[c], n, self.step_size_init, self.H_t[c], self.eps_bar[c], self.desired_accept_rate)
+                if n == self.burn:
+                    self.eps_host[c] = self.eps_bar[c]
+        self.n += 1
+
+    def result(self) -> ChainResult:
+        return ChainResult(self.samples, self.counts, self.accepted[:, :self.n], self.trace[:, :self.n],
+                           list(self.eps_host), sum(e.n_grad for e in self.evs), sum(e.n_value for e in self.evs))
+
+
+def run_chains(evaluators, theta0: torch.Tensor, num_samples: int, num_steps_per_sample: int, step_size,
+               **kw) -> ChainResult:
+    """Run C independent chains for ``num_samples`` iterations (see HMCRunner)."""
+    r = HMCRunner(evaluators, theta0, num_samples, num_steps_per_sample, step_size, **kw)
+    for _ in range(num_samples):
+        r.step()
+    return r.result()
+
+
+# ------------------------------------------------------------------------------------------------
+# hamiltorch-compatible entry point
+# ------------------------------------------------------------------------------------------------
+def sample(log_prob_func, params_init, num_samples=10, num_steps_per_sample=10, step_size=0.1, burn=0, jitter=None,
+           inv_mass=None, normalizing_const=1., softabs_const=None, explicit_binding_const=100,
+           fixed_point_threshold=1e-5, fixed_point_max_iterations=1000, jitter_max_tries=10, sampler=Sampler.HMC,
+           integrator=Integrator.IMPLICIT, metric=None, debug=False, desired_accept_rate=0.8, store_on_GPU=True,
+           pass_grad=None, verbose=False, rng: str = "global", seed: Optional[int] = None):
+    """Drop-in for ``hamiltorch.samplers.sample`` on the VI-HMC path: returns a list of [K] tensors
+    (hamiltorch's ``ret_params``). A ``log_prob_func`` built by vihmc's ``define_model_log_prob`` runs
+    on the batched HIP engine; any other torch closure runs through autograd. ``debug=2`` returns
+    (samples, acceptance rate) / (samples, step size) for NUTS as hamiltorch does."""
+    if params_init.dim() != 1:
+        raise RuntimeError("params_init must be a 1d tensor.")
+    fns = log_prob_func if isinstance(log_prob_func, list) else [log_prob_func]
+    K = params_init.shape[0]
+    device = params_init.device
+    evs = [evaluator_for(f, K, device) for f in fns]
+    device = evs[0].device
+    if rng == "global":
+        r = ChainRNG(1, K, device, mode="global")
+    else:
+        r = ChainRNG(1, K, device, seeds=[seed if seed is not None else torch.initial_seed()])
+    res = run_chains(evs if len(evs) > 1 else evs[0], params_init[None], num_samples, num_steps_per_sample, step_size,
+                     burn=burn, inv_mass=inv_mass, sampler=sampler, integrator=integrator,
+                     desired_accept_rate=desired_accept_rate, rng=r)
+    out = [t.to(params_init.device) for t in res.chain(0)]
+    if not verbose:
+        rate = 1 - float((~res.accepted[0]).sum()) / num_samples
+        print(f"Acceptance Rate {rate:.2f}")
+    if debug == 2:
+        if sampler == Sampler.HMC_NUTS:
+            return out, res.step_size[0]
+        return out, 1 - float((~res.accepted[0]).sum()) / num_samples
+    return out
