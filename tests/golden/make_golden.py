@@ -246,9 +246,32 @@ def deeponet_split_cases(out):
                         spec=np.array([16, 16, 12, 5, 3, 3, 16]), **res)
 
 
+def init_cases(out):
+    """Reference model construction consumes the torch RNG (nn.Linear init): flat parameter vectors of
+    the reference DeepONet (model.py:11-75) and BNN get_model (main_VI_HMC.py:297-334) after
+    torch.manual_seed(123), to pin the build's modules to the same init."""
+    M = import_ref("Operator_network/VI_HMC", "main_VI_HMC_burgers")
+    torch.manual_seed(123)
+    net = M.DeepONet(16, 16, 12, 5, 3, 3, "tanh", None)
+    don = torch.cat([p.detach().flatten() for p in net.parameters()]).numpy()
+    cwd = os.getcwd()
+    os.chdir(os.path.join(REF, "Neural_network", "VI_HMC"))
+    try:
+        B = import_ref("Neural_network/VI_HMC", "main_VI_HMC")
+    finally:
+        os.chdir(cwd)
+    torch.manual_seed(123)
+    bnn = torch.cat([p.detach().flatten() for p in B.get_model(True).parameters()]).numpy()
+    np.savez(os.path.join(out, "init_fixtures.npz"), deeponet_16_12_3=don, bnn_10_10=bnn)
+
+
 if __name__ == "__main__":
     stub_hamiltorch()
     torch.set_num_threads(8)
+    if "--init-only" in sys.argv:
+        init_cases(HERE)
+        sys.exit(0)
+    init_cases(HERE)
     bnn_cases(HERE)
     deeponet_cases(HERE, full_size="--no-full" not in sys.argv)
     deeponet_split_cases(HERE)

@@ -58,7 +58,7 @@ class _Engine:
         self.device_bytes = self.L.vihmc_plan_device_bytes(self._plan)
 
     def close(self):
-        if getattr(self, "_plan", None) and self._plan.value:
+        if getattr(self, "_plan", None) is not None and self._plan.value:
             self.L.vihmc_plan_destroy(self._plan)
             self._plan = ctypes.c_void_p()
 
