@@ -1,0 +1,239 @@
+// Fused branch x trunk contraction + Gaussian likelihood (+ its backward) -- v2.
+//
+// Replaces torch.einsum("...i,...i->...", xb, xtr) + b (Operator_network/VI_HMC/my_make_func.py:79-82),
+// GaussianNLLLoss / regression ll (main_VI_HMC_burgers.py:157-163) and their autograd backward.
+//
+// Owner form (see ContractProb): a 256-thread workgroup owns 128 rows of `Own` (32 per wave, held in
+// registers as the B operand of S = Q . Own^T for the whole sweep) and streams `Q` in 16-row chunks
+// through a double-buffered LDS image that all four waves share; the next chunk is prefetched
+// global -> registers while the current one is consumed, then written to the other buffer.
+//   S tile (16 q x 16 o per MFMA tile)  : A = Q rows   (ds_read_b128, 16 k per float4, k-permuted)
+//   dOwn += G^T Q (16 o x 16 j tiles)   : A = G (the S accumulator registers, MFMA step rr = register rr)
+//                                          B = Q[q][j] (ds_read_b32)
+// The LDS row stride LDQ satisfies LDQ/4 odd, which makes both read patterns bank-conflict free:
+// b128 row reads of 16 consecutive rows hit 16 distinct 4-bank groups, and the b32 reads of row pairs
+// 4 apart (lane groups 0/1 and 2/3 of each half-wave) are 16 banks apart.
+#include "vihmc_internal.h"
+
+namespace vihmc {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma_c(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum_c(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__host__ __device__ constexpr int contract_ldq(int W) {
+    return ((((W + 3) & ~3) / 4) & 1) ? ((W + 3) & ~3) : ((W + 3) & ~3) + 4;
+}
+
+// SNKB/SNTAIL >= 0 fix the k-block structure at compile time (the production width W = 100 is
+// SNKB = 6 full 16-wide blocks + SNTAIL = 1 four-wide step); -1 reads it from W at run time.
+template <int WMAX, int SNKB, int SNTAIL, bool GRAD>
+__global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
+    constexpr int NB = WMAX / 16;
+    constexpr int QC = CONTRACT_QC;
+    extern __shared__ float qs[];                           // 2 x QC x LDQ
+    const int W = P.W;
+    const int W4 = (W + 3) & ~3;
+    const int LDQ = contract_ldq(W);
+    const int LDQ4 = LDQ >> 2;
+    float4* qs4 = reinterpret_cast<float4*>(qs);
+    int b = blockIdx.x;
+    const int per_chain = P.o_tiles * P.q_chunks;
+    const int c = b / per_chain;
+    b -= c * per_chain;
+    const int qc = b / P.o_tiles;
+    const int og = b - qc * P.o_tiles;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const float* Own = P.Own + c * P.own_cs;
+    const float* Q = P.Q + c * P.q_cs;
+    const float b0 = P.b0[c * P.b0_cs];
+    const int o0 = og * CONTRACT_OWN_PER_WG + wave * 32;
+    const int nkb = SNKB >= 0 ? SNKB : (W >> 4);
+    const int ntail = SNTAIL >= 0 ? SNTAIL : ((W4 - (nkb << 4)) >> 2);
+    const int JT = SNKB >= 0 ? SNKB + (SNTAIL > 0 ? 1 : 0) : ((W + 15) >> 4);
+
+    float4 ob[2][NB];
+    float otl[2][3];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const float* orow = Own + (int64_t)min(o0 + 16 * s + lr, P.Mo - 1) * P.ldown;
+#pragma unroll
+        for (int bb = 0; bb < NB; ++bb)
+            ob[s][bb] = (bb < nkb) ? *reinterpret_cast<const float4*>(orow + 16 * bb + 4 * lg)
+                                   : float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ts = 0; ts < 3; ++ts) otl[s][ts] = (ts < ntail) ? orow[16 * nkb + 4 * ts + lg] : 0.f;
+    }
+    f32x4 dacc[2][NB];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < NB; ++t) dacc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int q_lo = qc * P.q_per_chunk;
+    const int q_hi = min(q_lo + P.q_per_chunk, P.Mq);
+    const int nchunks = q_hi > q_lo ? (q_hi - q_lo + QC - 1) / QC : 0;
+    const int w4q = W4 >> 2;
+    const int n4 = QC * w4q;
+    // Q chunk staging: QC*W4/4 <= 512 float4 -> two per thread, always loaded (clamped index) so the
+    // staging values live in registers across the compute of the current chunk.
+    static_assert(QC * (WMAX / 4) <= 512, "chunk staging assumes <= 2 float4 per thread");
+    const int i0 = min(tid, n4 - 1), i1 = min(tid + 256, n4 - 1);
+    const int r0s = i0 / w4q, c0s = i0 - r0s * w4q, r1s = i1 / w4q, c1s = i1 - r1s * w4q;
+    const bool st0 = tid < n4, st1 = tid + 256 < n4;
+    float4 stg0, stg1;
+#define VIHMC_LOAD_CHUNK(QROW0)                                                                       \
+    stg0 = reinterpret_cast<const float4*>(Q + (int64_t)min((QROW0) + r0s, P.Mq - 1) * P.ldq)[c0s]; \
+    stg1 = reinterpret_cast<const float4*>(Q + (int64_t)min((QROW0) + r1s, P.Mq - 1) * P.ldq)[c1s];
+#define VIHMC_STORE_CHUNK(BUF4)                     \
+    if (st0) (BUF4)[r0s * LDQ4 + c0s] = stg0;      \
+    if (st1) (BUF4)[r1s * LDQ4 + c1s] = stg1;
+
+    double ssq = 0.0, gsum = 0.0;
+    float* sout = P.out + c * P.out_cs;
+    if (nchunks > 0) {
+        VIHMC_LOAD_CHUNK(q_lo)
+        VIHMC_STORE_CHUNK(qs4)
+    }
+    __syncthreads();
+    for (int ci = 0; ci < nchunks; ++ci) {
+        const int q0 = q_lo + ci * QC;
+        const float* cur = qs + (ci & 1) * QC * LDQ;
+        const bool more = ci + 1 < nchunks;
+        {
+            const int h = 0;
+            float yv[2][4];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    yv[s][r] = P.Y[(int64_t)min(q0 + 16 * h + 4 * lg + r, P.Mq - 1) * P.ldy +
+                                   min(o0 + 16 * s + lr, P.Mo - 1)];
+            if (more) {
+                VIHMC_LOAD_CHUNK(q0 + QC)
+            }
+            f32x4 sacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            const float* qrow = cur + (16 * h + lr) * LDQ;
+            const float4* qrow4 = reinterpret_cast<const float4*>(cur) + (16 * h + lr) * LDQ4;
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+                if (bb < nkb) {
+                    const float4 qa = qrow4[4 * bb + lg];
+                    sacc[0] = mfma_c(qa.x, ob[0][bb].x, sacc[0]);
+                    sacc[1] = mfma_c(qa.x, ob[1][bb].x, sacc[1]);
+                    sacc[0] = mfma_c(qa.y, ob[0][bb].y, sacc[0]);
+                    sacc[1] = mfma_c(qa.y, ob[1][bb].y, sacc[1]);
+                    sacc[0] = mfma_c(qa.z, ob[0][bb].z, sacc[0]);
+                    sacc[1] = mfma_c(qa.z, ob[1][bb].z, sacc[1]);
+                    sacc[0] = mfma_c(qa.w, ob[0][bb].w, sacc[0]);
+                    sacc[1] = mfma_c(qa.w, ob[1][bb].w, sacc[1]);
+                }
+            }
+#pragma unroll
+            for (int ts = 0; ts < 3; ++ts) {
+                if (ts < ntail) {
+                    const float qa = qrow[16 * nkb + 4 * ts + lg];
+                    sacc[0] = mfma_c(qa, otl[0][ts], sacc[0]);
+                    sacc[1] = mfma_c(qa, otl[1][ts], sacc[1]);
+                }
+            }
+            float g[2][4];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int qq = q0 + 16 * h + 4 * lg + r;
+                    const int oo = o0 + 16 * s + lr;
+                    const bool ok = (qq < q_hi) && (oo < P.Mo);
+                    const float sv = sacc[s][r] + b0;
+                    if (!GRAD && P.write_s && ok) sout[(int64_t)qq * P.ldout + oo] = sv;
+                    const float rv = sv - yv[s][r];
+                    g[s][r] = ok ? P.gscale * rv : 0.f;
+                    if (ok) {
+                        ssq += (double)rv * (double)rv;
+                        gsum += (double)g[s][r];
+                    }
+                }
+            if (GRAD) {
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const float* qr = cur + (16 * h + 4 * lg + rr) * LDQ;
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) {
+                        if (t < JT) {
+                            const float bq = qr[min(16 * t + lr, W - 1)];
+                            dacc[0][t] = mfma_c(g[0][rr], bq, dacc[0][t]);
+                            dacc[1][t] = mfma_c(g[1][rr], bq, dacc[1][t]);
+                        }
+                    }
+                }
+            }
+        }
+        if (more) {
+            VIHMC_STORE_CHUNK(qs4 + ((ci + 1) & 1) * QC * LDQ4)
+        }
+        __syncthreads();
+    }
+
+    if (GRAD) {
+        float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int t = 0; t < NB; ++t) {
+                const int j = 16 * t + lr;
+                if (t >= JT || j >= P.ldout) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int oo = o0 + 16 * s + 4 * lg + r;
+                    if (oo < P.Mo) out[(int64_t)oo * P.ldout + j] = (j < W) ? dacc[s][t][r] : 0.f;
+                }
+            }
+    }
+    if (P.with_stats) {
+        ssq = wave_sum_c(ssq);
+        gsum = wave_sum_c(gsum);
+        if (lane == 0) {
+            double* st = P.stats + c * P.stats_cs + 2 * (int64_t)((qc * P.o_tiles + og) * 4 + wave);
+            st[0] = ssq;
+            st[1] = gsum;
+        }
+    }
+}
+
+#undef VIHMC_LOAD_CHUNK
+#undef VIHMC_STORE_CHUNK
+
+size_t contract_lds_bytes(int W) { return sizeof(float) * 2 * CONTRACT_QC * contract_ldq(W); }
+
+#define VIHMC_LAUNCH_C(kern, grid, block, shm, s, ...) \
+    do { hipLaunchKernelGGL(kern, grid, block, shm, s, __VA_ARGS__); return hipGetLastError(); } while (0)
+
+template <bool GRAD>
+static hipError_t launch_contract_t(const ContractProb& p, int C, hipStream_t s) {
+    dim3 g(C * p.o_tiles * p.q_chunks), blk(256);
+    const size_t shm = contract_lds_bytes(p.W);
+    const int w = p.W;
+    if (w == 100) VIHMC_LAUNCH_C((k_contract2<112, 6, 1, GRAD>), g, blk, shm, s, p);
+    if (w <= 16) VIHMC_LAUNCH_C((k_contract2<16, -1, -1, GRAD>), g, blk, shm, s, p);
+    if (w <= 32) VIHMC_LAUNCH_C((k_contract2<32, -1, -1, GRAD>), g, blk, shm, s, p);
+    if (w <= 64) VIHMC_LAUNCH_C((k_contract2<64, -1, -1, GRAD>), g, blk, shm, s, p);
+    if (w <= 112) VIHMC_LAUNCH_C((k_contract2<112, -1, -1, GRAD>), g, blk, shm, s, p);
+    if (w <= 128) VIHMC_LAUNCH_C((k_contract2<128, -1, -1, GRAD>), g, blk, shm, s, p);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_contract(const ContractProb& p, int C, bool with_grad, hipStream_t s) {
+    return with_grad ? launch_contract_t<true>(p, C, s) : launch_contract_t<false>(p, C, s);
+}
+
+}  // namespace vihmc

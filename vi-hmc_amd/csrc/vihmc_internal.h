@@ -9,6 +9,12 @@ namespace vihmc {
 enum { ACT_ID = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SINE = 3 };
 enum { MODE_FWD = 0, MODE_BWD = 1 };
 
+// contraction geometry (vihmc_contract.hip): 4 waves x 32 owner rows per workgroup, 16-row Q chunks
+constexpr int CONTRACT_OWN_PER_WG = 128;
+constexpr int CONTRACT_QC = 16;
+// row-dot geometry (vihmc_layers.hip): 4 waves per workgroup, 16*MS rows per wave
+constexpr int ROWDOT_WAVES = 4;
+
 // ---------------------------------------------------------------------------------------------
 // Row-dot GEMM: O[m][n] = epilogue( sum_k A[m][k] * B[n][k] ), both operands row-major with the
 // contraction index contiguous. Used for every forward layer (A = activations, B = W[n_out][n_in])
@@ -24,7 +30,7 @@ struct RowdotProb {
     const float* bias; int64_t bias_cs;
     const float* H; int64_t h_cs; int32_t ldh;
     int32_t M, Nn, K, act;
-    int32_t tiles;          // ceil(M / (16*MS))
+    int32_t tiles;          // ceil(M / (ROWDOT_WAVES*16*MS)) workgroups per chain
 };
 struct RowdotArgs {
     RowdotProb p[2];
@@ -63,8 +69,9 @@ struct ContractProb {
     const float* b0;  int64_t b0_cs;
     float* out;       int64_t out_cs; int32_t ldout; int64_t out_chunk_stride;
     double* stats;    int64_t stats_cs;   // 2 doubles per wave (sum r^2, sum G) when with_stats
+                                          // (4 waves per workgroup, index ((qc*o_tiles+og)*4+wave))
     int32_t Mo, Mq, W;
-    int32_t o_tiles, q_chunks, q_per_chunk;
+    int32_t o_tiles, q_chunks, q_per_chunk;   // o_tiles = ceil(Mo / CONTRACT_OWN_PER_WG)
     int32_t with_stats, write_s;
     float gscale;
 };
@@ -73,6 +80,7 @@ struct ContractProb {
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s);
 hipError_t launch_colsum(const ColsumArgs& a, int jt, hipStream_t s);
 hipError_t launch_contract(const ContractProb& p, int C, bool with_grad, hipStream_t s);
+size_t contract_lds_bytes(int W);
 hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* frozen, const int32_t* map_w,
                               const int32_t* map_wt, int64_t D, hipStream_t s);
 hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, int K, const int32_t* smap_w,

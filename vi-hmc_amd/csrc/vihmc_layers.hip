@@ -1,0 +1,296 @@
+// Layer GEMMs of the two MLPs (branch: N rows, trunk: P rows), batched over chains and grouped
+// branch+trunk per launch.
+//   k_rowdot2 : forward layer  h = act(x W^T + b)                   (F.linear + tanh, my_make_func.py:52-77)
+//               backward input delta_{l-1} = (delta_l W) * act'(h)  (autograd of the same)
+//   k_colsum  : weight / bias gradients dW = delta^T h, db = sum delta, per row chunk (fixed-order reduce)
+// fp32 MFMA v_mfma_f32_16x16x4_f32; operand maps and the float4 k-permutation: see vihmc_kernels.hip.
+#include "vihmc_internal.h"
+
+namespace vihmc {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float act_apply_l(int act, float z) {
+    if (act == ACT_TANH) return tanhf(z);
+    if (act == ACT_RELU) return fmaxf(z, 0.f);
+    return z;
+}
+
+__device__ __forceinline__ float act_grad_from_out_l(int act, float h) {
+    if (act == ACT_TANH) return 1.f - h * h;
+    if (act == ACT_RELU) return h > 0.f ? 1.f : 0.f;
+    return 1.f;
+}
+
+// LDS row stride for the staged weight block: stride/4 odd keeps 16 consecutive-row b128 reads on
+// 16 distinct 4-bank groups.
+__host__ __device__ constexpr int rowdot_ldb(int k4) { return ((k4 / 4) & 1) ? k4 : k4 + 4; }
+
+// =============================================================================================
+// Row-dot GEMM v2: 256-thread workgroup = 4 waves x 16*MS rows, the whole weight block B [Nn x K]
+// staged once in LDS and shared; A rows streamed from HBM/L2 as float4 with a one-block register
+// prefetch; MFMAs interleaved over MS*NT independent accumulators.
+// =============================================================================================
+template <int NT, int MS, int MODE>
+__global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
+    extern __shared__ float bs[];
+    int b = blockIdx.x;
+    const int first = args.C * args.p[0].tiles;
+    const bool second = b >= first;
+    const RowdotProb P = second ? args.p[1] : args.p[0];
+    if (second) b -= first;
+    const int c = b / P.tiles;
+    const int tile = b - c * P.tiles;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const float* A = P.A + c * P.a_cs;
+    const float* B = P.B + c * P.b_cs;
+    const int K4 = (P.K + 3) & ~3;
+    const int LDB = rowdot_ldb(K4);
+
+    // stage B (rows n < Nn, K4 floats each; global row stride ldb >= K4, zero padded)
+    {
+        const int q4 = K4 >> 2;
+        const int n4 = P.Nn * q4;
+        for (int i = tid; i < n4; i += 256) {
+            const int r = i / q4, c4 = i - r * q4;
+            *reinterpret_cast<float4*>(bs + r * LDB + 4 * c4) =
+                *reinterpret_cast<const float4*>(B + (int64_t)r * P.ldb + 4 * c4);
+        }
+    }
+
+    const int m0 = tile * (ROWDOT_WAVES * 16 * MS) + wave * 16 * MS;
+    const float* ar[MS];
+#pragma unroll
+    for (int s = 0; s < MS; ++s) ar[s] = A + (int64_t)min(m0 + 16 * s + lr, P.M - 1) * P.lda;
+    const float* br[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) br[t] = bs + min(16 * t + lr, P.Nn - 1) * LDB;
+
+    f32x4 acc[MS][NT];
+#pragma unroll
+    for (int s = 0; s < MS; ++s)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int kfull = P.K & ~15;
+    float4 a_cur[MS];
+    if (kfull > 0) {
+#pragma unroll
+        for (int s = 0; s < MS; ++s) a_cur[s] = *reinterpret_cast<const float4*>(ar[s] + 4 * lg);
+    }
+    __syncthreads();
+    for (int kb = 0; kb < kfull; kb += 16) {
+        float4 a_nxt[MS];
+        const bool more = kb + 16 < kfull;
+        if (more) {
+#pragma unroll
+            for (int s = 0; s < MS; ++s) a_nxt[s] = *reinterpret_cast<const float4*>(ar[s] + kb + 16 + 4 * lg);
+        }
+        float4 w[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) w[t] = *reinterpret_cast<const float4*>(br[t] + kb + 4 * lg);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a_cur[s].x, w[t].x, acc[s][t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a_cur[s].y, w[t].y, acc[s][t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a_cur[s].z, w[t].z, acc[s][t]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a_cur[s].w, w[t].w, acc[s][t]);
+        if (more) {
+#pragma unroll
+            for (int s = 0; s < MS; ++s) a_cur[s] = a_nxt[s];
+        }
+    }
+    // tail: K rounded up to 4 (operand padding columns are zero)
+    for (int kb = kfull; kb < K4; kb += 4) {
+        float a[MS], w[NT];
+#pragma unroll
+        for (int s = 0; s < MS; ++s) a[s] = ar[s][kb + lg];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) w[t] = br[t][kb + lg];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a[s], w[t], acc[s][t]);
+    }
+
+    float* O = P.O + c * P.o_cs;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int n = 16 * t + lr;
+        if (n >= P.ldo) continue;
+        const bool live = n < P.Nn;
+        float bv = 0.f;
+        if (MODE == MODE_FWD && live && P.bias) bv = P.bias[c * P.bias_cs + n];
+#pragma unroll
+        for (int s = 0; s < MS; ++s)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + 16 * s + 4 * lg + r;
+                if (m >= P.M) continue;
+                float o = 0.f;
+                if (live) {
+                    const float v = acc[s][t][r];
+                    if (MODE == MODE_FWD) {
+                        o = act_apply_l(P.act, v + bv);
+                    } else {
+                        const float h = P.H[c * P.h_cs + (int64_t)m * P.ldh + n];
+                        o = v * act_grad_from_out_l(P.act, h);
+                    }
+                }
+                O[(int64_t)m * P.ldo + n] = o;
+            }
+    }
+}
+
+// =============================================================================================
+// Column-sum GEMM (weight + bias gradients): one wave per (chain, row chunk, pair of 16-row
+// output sub-tiles); partial slabs are reduced in fixed order afterwards.
+// =============================================================================================
+template <int JT>
+__global__ __launch_bounds__(64) void k_colsum(ColsumArgs args) {
+    int b = blockIdx.x;
+    const int per0 = args.C * args.p[0].n_chunks * args.p[0].n_pairs;
+    const bool second = b >= per0;
+    const ColsumProb P = second ? args.p[1] : args.p[0];
+    if (second) b -= per0;
+    const int per_chain = P.n_chunks * P.n_pairs;
+    const int c = b / per_chain;
+    b -= c * per_chain;
+    const int chunk = b / P.n_pairs;
+    const int pair = b - chunk * P.n_pairs;
+    const int lane = threadIdx.x, lr = lane & 15, lg = lane >> 4;
+    const float* D = P.D + c * P.d_cs;
+    const float* H = P.H + c * P.h_cs;
+    const int r0 = chunk * P.rows_per_chunk;
+    const int r1 = min(r0 + P.rows_per_chunk, P.M);
+
+    int ncol[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) ncol[s] = min(32 * pair + 16 * s + lr, P.n_out - 1);
+    int jcol[JT];
+#pragma unroll
+    for (int t = 0; t < JT; ++t) jcol[t] = min(16 * t + lr, P.n_in - 1);
+
+    f32x4 acc[2][JT];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < JT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dsum[2] = {0.f, 0.f};
+
+    for (int m = r0; m < r1; m += 4) {
+        const int mm = m + lg;
+        const bool mok = mm < r1;
+        const int mr = mok ? mm : r0;
+        const float* drow = D + (int64_t)mr * P.ldd;
+        const float* hrow = H + (int64_t)mr * P.ldh;
+        float a[2], h[JT];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const float v = drow[ncol[s]];
+            a[s] = mok ? v : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < JT; ++t) h[t] = hrow[jcol[t]];
+#pragma unroll
+        for (int t = 0; t < JT; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) acc[s][t] = mfma(a[s], h[t], acc[s][t]);
+        dsum[0] += a[0];
+        dsum[1] += a[1];
+    }
+
+    float* part = P.part + c * P.part_cs + (int64_t)chunk * P.part_stride;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < JT; ++t) {
+            const int j = 16 * t + lr;
+            if (j >= P.ldh) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = 32 * pair + 16 * s + 4 * lg + r;
+                if (n < P.n_out) part[(int64_t)n * P.ldh + j] = (j < P.n_in) ? acc[s][t][r] : 0.f;
+            }
+        }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        float v = dsum[s];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const int n = 32 * pair + 16 * s + lr;
+        if (lg == 0 && n < P.n_out) part[(int64_t)P.n_out * P.ldh + n] = v;
+    }
+}
+
+
+// =============================================================================================
+// launchers
+// =============================================================================================
+#define VIHMC_LAUNCH_L(kern, grid, block, shm, s, ...) \
+    do { hipLaunchKernelGGL(kern, grid, block, shm, s, __VA_ARGS__); return hipGetLastError(); } while (0)
+
+size_t rowdot_lds_bytes(const RowdotArgs& a) {
+    size_t m = 0;
+    for (int i = 0; i < a.nprob; ++i) {
+        const int k4 = (a.p[i].K + 3) & ~3;
+        m = std::max(m, sizeof(float) * (size_t)a.p[i].Nn * rowdot_ldb(k4));
+    }
+    return m;
+}
+
+template <int MS, int MODE>
+static hipError_t rowdot_nt(const RowdotArgs& a, int nt, hipStream_t s) {
+    const int blocks = a.C * a.p[0].tiles + (a.nprob > 1 ? a.C * a.p[1].tiles : 0);
+    const size_t shm = rowdot_lds_bytes(a);
+    dim3 g(blocks), blk(256);
+    switch (nt) {
+        case 1: VIHMC_LAUNCH_L((k_rowdot2<1, MS, MODE>), g, blk, shm, s, a);
+        case 2: VIHMC_LAUNCH_L((k_rowdot2<2, MS, MODE>), g, blk, shm, s, a);
+        case 3: VIHMC_LAUNCH_L((k_rowdot2<3, MS, MODE>), g, blk, shm, s, a);
+        case 4: VIHMC_LAUNCH_L((k_rowdot2<4, MS, MODE>), g, blk, shm, s, a);
+        case 5: VIHMC_LAUNCH_L((k_rowdot2<5, MS, MODE>), g, blk, shm, s, a);
+        case 6: VIHMC_LAUNCH_L((k_rowdot2<6, MS, MODE>), g, blk, shm, s, a);
+        case 7: VIHMC_LAUNCH_L((k_rowdot2<7, MS, MODE>), g, blk, shm, s, a);
+        case 8: VIHMC_LAUNCH_L((k_rowdot2<8, MS, MODE>), g, blk, shm, s, a);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s) {
+    if (ms == 1) return mode == MODE_FWD ? rowdot_nt<1, MODE_FWD>(a, nt, s) : rowdot_nt<1, MODE_BWD>(a, nt, s);
+    return mode == MODE_FWD ? rowdot_nt<2, MODE_FWD>(a, nt, s) : rowdot_nt<2, MODE_BWD>(a, nt, s);
+}
+
+hipError_t launch_colsum(const ColsumArgs& a, int jt, hipStream_t s) {
+    int blocks = a.C * a.p[0].n_chunks * a.p[0].n_pairs +
+                 (a.nprob > 1 ? a.C * a.p[1].n_chunks * a.p[1].n_pairs : 0);
+    dim3 g(blocks), blk(64);
+    switch (jt) {
+        case 1: VIHMC_LAUNCH_L(k_colsum<1>, g, blk, 0, s, a);
+        case 2: VIHMC_LAUNCH_L(k_colsum<2>, g, blk, 0, s, a);
+        case 3: VIHMC_LAUNCH_L(k_colsum<3>, g, blk, 0, s, a);
+        case 4: VIHMC_LAUNCH_L(k_colsum<4>, g, blk, 0, s, a);
+        case 5: VIHMC_LAUNCH_L(k_colsum<5>, g, blk, 0, s, a);
+        case 6: VIHMC_LAUNCH_L(k_colsum<6>, g, blk, 0, s, a);
+        case 7: VIHMC_LAUNCH_L(k_colsum<7>, g, blk, 0, s, a);
+        case 8: VIHMC_LAUNCH_L(k_colsum<8>, g, blk, 0, s, a);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace vihmc

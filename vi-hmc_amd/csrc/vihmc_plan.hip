@@ -89,7 +89,12 @@ struct vihmc_plan {
     float *y = nullptr, *yT = nullptr;
     float* partB = nullptr;
     int64_t partB_cs = 0;
-    int qchunksB = 1, qperB = 16;
+    int qchunksB = 1, qperB = 32;
+    int qchunksA = 1, qperA = 32;          // side A splits its q range only for small chain counts
+    float* partA = nullptr;
+    int64_t partA_cs = 0;
+    ReduceJob* jobsA = nullptr;
+    int lenA = 0;
     double* stats = nullptr;
     int64_t stats_cs = 0;
     int nwavesA = 0;
@@ -319,14 +324,24 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     }
     // contraction side B (branch-owner) partials over trunk chunks
     {
-        const int waves_a = cdiv(p->P, 32), waves_b = cdiv(p->N, 32);
-        int qc = std::max(1, (int)std::lround((double)waves_a / waves_b));
-        p->qperB = (int)(((int64_t)cdiv(p->P, qc) + 15) / 16 * 16);
+        // side A: workgroups own 128 trunk rows and sweep the branch rows; split the sweep (partial
+        // dZ_trunk slabs + fixed-order reduce) only when too few workgroups would fill the chip
+        const int og_a = cdiv(p->P, CONTRACT_OWN_PER_WG), og_b = cdiv(p->N, CONTRACT_OWN_PER_WG);
+        int qa = std::max(1, std::min(8, (int)std::lround(1024.0 / ((double)C * og_a))));
+        p->qperA = (int)(((int64_t)cdiv(p->N, qa) + CONTRACT_QC - 1) / CONTRACT_QC * CONTRACT_QC);
+        p->qchunksA = cdiv(p->N, p->qperA);
+        if (p->qchunksA > 1) {
+            p->partA_cs = r64((int64_t)p->qchunksA * p->P * p->ldz);
+            if (int rc = p->alloc(&p->partA, p->partA_cs * C)) return rc;
+        }
+        // side B: workgroups own 128 branch rows, the trunk sweep is split to match side A's grid
+        int qc = std::max(1, (int)std::lround((double)og_a * p->qchunksA / og_b));
+        p->qperB = (int)(((int64_t)cdiv(p->P, qc) + CONTRACT_QC - 1) / CONTRACT_QC * CONTRACT_QC);
         p->qchunksB = cdiv(p->P, p->qperB);
         p->partB_cs = r64((int64_t)p->qchunksB * p->N * p->ldz);
         if (int rc = p->alloc(&p->partB, p->partB_cs * C)) return rc;
-        p->nwavesA = waves_a;
-        p->stats_cs = 2 * (int64_t)waves_a;
+        p->nwavesA = p->qchunksA * og_a * 4;
+        p->stats_cs = 2 * (int64_t)p->nwavesA;
         if (int rc = p->alloc(&p->stats, p->stats_cs * C)) return rc;
         if (int rc = p->alloc(&p->lik_buf, C)) return rc;
     }
@@ -342,6 +357,18 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         jb.dst_cs = p->nets[0].delta_cs;
         p->lenB = jb.len;
         if (int rc = p->upload(&p->jobsB, &jb, 1)) return rc;
+        if (p->qchunksA > 1) {
+            ReduceJob ja{};
+            ja.src = p->partA;
+            ja.in_cs = p->partA_cs;
+            ja.part_stride = (int64_t)p->P * p->ldz;
+            ja.n_parts = p->qchunksA;
+            ja.len = p->P * p->ldz;
+            ja.dst = p->nets[1].delta[0];
+            ja.dst_cs = p->nets[1].delta_cs;
+            p->lenA = ja.len;
+            if (int rc = p->upload(&p->jobsA, &ja, 1)) return rc;
+        }
         std::vector<ReduceJob> jw;
         for (int net = 0; net < 2; ++net) {
             Net& n = p->nets[net];
@@ -373,12 +400,12 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
         RowdotArgs a{};
         a.C = C;
         int nt = 1;
-        int64_t waves32 = 0;
+        int64_t wgs = 0;
         for (int net = 0; net < 2; ++net) {
             Net& n = p->nets[net];
-            if (j < (int)n.L.size()) waves32 += (int64_t)C * cdiv(n.rows, 32);
+            if (j < (int)n.L.size()) wgs += (int64_t)C * cdiv(n.rows, ROWDOT_WAVES * 32);
         }
-        const int ms = waves32 >= 2048 ? 2 : 1;
+        const int ms = wgs >= 512 ? 2 : 1;
         for (int net = 0; net < 2; ++net) {
             Net& n = p->nets[net];
             if (j >= (int)n.L.size()) continue;
@@ -399,7 +426,7 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
             q.Nn = L.n_out;
             q.K = L.n_in;
             q.act = L.act;
-            q.tiles = cdiv(n.rows, 16 * ms);
+            q.tiles = cdiv(n.rows, ROWDOT_WAVES * 16 * ms);
             nt = std::max(nt, nt_of(L.n_out));
         }
         if (a.nprob == 1) a.p[1] = a.p[0];
@@ -423,24 +450,24 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
     q.b0 = p->packed;
     q.b0_cs = p->dp;
     if (grad) {
-        q.out = t.delta[0];
-        q.out_cs = t.delta_cs;
+        q.out = p->qchunksA > 1 ? p->partA : t.delta[0];
+        q.out_cs = p->qchunksA > 1 ? p->partA_cs : t.delta_cs;
         q.ldout = p->ldz;
+        q.out_chunk_stride = p->qchunksA > 1 ? (int64_t)p->P * p->ldz : 0;
     } else {
         q.out = out ? out : p->lik_buf;   // dummy when not writing S
         q.out_cs = out ? (int64_t)p->N * p->P : 0;
         q.ldout = p->P;
         q.write_s = out ? 1 : 0;
     }
-    q.out_chunk_stride = 0;
     q.stats = p->stats;
     q.stats_cs = p->stats_cs;
     q.Mo = p->P;
     q.Mq = p->N;
     q.W = p->W;
-    q.o_tiles = cdiv(p->P, 32);
-    q.q_chunks = 1;
-    q.q_per_chunk = p->N;
+    q.o_tiles = cdiv(p->P, CONTRACT_OWN_PER_WG);
+    q.q_chunks = p->qchunksA;
+    q.q_per_chunk = p->qperA;
     q.with_stats = 1;
     const float v = std::max(p->lik.tau_out, 1e-6f);
     q.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
@@ -484,7 +511,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         q.Mo = p->N;
         q.Mq = p->P;
         q.W = p->W;
-        q.o_tiles = cdiv(p->N, 32);
+        q.o_tiles = cdiv(p->N, CONTRACT_OWN_PER_WG);
         q.q_chunks = p->qchunksB;
         q.q_per_chunk = p->qperB;
         q.with_stats = 0;
@@ -495,6 +522,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         HIPCHK(launch_contract(q, C, true, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
         HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s));
+        if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 1, p->lenA, C, s));
 
         // backward through both MLPs, last layer first
         int cur[2] = {0, 0};
@@ -505,13 +533,13 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
             RowdotArgs ra{};
             ra.C = C;
             int jt = 1, nt = 1;
-            int64_t waves32 = 0;
+            int64_t wgs = 0;
             for (int net = 0; net < 2; ++net) {
                 Net& n = p->nets[net];
                 const int j = (int)n.L.size() - 1 - i;
-                if (j >= 1) waves32 += (int64_t)C * cdiv(n.rows, 32);
+                if (j >= 1) wgs += (int64_t)C * cdiv(n.rows, ROWDOT_WAVES * 32);
             }
-            const int ms = waves32 >= 2048 ? 2 : 1;
+            const int ms = wgs >= 512 ? 2 : 1;
             for (int net = 0; net < 2; ++net) {
                 Net& n = p->nets[net];
                 const int j = (int)n.L.size() - 1 - i;
@@ -553,7 +581,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
                     r.Nn = L.n_in;
                     r.K = L.n_out;
                     r.act = Lp.act;
-                    r.tiles = cdiv(n.rows, 16 * ms);
+                    r.tiles = cdiv(n.rows, ROWDOT_WAVES * 16 * ms);
                     nt = std::max(nt, nt_of(L.n_in));
                 }
             }
