@@ -14,8 +14,24 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// tanh for the layer epilogues: odd Taylor series through x^11 for |x| < 0.25 (truncation < 1e-8
+// relative), 1 - 2/(exp(2|x|)+1) with v_exp_f32 / v_rcp_f32 above (<= ~4 ulp); ~15 VALU ops
+// instead of the ~40 of the libm-accurate tanhf.
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float ax = fabsf(x);
+    const float x2 = x * x;
+    float p = fmaf(x2, -0.0088632355f, 0.0218694885f);
+    p = fmaf(x2, p, -0.0539682540f);
+    p = fmaf(x2, p, 0.1333333333f);
+    p = fmaf(x2, p, -0.3333333333f);
+    const float small = fmaf(x * x2, p, x);
+    const float e = __expf(2.f * ax);
+    const float big = copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f), x);
+    return ax < 0.25f ? small : big;
+}
+
 __device__ __forceinline__ float act_apply_l(int act, float z) {
-    if (act == ACT_TANH) return tanhf(z);
+    if (act == ACT_TANH) return tanh_fast(z);
     if (act == ACT_RELU) return fmaxf(z, 0.f);
     return z;
 }
@@ -70,6 +86,9 @@ __global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) br[t] = bs + min(16 * t + lr, P.Nn - 1) * LDB;
 
+    // acc[s][t] holds the TRANSPOSED 16x16 tile O^T (MFMA A operand = weight rows n, B operand = data
+    // rows m): lane l, register r = O[m0 + 16s + (l&15)][16t + 4(l>>4) + r], i.e. 4 consecutive output
+    // columns of one row per lane -> float4 epilogue loads/stores.
     f32x4 acc[MS][NT];
 #pragma unroll
     for (int s = 0; s < MS; ++s)
@@ -96,19 +115,19 @@ __global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a_cur[s].x, w[t].x, acc[s][t]);
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].x, a_cur[s].x, acc[s][t]);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a_cur[s].y, w[t].y, acc[s][t]);
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].y, a_cur[s].y, acc[s][t]);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a_cur[s].z, w[t].z, acc[s][t]);
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].z, a_cur[s].z, acc[s][t]);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a_cur[s].w, w[t].w, acc[s][t]);
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].w, a_cur[s].w, acc[s][t]);
         if (more) {
 #pragma unroll
             for (int s = 0; s < MS; ++s) a_cur[s] = a_nxt[s];
@@ -124,35 +143,43 @@ __global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(a[s], w[t], acc[s][t]);
+            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t], a[s], acc[s][t]);
     }
 
     float* O = P.O + c * P.o_cs;
+    const float* H = P.H + c * P.h_cs;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const int n = 16 * t + lr;
-        if (n >= P.ldo) continue;
-        const bool live = n < P.Nn;
-        float bv = 0.f;
-        if (MODE == MODE_FWD && live && P.bias) bv = P.bias[c * P.bias_cs + n];
+        const int n = 16 * t + 4 * lg;           // first of this lane's 4 output columns
+        if (n >= P.ldo) continue;                // ldo is a multiple of 4: groups are all-in or all-out
+        float4 bv = {0.f, 0.f, 0.f, 0.f};
+        if (MODE == MODE_FWD && P.bias) bv = *reinterpret_cast<const float4*>(P.bias + c * P.bias_cs + n);
 #pragma unroll
-        for (int s = 0; s < MS; ++s)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + 16 * s + 4 * lg + r;
-                if (m >= P.M) continue;
-                float o = 0.f;
-                if (live) {
-                    const float v = acc[s][t][r];
-                    if (MODE == MODE_FWD) {
-                        o = act_apply_l(P.act, v + bv);
-                    } else {
-                        const float h = P.H[c * P.h_cs + (int64_t)m * P.ldh + n];
-                        o = v * act_grad_from_out_l(P.act, h);
-                    }
-                }
-                O[(int64_t)m * P.ldo + n] = o;
+        for (int s = 0; s < MS; ++s) {
+            const int m = m0 + 16 * s + lr;
+            if (m >= P.M) continue;
+            float4 o;
+            if (MODE == MODE_FWD) {
+                o.x = act_apply_l(P.act, acc[s][t][0] + bv.x);
+                o.y = act_apply_l(P.act, acc[s][t][1] + bv.y);
+                o.z = act_apply_l(P.act, acc[s][t][2] + bv.z);
+                o.w = act_apply_l(P.act, acc[s][t][3] + bv.w);
+            } else {
+                const float4 h = *reinterpret_cast<const float4*>(H + (int64_t)m * P.ldh + n);
+                o.x = acc[s][t][0] * act_grad_from_out_l(P.act, h.x);
+                o.y = acc[s][t][1] * act_grad_from_out_l(P.act, h.y);
+                o.z = acc[s][t][2] * act_grad_from_out_l(P.act, h.z);
+                o.w = acc[s][t][3] * act_grad_from_out_l(P.act, h.w);
             }
+            // columns in [Nn, ldo) are written as zeros (padding read by the next GEMM)
+            if (n + 3 >= P.Nn) {
+                if (n + 0 >= P.Nn) o.x = 0.f;
+                if (n + 1 >= P.Nn) o.y = 0.f;
+                if (n + 2 >= P.Nn) o.z = 0.f;
+                if (n + 3 >= P.Nn) o.w = 0.f;
+            }
+            *reinterpret_cast<float4*>(O + (int64_t)m * P.ldo + n) = o;
+        }
     }
 }
 
@@ -192,27 +219,49 @@ __global__ __launch_bounds__(64) void k_colsum(ColsumArgs args) {
         for (int t = 0; t < JT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float dsum[2] = {0.f, 0.f};
 
-    for (int m = r0; m < r1; m += 4) {
-        const int mm = m + lg;
-        const bool mok = mm < r1;
-        const int mr = mok ? mm : r0;
-        const float* drow = D + (int64_t)mr * P.ldd;
-        const float* hrow = H + (int64_t)mr * P.ldh;
-        float a[2], h[JT];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const float v = drow[ncol[s]];
-            a[s] = mok ? v : 0.f;
+    // operands for U row-steps of 4 rows are loaded one group ahead (register double buffer) so the
+    // L2 latency of group g+1 hides under the MFMAs of group g
+    constexpr int U = 2;
+    float a_c[U][2], h_c[U][JT], a_n[U][2], h_n[U][JT];
+#define VIHMC_COLSUM_LOAD(M0, AA, HH)                                                          \
+    _Pragma("unroll") for (int u = 0; u < U; ++u) {                                            \
+        const int mm = (M0) + 4 * u + lg;                                                      \
+        const bool mok = mm < r1;                                                              \
+        const int mr = mok ? mm : r0;                                                          \
+        const float* drow = D + (int64_t)mr * P.ldd;                                           \
+        const float* hrow = H + (int64_t)mr * P.ldh;                                           \
+        _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                        \
+            const float v = drow[ncol[s]];                                                     \
+            AA[u][s] = mok ? v : 0.f;                                                          \
+        }                                                                                      \
+        _Pragma("unroll") for (int t = 0; t < JT; ++t) HH[u][t] = hrow[jcol[t]];               \
+    }
+    VIHMC_COLSUM_LOAD(r0, a_c, h_c)
+    for (int m = r0; m < r1; m += 4 * U) {
+        const bool more = m + 4 * U < r1;
+        if (more) {
+            VIHMC_COLSUM_LOAD(m + 4 * U, a_n, h_n)
         }
 #pragma unroll
-        for (int t = 0; t < JT; ++t) h[t] = hrow[jcol[t]];
+        for (int u = 0; u < U; ++u) {
 #pragma unroll
-        for (int t = 0; t < JT; ++t)
+            for (int t = 0; t < JT; ++t)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) acc[s][t] = mfma(a[s], h[t], acc[s][t]);
-        dsum[0] += a[0];
-        dsum[1] += a[1];
+                for (int s = 0; s < 2; ++s) acc[s][t] = mfma(a_c[u][s], h_c[u][t], acc[s][t]);
+            dsum[0] += a_c[u][0];
+            dsum[1] += a_c[u][1];
+        }
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                a_c[u][0] = a_n[u][0];
+                a_c[u][1] = a_n[u][1];
+#pragma unroll
+                for (int t = 0; t < JT; ++t) h_c[u][t] = h_n[u][t];
+            }
+        }
     }
+#undef VIHMC_COLSUM_LOAD
 
     float* part = P.part + c * P.part_cs + (int64_t)chunk * P.part_stride;
 #pragma unroll
