@@ -30,7 +30,9 @@ struct RowdotProb {
     const float* bias; int64_t bias_cs;
     const float* H; int64_t h_cs; int32_t ldh;
     int32_t M, Nn, K, act;
-    int32_t tiles;          // ceil(M / (ROWDOT_WAVES*16*MS)) workgroups per chain
+    int32_t tiles;          // workgroups per chain = ceil(ntiles / tpw)
+    int32_t ntiles;         // ceil(M / (ROWDOT_WAVES*16*MS)) row tiles
+    int32_t tpw;            // row tiles per workgroup (amortises the LDS weight staging)
 };
 struct RowdotArgs {
     RowdotProb p[2];
@@ -52,6 +54,30 @@ struct ColsumArgs {
     ColsumProb p[2];
     int32_t nprob, C;
 };
+
+// ---------------------------------------------------------------------------------------------
+// Fused backward of one linear layer l (grouped branch + trunk):
+//   Dout = (D W) * act'(H)        (D = delta_l [M][ldd], W^T = WT [n_in][ldw], H = h_{l-1} [M][ldh])
+//   part[wg] = D^T H (weight gradient partial) and sum_rows D (bias gradient partial)
+// One 256-thread workgroup per rows_per_wg rows; D and H are staged in LDS in 32-row sub-tiles (read
+// once from HBM for both products), W^T is staged once per workgroup.
+// ---------------------------------------------------------------------------------------------
+constexpr int BWD_SUB = 32;
+constexpr int GATHER_SPLIT_MAX = 16;
+struct BwdProb {
+    const float* D;  int64_t d_cs;  int32_t ldd;
+    const float* WT; int64_t wt_cs; int32_t ldw;
+    const float* H;  int64_t h_cs;  int32_t ldh;
+    float* Dout;     int64_t o_cs;
+    float* part;     int64_t part_cs; int32_t part_stride;
+    int32_t M, n_out, n_in, act, has_dx;
+    int32_t rows_per_wg, n_wg;
+};
+struct BwdArgs {
+    BwdProb p[2];
+    int32_t nprob, C;
+};
+hipError_t launch_bwd(const BwdArgs& a, int nti, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // Fused branch x trunk contraction with the Gaussian likelihood, owner form.
@@ -97,7 +123,7 @@ hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_wa
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
                                const float* prior_mu, const float* prior_inv_var, double prior_const,
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
-                               hipStream_t s);
+                               double* lp_part, hipStream_t s);
 
 // BNN: one wave per chain, everything in registers / LDS.
 struct MlpLayer { int32_t w_off, b_off, n_out, n_in, act; };

@@ -121,16 +121,21 @@ __global__ __launch_bounds__(256) void k_contract_stats(const double* stats, int
     }
 }
 
+// Gradient gather + prior: grid (GATHER_SPLIT slices, C); each block writes its partial log-prior
+// and the last kernel of the pair adds them in a fixed order.
+constexpr int GATHER_SPLIT = 16;
+
 __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap,
                                                       const float* theta, int K, const float* prior_mu,
-                                                      const float* prior_inv_var, double prior_const,
-                                                      float prior_scale, const float* lik, float* logp,
-                                                      float* grad) {
+                                                      const float* prior_inv_var, float prior_scale,
+                                                      float* grad, double* lp_part) {
     __shared__ double sh[8];
-    const int c = blockIdx.x;
+    const int c = blockIdx.y;
+    const int per = (K + gridDim.x - 1) / gridDim.x;
+    const int k0 = blockIdx.x * per, k1 = min(K, k0 + per);
     const float inv_scale = 1.f / prior_scale;
     double lp = 0.0;
-    for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
         const float th = theta[(int64_t)c * K + k];
         const float d = th - prior_mu[k];
         const float iv = prior_inv_var[k];
@@ -138,7 +143,16 @@ __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t g
         if (grad) grad[(int64_t)c * K + k] = gp[c * gp_cs + smap[k]] - d * iv * inv_scale;
     }
     lp = block_sum_256(lp, sh);
-    if (threadIdx.x == 0) logp[c] = (float)((double)lik[c] + (lp + prior_const) / (double)prior_scale);
+    if (threadIdx.x == 0) lp_part[c * gridDim.x + blockIdx.x] = lp;
+}
+
+__global__ void k_logp_finalize(const double* lp_part, int nparts, const float* lik, double prior_const,
+                                float prior_scale, float* logp, int C) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double lp = 0.0;
+    for (int i = 0; i < nparts; ++i) lp += lp_part[c * nparts + i];
+    logp[c] = (float)((double)lik[c] + (lp + prior_const) / (double)prior_scale);
 }
 
 // =============================================================================================
@@ -295,9 +309,13 @@ hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_wa
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
                                const float* prior_mu, const float* prior_inv_var, double prior_const,
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
-                               hipStream_t s) {
-    VIHMC_LAUNCH(k_gather_prior, dim3(C), dim3(256), 0, s, gp, gp_cs, smap, theta, K, prior_mu, prior_inv_var,
-                 prior_const, prior_scale, lik, logp, grad);
+                               double* lp_part, hipStream_t s) {
+    hipLaunchKernelGGL(k_gather_prior, dim3(GATHER_SPLIT, C), dim3(256), 0, s, gp, gp_cs, smap, theta, K, prior_mu,
+                       prior_inv_var, prior_scale, grad, lp_part);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    VIHMC_LAUNCH(k_logp_finalize, dim3((C + 63) / 64), dim3(64), 0, s, lp_part, GATHER_SPLIT, lik, prior_const,
+                 prior_scale, logp, C);
 }
 
 size_t mlp_lds_bytes(int D, int n_layers, int maxw) {

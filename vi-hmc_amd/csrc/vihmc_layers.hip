@@ -51,7 +51,9 @@ __host__ __device__ constexpr int rowdot_ldb(int k4) { return ((k4 / 4) & 1) ? k
 // staged once in LDS and shared; A rows streamed from HBM/L2 as float4 with a one-block register
 // prefetch; MFMAs interleaved over MS*NT independent accumulators.
 // =============================================================================================
-template <int NT, int MS, int MODE>
+// KF > 0: the contraction length is KF for every problem of the launch (hidden 100x100 layers), which
+// makes the k-loop a compile-time loop the compiler can software-pipeline; KF = 0 reads P.K.
+template <int NT, int MS, int MODE, int KF>
 __global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
     extern __shared__ float bs[];
     int b = blockIdx.x;
@@ -60,11 +62,12 @@ __global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
     const RowdotProb P = second ? args.p[1] : args.p[0];
     if (second) b -= first;
     const int c = b / P.tiles;
-    const int tile = b - c * P.tiles;
+    const int grp = b - c * P.tiles;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const float* A = P.A + c * P.a_cs;
     const float* B = P.B + c * P.b_cs;
-    const int K4 = (P.K + 3) & ~3;
+    const int KK = KF > 0 ? KF : P.K;
+    const int K4 = (KK + 3) & ~3;
     const int LDB = rowdot_ldb(K4);
 
     // stage B (rows n < Nn, K4 floats each; global row stride ldb >= K4, zero padded)
@@ -78,108 +81,114 @@ __global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
         }
     }
 
-    const int m0 = tile * (ROWDOT_WAVES * 16 * MS) + wave * 16 * MS;
-    const float* ar[MS];
-#pragma unroll
-    for (int s = 0; s < MS; ++s) ar[s] = A + (int64_t)min(m0 + 16 * s + lr, P.M - 1) * P.lda;
-    const float* br[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) br[t] = bs + min(16 * t + lr, P.Nn - 1) * LDB;
-
-    // acc[s][t] holds the TRANSPOSED 16x16 tile O^T (MFMA A operand = weight rows n, B operand = data
-    // rows m): lane l, register r = O[m0 + 16s + (l&15)][16t + 4(l>>4) + r], i.e. 4 consecutive output
-    // columns of one row per lane -> float4 epilogue loads/stores.
-    f32x4 acc[MS][NT];
-#pragma unroll
-    for (int s = 0; s < MS; ++s)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int kfull = P.K & ~15;
-    float4 a_cur[MS];
-    if (kfull > 0) {
-#pragma unroll
-        for (int s = 0; s < MS; ++s) a_cur[s] = *reinterpret_cast<const float4*>(ar[s] + 4 * lg);
-    }
     __syncthreads();
-    for (int kb = 0; kb < kfull; kb += 16) {
-        float4 a_nxt[MS];
-        const bool more = kb + 16 < kfull;
-        if (more) {
+    // the staged weights serve tpw consecutive 4-wave row tiles
+    for (int tile = grp * P.tpw; tile < (grp + 1) * P.tpw; ++tile) {
+        const int m0 = tile * (ROWDOT_WAVES * 16 * MS) + wave * 16 * MS;
+        if (tile >= P.ntiles) break;
+        const float* ar[MS];
 #pragma unroll
-            for (int s = 0; s < MS; ++s) a_nxt[s] = *reinterpret_cast<const float4*>(ar[s] + kb + 16 + 4 * lg);
-        }
-        float4 w[NT];
+        for (int s = 0; s < MS; ++s) ar[s] = A + (int64_t)min(m0 + 16 * s + lr, P.M - 1) * P.lda;
+        const float* br[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) w[t] = *reinterpret_cast<const float4*>(br[t] + kb + 4 * lg);
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].x, a_cur[s].x, acc[s][t]);
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].y, a_cur[s].y, acc[s][t]);
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].z, a_cur[s].z, acc[s][t]);
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].w, a_cur[s].w, acc[s][t]);
-        if (more) {
-#pragma unroll
-            for (int s = 0; s < MS; ++s) a_cur[s] = a_nxt[s];
-        }
-    }
-    // tail: K rounded up to 4 (operand padding columns are zero)
-    for (int kb = kfull; kb < K4; kb += 4) {
-        float a[MS], w[NT];
-#pragma unroll
-        for (int s = 0; s < MS; ++s) a[s] = ar[s][kb + lg];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) w[t] = br[t][kb + lg];
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t], a[s], acc[s][t]);
-    }
+        for (int t = 0; t < NT; ++t) br[t] = bs + min(16 * t + lr, P.Nn - 1) * LDB;
 
-    float* O = P.O + c * P.o_cs;
-    const float* H = P.H + c * P.h_cs;
+        // acc[s][t] holds the TRANSPOSED 16x16 tile O^T (MFMA A operand = weight rows n, B operand = data
+        // rows m): lane l, register r = O[m0 + 16s + (l&15)][16t + 4(l>>4) + r], i.e. 4 consecutive output
+        // columns of one row per lane -> float4 epilogue loads/stores.
+        f32x4 acc[MS][NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int n = 16 * t + 4 * lg;           // first of this lane's 4 output columns
-        if (n >= P.ldo) continue;                // ldo is a multiple of 4: groups are all-in or all-out
-        float4 bv = {0.f, 0.f, 0.f, 0.f};
-        if (MODE == MODE_FWD && P.bias) bv = *reinterpret_cast<const float4*>(P.bias + c * P.bias_cs + n);
+        for (int s = 0; s < MS; ++s)
 #pragma unroll
-        for (int s = 0; s < MS; ++s) {
-            const int m = m0 + 16 * s + lr;
-            if (m >= P.M) continue;
-            float4 o;
-            if (MODE == MODE_FWD) {
-                o.x = act_apply_l(P.act, acc[s][t][0] + bv.x);
-                o.y = act_apply_l(P.act, acc[s][t][1] + bv.y);
-                o.z = act_apply_l(P.act, acc[s][t][2] + bv.z);
-                o.w = act_apply_l(P.act, acc[s][t][3] + bv.w);
-            } else {
-                const float4 h = *reinterpret_cast<const float4*>(H + (int64_t)m * P.ldh + n);
-                o.x = acc[s][t][0] * act_grad_from_out_l(P.act, h.x);
-                o.y = acc[s][t][1] * act_grad_from_out_l(P.act, h.y);
-                o.z = acc[s][t][2] * act_grad_from_out_l(P.act, h.z);
-                o.w = acc[s][t][3] * act_grad_from_out_l(P.act, h.w);
-            }
-            // columns in [Nn, ldo) are written as zeros (padding read by the next GEMM)
-            if (n + 3 >= P.Nn) {
-                if (n + 0 >= P.Nn) o.x = 0.f;
-                if (n + 1 >= P.Nn) o.y = 0.f;
-                if (n + 2 >= P.Nn) o.z = 0.f;
-                if (n + 3 >= P.Nn) o.w = 0.f;
-            }
-            *reinterpret_cast<float4*>(O + (int64_t)m * P.ldo + n) = o;
+            for (int t = 0; t < NT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+        const int kfull = KK & ~15;
+        float4 a_cur[MS];
+        if (kfull > 0) {
+#pragma unroll
+            for (int s = 0; s < MS; ++s) a_cur[s] = *reinterpret_cast<const float4*>(ar[s] + 4 * lg);
         }
+#pragma unroll
+        for (int kb = 0; kb < kfull; kb += 16) {
+            float4 a_nxt[MS];
+            const bool more = kb + 16 < kfull;
+            if (more) {
+#pragma unroll
+                for (int s = 0; s < MS; ++s) a_nxt[s] = *reinterpret_cast<const float4*>(ar[s] + kb + 16 + 4 * lg);
+            }
+            float4 w[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) w[t] = *reinterpret_cast<const float4*>(br[t] + kb + 4 * lg);
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].x, a_cur[s].x, acc[s][t]);
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].y, a_cur[s].y, acc[s][t]);
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].z, a_cur[s].z, acc[s][t]);
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].w, a_cur[s].w, acc[s][t]);
+            if (more) {
+#pragma unroll
+                for (int s = 0; s < MS; ++s) a_cur[s] = a_nxt[s];
+            }
+        }
+        // tail: K rounded up to 4 (operand padding columns are zero)
+        for (int kb = kfull; kb < K4; kb += 4) {
+            float a[MS], w[NT];
+#pragma unroll
+            for (int s = 0; s < MS; ++s) a[s] = ar[s][kb + lg];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) w[t] = br[t][kb + lg];
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+#pragma unroll
+                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t], a[s], acc[s][t]);
+        }
+
+        float* O = P.O + c * P.o_cs;
+        const float* H = P.H + c * P.h_cs;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int n = 16 * t + 4 * lg;           // first of this lane's 4 output columns
+            if (n >= P.ldo) continue;                // ldo is a multiple of 4: groups are all-in or all-out
+            float4 bv = {0.f, 0.f, 0.f, 0.f};
+            if (MODE == MODE_FWD && P.bias) bv = *reinterpret_cast<const float4*>(P.bias + c * P.bias_cs + n);
+#pragma unroll
+            for (int s = 0; s < MS; ++s) {
+                const int m = m0 + 16 * s + lr;
+                if (m >= P.M) continue;
+                float4 o;
+                if (MODE == MODE_FWD) {
+                    o.x = act_apply_l(P.act, acc[s][t][0] + bv.x);
+                    o.y = act_apply_l(P.act, acc[s][t][1] + bv.y);
+                    o.z = act_apply_l(P.act, acc[s][t][2] + bv.z);
+                    o.w = act_apply_l(P.act, acc[s][t][3] + bv.w);
+                } else {
+                    const float4 h = *reinterpret_cast<const float4*>(H + (int64_t)m * P.ldh + n);
+                    o.x = acc[s][t][0] * act_grad_from_out_l(P.act, h.x);
+                    o.y = acc[s][t][1] * act_grad_from_out_l(P.act, h.y);
+                    o.z = acc[s][t][2] * act_grad_from_out_l(P.act, h.z);
+                    o.w = acc[s][t][3] * act_grad_from_out_l(P.act, h.w);
+                }
+                // columns in [Nn, ldo) are written as zeros (padding read by the next GEMM)
+                if (n + 3 >= P.Nn) {
+                    if (n + 0 >= P.Nn) o.x = 0.f;
+                    if (n + 1 >= P.Nn) o.y = 0.f;
+                    if (n + 2 >= P.Nn) o.z = 0.f;
+                    if (n + 3 >= P.Nn) o.w = 0.f;
+                }
+                *reinterpret_cast<float4*>(O + (int64_t)m * P.ldo + n) = o;
+            }
+        }
+
     }
 }
 
@@ -288,6 +297,193 @@ __global__ __launch_bounds__(64) void k_colsum(ColsumArgs args) {
 
 
 // =============================================================================================
+// Fused layer backward (see BwdProb): per 32-row sub-tile, delta_l and h_{l-1} are staged once in LDS
+// (register prefetch of the next sub-tile while the current one is consumed) and feed both
+//   dX : Dout = (delta W) * act'(h)   -- waves split 2 row halves x 2 column-tile parities, transposed
+//        accumulators (4 consecutive output columns per lane, float4 epilogue, h read from LDS)
+//   dW : part += delta^T h, db += sum delta -- wave w owns output rows n in subtiles {2w, 2w+1}
+// W^T is staged once per workgroup. Deterministic: every partial slab has exactly one writer.
+// =============================================================================================
+template <int NTI, int KF>
+__global__ __launch_bounds__(256, 2) void k_bwd_fused(BwdArgs args) {
+    constexpr int NU = (NTI + 1) / 2;          // dX column tiles per wave (parity split)
+    extern __shared__ float sm[];
+    int b = blockIdx.x;
+    const int per0 = args.C * args.p[0].n_wg;
+    const bool second = b >= per0;
+    const BwdProb P = second ? args.p[1] : args.p[0];
+    if (second) b -= per0;
+    const int c = b / P.n_wg;
+    const int wg = b - c * P.n_wg;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int n_out = KF > 0 ? KF : P.n_out;
+    const int NO4 = (n_out + 3) & ~3, NI4 = (P.n_in + 3) & ~3;
+    const int LDW = rowdot_ldb(NO4), LDT = rowdot_ldb(NO4), LDH = rowdot_ldb(NI4);
+    float* wt = sm;
+    float* dt = wt + (P.has_dx ? P.n_in * LDW : 0);
+    float* ht = dt + BWD_SUB * LDT;
+    const float* D = P.D + c * P.d_cs;
+    const float* H = P.H + c * P.h_cs;
+    const int r0 = wg * P.rows_per_wg;
+    const int r1 = min(P.M, r0 + P.rows_per_wg);
+
+    if (P.has_dx) {
+        const float* WT = P.WT + c * P.wt_cs;
+        const int q4 = NO4 >> 2, n4 = P.n_in * q4;
+        for (int i = tid; i < n4; i += 256) {
+            const int r = i / q4, c4 = i - r * q4;
+            reinterpret_cast<float4*>(wt + r * LDW)[c4] = reinterpret_cast<const float4*>(WT + (int64_t)r * P.ldw)[c4];
+        }
+    }
+
+    // sub-tile staging: delta rows (NO4/4 float4 each) then h rows (NI4/4 float4 each); <= 8 per thread
+    const int dq4 = NO4 >> 2, hq4 = NI4 >> 2;
+    const int nd4 = BWD_SUB * dq4, ntot = nd4 + BWD_SUB * hq4;
+    float4 pf[8];
+#define VIHMC_BWD_LOAD(SUB)                                                                         \
+    _Pragma("unroll") for (int v = 0; v < 8; ++v) {                                                 \
+        const int idx = min(tid + 256 * v, ntot - 1);                                               \
+        const bool isd = idx < nd4;                                                                 \
+        const int e = isd ? idx : idx - nd4;                                                        \
+        const int q = isd ? dq4 : hq4;                                                              \
+        const int r = e / q, c4 = e - r * q;                                                        \
+        const int row = min((SUB) + r, P.M - 1);                                                    \
+        const float* src = isd ? D + (int64_t)row * P.ldd : H + (int64_t)row * P.ldh;               \
+        pf[v] = reinterpret_cast<const float4*>(src)[c4];                                           \
+    }
+#define VIHMC_BWD_STORE(SUB)                                                                        \
+    _Pragma("unroll") for (int v = 0; v < 8; ++v) {                                                 \
+        const int idx = tid + 256 * v;                                                              \
+        if (idx < ntot) {                                                                           \
+            const bool isd = idx < nd4;                                                             \
+            const int e = isd ? idx : idx - nd4;                                                    \
+            const int q = isd ? dq4 : hq4;                                                          \
+            const int r = e / q, c4 = e - r * q;                                                    \
+            const float4 val = ((SUB) + r < r1) ? pf[v] : float4{0.f, 0.f, 0.f, 0.f};               \
+            reinterpret_cast<float4*>(isd ? dt + r * LDT : ht + r * LDH)[c4] = val;                 \
+        }                                                                                           \
+    }
+
+    // dW accumulators: this wave's two 16-row output subtiles of dW
+    const int ns0 = 2 * wave, ns1 = 2 * wave + 1;
+    const bool dw0 = 16 * ns0 < P.n_out, dw1 = 16 * ns1 < P.n_out;
+    f32x4 acc_w[2][NTI];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < NTI; ++t) acc_w[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dsum[2] = {0.f, 0.f};
+    const int ncol0 = min(16 * ns0 + lr, P.n_out - 1), ncol1 = min(16 * ns1 + lr, P.n_out - 1);
+    int jcol[NTI];
+#pragma unroll
+    for (int t = 0; t < NTI; ++t) jcol[t] = min(16 * t + lr, P.n_in - 1);
+    // dX geometry
+    const int xh = wave & 1, xpar = wave >> 1;
+    const int kfull = n_out & ~15;
+
+    if (r0 < r1) {
+        VIHMC_BWD_LOAD(r0)
+    }
+    for (int sub = r0; sub < r1; sub += BWD_SUB) {
+        VIHMC_BWD_STORE(sub)
+        __syncthreads();
+        if (sub + BWD_SUB < r1) {
+            VIHMC_BWD_LOAD(sub + BWD_SUB)
+        }
+        if (P.has_dx) {
+            f32x4 acc_x[NU];
+#pragma unroll
+            for (int u = 0; u < NU; ++u) acc_x[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const float4* drow = reinterpret_cast<const float4*>(dt + (16 * xh + lr) * LDT);
+            const float* wrow[NU];
+#pragma unroll
+            for (int u = 0; u < NU; ++u) wrow[u] = wt + min(16 * (2 * u + xpar) + lr, P.n_in - 1) * LDW;
+#pragma unroll
+            for (int kb = 0; kb < kfull; kb += 16) {
+                const float4 dv = drow[(kb >> 2) + lg];
+                float4 wv[NU];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) wv[u] = reinterpret_cast<const float4*>(wrow[u])[(kb >> 2) + lg];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].x, dv.x, acc_x[u]);
+#pragma unroll
+                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].y, dv.y, acc_x[u]);
+#pragma unroll
+                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].z, dv.z, acc_x[u]);
+#pragma unroll
+                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].w, dv.w, acc_x[u]);
+            }
+            for (int kb = kfull; kb < NO4; kb += 4) {
+                const float dv = dt[(16 * xh + lr) * LDT + kb + lg];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wrow[u][kb + lg], dv, acc_x[u]);
+            }
+            const int m = sub + 16 * xh + lr;
+            if (m < r1) {
+                const float* hrow = ht + (16 * xh + lr) * LDH;
+                float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const int i = 16 * (2 * u + xpar) + 4 * lg;
+                    if (2 * u + xpar >= NTI || i >= NI4) continue;
+                    const float4 h = reinterpret_cast<const float4*>(hrow)[i >> 2];
+                    float4 o;
+                    o.x = (i + 0 < P.n_in) ? acc_x[u][0] * act_grad_from_out_l(P.act, h.x) : 0.f;
+                    o.y = (i + 1 < P.n_in) ? acc_x[u][1] * act_grad_from_out_l(P.act, h.y) : 0.f;
+                    o.z = (i + 2 < P.n_in) ? acc_x[u][2] * act_grad_from_out_l(P.act, h.z) : 0.f;
+                    o.w = (i + 3 < P.n_in) ? acc_x[u][3] * act_grad_from_out_l(P.act, h.w) : 0.f;
+                    reinterpret_cast<float4*>(orow)[i >> 2] = o;
+                }
+            }
+        }
+        if (dw0) {
+#pragma unroll 2
+            for (int mm = 0; mm < BWD_SUB; mm += 4) {
+                const float* drw = dt + (mm + lg) * LDT;
+                const float* hrw = ht + (mm + lg) * LDH;
+                const float a0 = drw[ncol0];
+                const float a1 = dw1 ? drw[ncol1] : 0.f;
+                float hv[NTI];
+#pragma unroll
+                for (int t = 0; t < NTI; ++t) hv[t] = hrw[jcol[t]];
+#pragma unroll
+                for (int t = 0; t < NTI; ++t) {
+                    acc_w[0][t] = mfma(a0, hv[t], acc_w[0][t]);
+                    acc_w[1][t] = mfma(a1, hv[t], acc_w[1][t]);
+                }
+                dsum[0] += a0;
+                dsum[1] += a1;
+            }
+        }
+        __syncthreads();
+    }
+#undef VIHMC_BWD_LOAD
+#undef VIHMC_BWD_STORE
+
+    if (!dw0) return;
+    float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int ns = s == 0 ? ns0 : ns1;
+#pragma unroll
+        for (int t = 0; t < NTI; ++t) {
+            const int j = 16 * t + lr;
+            if (j >= NI4) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = 16 * ns + 4 * lg + r;
+                if (n < P.n_out) part[(int64_t)n * NI4 + j] = (j < P.n_in) ? acc_w[s][t][r] : 0.f;
+            }
+        }
+        float v = dsum[s];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        const int n = 16 * ns + lr;
+        if (lg == 0 && n < P.n_out) part[(int64_t)P.n_out * NI4 + n] = v;
+    }
+}
+
+// =============================================================================================
 // launchers
 // =============================================================================================
 #define VIHMC_LAUNCH_L(kern, grid, block, shm, s, ...) \
@@ -307,15 +503,17 @@ static hipError_t rowdot_nt(const RowdotArgs& a, int nt, hipStream_t s) {
     const int blocks = a.C * a.p[0].tiles + (a.nprob > 1 ? a.C * a.p[1].tiles : 0);
     const size_t shm = rowdot_lds_bytes(a);
     dim3 g(blocks), blk(256);
+    const bool k100 = a.p[0].K == 100 && (a.nprob < 2 || a.p[1].K == 100);
+    if (k100 && nt == 7) VIHMC_LAUNCH_L((k_rowdot2<7, MS, MODE, 100>), g, blk, shm, s, a);
     switch (nt) {
-        case 1: VIHMC_LAUNCH_L((k_rowdot2<1, MS, MODE>), g, blk, shm, s, a);
-        case 2: VIHMC_LAUNCH_L((k_rowdot2<2, MS, MODE>), g, blk, shm, s, a);
-        case 3: VIHMC_LAUNCH_L((k_rowdot2<3, MS, MODE>), g, blk, shm, s, a);
-        case 4: VIHMC_LAUNCH_L((k_rowdot2<4, MS, MODE>), g, blk, shm, s, a);
-        case 5: VIHMC_LAUNCH_L((k_rowdot2<5, MS, MODE>), g, blk, shm, s, a);
-        case 6: VIHMC_LAUNCH_L((k_rowdot2<6, MS, MODE>), g, blk, shm, s, a);
-        case 7: VIHMC_LAUNCH_L((k_rowdot2<7, MS, MODE>), g, blk, shm, s, a);
-        case 8: VIHMC_LAUNCH_L((k_rowdot2<8, MS, MODE>), g, blk, shm, s, a);
+        case 1: VIHMC_LAUNCH_L((k_rowdot2<1, MS, MODE, 0>), g, blk, shm, s, a);
+        case 2: VIHMC_LAUNCH_L((k_rowdot2<2, MS, MODE, 0>), g, blk, shm, s, a);
+        case 3: VIHMC_LAUNCH_L((k_rowdot2<3, MS, MODE, 0>), g, blk, shm, s, a);
+        case 4: VIHMC_LAUNCH_L((k_rowdot2<4, MS, MODE, 0>), g, blk, shm, s, a);
+        case 5: VIHMC_LAUNCH_L((k_rowdot2<5, MS, MODE, 0>), g, blk, shm, s, a);
+        case 6: VIHMC_LAUNCH_L((k_rowdot2<6, MS, MODE, 0>), g, blk, shm, s, a);
+        case 7: VIHMC_LAUNCH_L((k_rowdot2<7, MS, MODE, 0>), g, blk, shm, s, a);
+        case 8: VIHMC_LAUNCH_L((k_rowdot2<8, MS, MODE, 0>), g, blk, shm, s, a);
         default: return hipErrorInvalidValue;
     }
 }
@@ -323,6 +521,37 @@ static hipError_t rowdot_nt(const RowdotArgs& a, int nt, hipStream_t s) {
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s) {
     if (ms == 1) return mode == MODE_FWD ? rowdot_nt<1, MODE_FWD>(a, nt, s) : rowdot_nt<1, MODE_BWD>(a, nt, s);
     return mode == MODE_FWD ? rowdot_nt<2, MODE_FWD>(a, nt, s) : rowdot_nt<2, MODE_BWD>(a, nt, s);
+}
+
+size_t bwd_lds_bytes(const BwdArgs& a) {
+    size_t m = 0;
+    for (int i = 0; i < a.nprob; ++i) {
+        const BwdProb& p = a.p[i];
+        const int no4 = (p.n_out + 3) & ~3, ni4 = (p.n_in + 3) & ~3;
+        const size_t f = (size_t)(p.has_dx ? p.n_in * rowdot_ldb(no4) : 0) + (size_t)BWD_SUB * rowdot_ldb(no4) +
+                         (size_t)BWD_SUB * rowdot_ldb(ni4);
+        m = std::max(m, f * sizeof(float));
+    }
+    return m;
+}
+
+hipError_t launch_bwd(const BwdArgs& a, int nti, hipStream_t s) {
+    const int blocks = a.C * a.p[0].n_wg + (a.nprob > 1 ? a.C * a.p[1].n_wg : 0);
+    const size_t shm = bwd_lds_bytes(a);
+    dim3 g(blocks), blk(256);
+    const bool k100 = a.p[0].n_out == 100 && (a.nprob < 2 || a.p[1].n_out == 100);
+    if (k100 && nti == 7) VIHMC_LAUNCH_L((k_bwd_fused<7, 100>), g, blk, shm, s, a);
+    switch (nti) {
+        case 1: VIHMC_LAUNCH_L((k_bwd_fused<1, 0>), g, blk, shm, s, a);
+        case 2: VIHMC_LAUNCH_L((k_bwd_fused<2, 0>), g, blk, shm, s, a);
+        case 3: VIHMC_LAUNCH_L((k_bwd_fused<3, 0>), g, blk, shm, s, a);
+        case 4: VIHMC_LAUNCH_L((k_bwd_fused<4, 0>), g, blk, shm, s, a);
+        case 5: VIHMC_LAUNCH_L((k_bwd_fused<5, 0>), g, blk, shm, s, a);
+        case 6: VIHMC_LAUNCH_L((k_bwd_fused<6, 0>), g, blk, shm, s, a);
+        case 7: VIHMC_LAUNCH_L((k_bwd_fused<7, 0>), g, blk, shm, s, a);
+        case 8: VIHMC_LAUNCH_L((k_bwd_fused<8, 0>), g, blk, shm, s, a);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_colsum(const ColsumArgs& a, int jt, hipStream_t s) {

@@ -79,6 +79,7 @@ struct vihmc_plan {
     float* prior_iv = nullptr;
     double prior_const = 0.0;
     float* lik_buf = nullptr;
+    double* lp_part = nullptr;            // [maxC][GATHER_SPLIT_MAX] partial log-priors
 
     // DeepONet
     int N = 0, P = 0, W = 0, ldz = 0;
@@ -344,6 +345,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         p->stats_cs = 2 * (int64_t)p->nwavesA;
         if (int rc = p->alloc(&p->stats, p->stats_cs * C)) return rc;
         if (int rc = p->alloc(&p->lik_buf, C)) return rc;
+        if (int rc = p->alloc(&p->lp_part, (int64_t)C * GATHER_SPLIT_MAX)) return rc;
     }
     // reduce jobs
     {
@@ -393,6 +395,13 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
 
 inline int nt_of(int n) { return (n + 15) / 16; }
 
+// row tiles per row-dot workgroup: amortise the weight staging while keeping >= ~3 workgroups per CU
+inline int rowdot_tpw(int ntiles, int C) {
+    int t = 1;
+    while (t < 4 && (int64_t)C * cdiv(ntiles, 2 * t) >= 768) t *= 2;
+    return t;
+}
+
 // Forward through both MLPs (grouped launches: branch + trunk layer j together).
 int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
     const int maxl = (int)std::max(p->nets[0].L.size(), p->nets[1].L.size());
@@ -426,7 +435,9 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
             q.Nn = L.n_out;
             q.K = L.n_in;
             q.act = L.act;
-            q.tiles = cdiv(n.rows, ROWDOT_WAVES * 16 * ms);
+            q.ntiles = cdiv(n.rows, ROWDOT_WAVES * 16 * ms);
+            q.tpw = rowdot_tpw(q.ntiles, C);
+            q.tiles = cdiv(q.ntiles, q.tpw);
             nt = std::max(nt, nt_of(L.n_out));
         }
         if (a.nprob == 1) a.p[1] = a.p[0];
@@ -524,73 +535,45 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s));
         if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 1, p->lenA, C, s));
 
-        // backward through both MLPs, last layer first
+        // backward through both MLPs, last layer first: one fused launch per layer (branch + trunk
+        // grouped) computes delta_{l-1} and the dW / db partial slabs
         int cur[2] = {0, 0};
         const int maxl = (int)std::max(b.L.size(), t.L.size());
         for (int i = 0; i < maxl; ++i) {
-            ColsumArgs ca{};
-            ca.C = C;
-            RowdotArgs ra{};
-            ra.C = C;
-            int jt = 1, nt = 1;
-            int64_t wgs = 0;
-            for (int net = 0; net < 2; ++net) {
-                Net& n = p->nets[net];
-                const int j = (int)n.L.size() - 1 - i;
-                if (j >= 1) wgs += (int64_t)C * cdiv(n.rows, ROWDOT_WAVES * 32);
-            }
-            const int ms = wgs >= 512 ? 2 : 1;
+            BwdArgs ba{};
+            ba.C = C;
+            int nti = 1;
             for (int net = 0; net < 2; ++net) {
                 Net& n = p->nets[net];
                 const int j = (int)n.L.size() - 1 - i;
                 if (j < 0) continue;
                 const LayerPk& L = n.L[j];
-                ColsumProb& c = ca.p[ca.nprob++];
-                c.D = n.delta[cur[net]];
-                c.d_cs = n.delta_cs;
-                c.ldd = L.ldo;
-                c.H = j == 0 ? n.input : n.act + n.h_off[j - 1];
-                c.h_cs = j == 0 ? 0 : n.act_cs;
-                c.ldh = L.ldi;
-                c.part = n.dwpart + L.part_off;
-                c.part_cs = n.dwpart_cs;
-                c.M = n.rows;
-                c.n_out = L.n_out;
-                c.n_in = L.n_in;
-                c.rows_per_chunk = n.rows_per_chunk;
-                c.n_chunks = L.n_chunks;
-                c.n_pairs = cdiv(L.n_out, 32);
-                c.part_stride = (int32_t)L.part_stride;
-                jt = std::max(jt, nt_of(L.n_in));
-                if (j >= 1) {
-                    const LayerPk& Lp = n.L[j - 1];
-                    RowdotProb& r = ra.p[ra.nprob++];
-                    r.A = n.delta[cur[net]];
-                    r.a_cs = n.delta_cs;
-                    r.lda = L.ldo;
-                    r.B = p->packed + L.wt;
-                    r.b_cs = p->dp;
-                    r.ldb = L.ldo;
-                    r.O = n.delta[cur[net] ^ 1];
-                    r.o_cs = n.delta_cs;
-                    r.ldo = Lp.ldo;
-                    r.H = n.act + n.h_off[j - 1];
-                    r.h_cs = n.act_cs;
-                    r.ldh = Lp.ldo;
-                    r.M = n.rows;
-                    r.Nn = L.n_in;
-                    r.K = L.n_out;
-                    r.act = Lp.act;
-                    r.tiles = cdiv(n.rows, ROWDOT_WAVES * 16 * ms);
-                    nt = std::max(nt, nt_of(L.n_in));
-                }
+                BwdProb& q = ba.p[ba.nprob++];
+                q.D = n.delta[cur[net]];
+                q.d_cs = n.delta_cs;
+                q.ldd = L.ldo;
+                q.WT = p->packed + L.wt;
+                q.wt_cs = p->dp;
+                q.ldw = L.ldo;
+                q.H = j == 0 ? n.input : n.act + n.h_off[j - 1];
+                q.h_cs = j == 0 ? 0 : n.act_cs;
+                q.ldh = L.ldi;
+                q.Dout = n.delta[cur[net] ^ 1];
+                q.o_cs = n.delta_cs;
+                q.part = n.dwpart + L.part_off;
+                q.part_cs = n.dwpart_cs;
+                q.part_stride = (int32_t)L.part_stride;
+                q.M = n.rows;
+                q.n_out = L.n_out;
+                q.n_in = L.n_in;
+                q.act = j >= 1 ? n.L[j - 1].act : 0;
+                q.has_dx = j >= 1;
+                q.rows_per_wg = n.rows_per_chunk;
+                q.n_wg = L.n_chunks;
+                nti = std::max(nti, nt_of(L.n_in));
             }
-            if (ca.nprob == 1) ca.p[1] = ca.p[0];
-            HIPCHK(launch_colsum(ca, jt, s));
-            if (ra.nprob > 0) {
-                if (ra.nprob == 1) ra.p[1] = ra.p[0];
-                HIPCHK(launch_rowdot(ra, nt, ms, MODE_BWD, s));
-            }
+            if (ba.nprob == 1) ba.p[1] = ba.p[0];
+            HIPCHK(launch_bwd(ba, nti, s));
             for (int net = 0; net < 2; ++net) {
                 const int j = (int)p->nets[net].L.size() - 1 - i;
                 if (j >= 1) cur[net] ^= 1;
@@ -599,7 +582,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         HIPCHK(launch_reduce(p->jobsW, p->n_jobsW, p->max_lenW, C, s));
     }
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
-                               p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, s));
+                               p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, s));
     return 0;
 }
 
