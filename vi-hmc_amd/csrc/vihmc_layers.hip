@@ -42,9 +42,12 @@ __device__ __forceinline__ float act_grad_from_out_l(int act, float h) {
     return 1.f;
 }
 
-// LDS row stride for the staged weight block: stride/4 odd keeps 16 consecutive-row b128 reads on
-// 16 distinct 4-bank groups.
-__host__ __device__ constexpr int rowdot_ldb(int k4) { return ((k4 / 4) & 1) ? k4 : k4 + 4; }
+// LDS row stride (floats) for row-major operand images read by the MFMA k-permuted float4 pattern
+// (lane l reads row l&15, float4 column kb/4 + (l>>4)). ds_read_b128 services the lanes in the groups
+// {0-3,12-15,20-27} and {4-11,16-19,28-31} (+32); a stride == 8 (mod 16) puts the 16 lanes of each
+// group on 16 distinct 4-bank groups (stride/4 odd alone leaves the lg=0/lg=1 halves 2-way; exhaustive
+// check in DESIGN.md section 4). 100 -> 104.
+__host__ __device__ constexpr int rowdot_ldb(int k4) { return k4 + ((24 - (k4 & 15)) & 15); }
 
 // =============================================================================================
 // Row-dot GEMM v2: 256-thread workgroup = 4 waves x 16*MS rows, the whole weight block B [Nn x K]
@@ -297,15 +300,22 @@ __global__ __launch_bounds__(64) void k_colsum(ColsumArgs args) {
 
 
 // =============================================================================================
-// Fused layer backward (see BwdProb): per 32-row sub-tile, delta_l and h_{l-1} are staged once in LDS
-// (register prefetch of the next sub-tile while the current one is consumed) and feed both
-//   dX : Dout = (delta W) * act'(h)   -- waves split 2 row halves x 2 column-tile parities, transposed
-//        accumulators (4 consecutive output columns per lane, float4 epilogue, h read from LDS)
-//   dW : part += delta^T h, db += sum delta -- wave w owns output rows n in subtiles {2w, 2w+1}
-// W^T is staged once per workgroup. Deterministic: every partial slab has exactly one writer.
+// Fused layer backward (see BwdProb), wave-specialised: a 512-thread workgroup = 4 dX waves + 4 dW
+// waves sharing one LDS image of W^T (staged once) and of each 32-row sub-tile of delta_l and h_{l-1}
+// (register prefetch of the next sub-tile by all 8 waves while the current one is consumed).
+//   dX waves : Dout = (delta W) * act'(h) -- 2 row halves x 2 column-tile parities, transposed
+//              accumulators (4 consecutive output columns per lane, float4 epilogue, h from LDS)
+//   dW waves : part += delta^T h, db += sum delta -- wave w owns output rows n in subtiles {2w, 2w+1};
+//              the 2 + NTI operands of step i+1 are read from LDS while the 2*NTI MFMAs of step i run
+// Splitting the roles keeps each wave under 128 VGPRs (4 waves/SIMD at 2 workgroups/CU), which is what
+// lets the LDS latency hide; the single-role v1 kernel needed 233 and serialised read -> wait -> MFMA.
+// Deterministic: every partial slab has exactly one writer.
 // =============================================================================================
+constexpr int BWD_THREADS = 512;
+constexpr int BWD_SLOTS = 4;   // staged float4 per thread per sub-tile (2 x 32 rows x <= 32 float4)
+
 template <int NTI, int KF>
-__global__ __launch_bounds__(256, 2) void k_bwd_fused(BwdArgs args) {
+__global__ __launch_bounds__(BWD_THREADS, 4) void k_bwd_ws(BwdArgs args) {
     constexpr int NU = (NTI + 1) / 2;          // dX column tiles per wave (parity split)
     extern __shared__ float sm[];
     int b = blockIdx.x;
@@ -316,6 +326,8 @@ __global__ __launch_bounds__(256, 2) void k_bwd_fused(BwdArgs args) {
     const int c = b / P.n_wg;
     const int wg = b - c * P.n_wg;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const bool xrole = wave < 4;
+    const int rw = wave & 3;
     const int n_out = KF > 0 ? KF : P.n_out;
     const int NO4 = (n_out + 3) & ~3, NI4 = (P.n_in + 3) & ~3;
     const int LDW = rowdot_ldb(NO4), LDT = rowdot_ldb(NO4), LDH = rowdot_ldb(NI4);
@@ -330,122 +342,149 @@ __global__ __launch_bounds__(256, 2) void k_bwd_fused(BwdArgs args) {
     if (P.has_dx) {
         const float* WT = P.WT + c * P.wt_cs;
         const int q4 = NO4 >> 2, n4 = P.n_in * q4;
-        for (int i = tid; i < n4; i += 256) {
+        for (int i = tid; i < n4; i += BWD_THREADS) {
             const int r = i / q4, c4 = i - r * q4;
             reinterpret_cast<float4*>(wt + r * LDW)[c4] = reinterpret_cast<const float4*>(WT + (int64_t)r * P.ldw)[c4];
         }
     }
 
-    // sub-tile staging: delta rows (NO4/4 float4 each) then h rows (NI4/4 float4 each); <= 8 per thread
+    // staging geometry (identical for every sub-tile): slot v of this thread moves one float4 of a delta
+    // (bit v of st_d) or h row
     const int dq4 = NO4 >> 2, hq4 = NI4 >> 2;
     const int nd4 = BWD_SUB * dq4, ntot = nd4 + BWD_SUB * hq4;
-    float4 pf[8];
+    float4 pf[BWD_SLOTS];
+    int st[BWD_SLOTS];         // (row << 8) | float4 column, -1 = idle slot
+    unsigned st_d = 0;         // bit v: slot v stages delta (else h)
+#pragma unroll
+    for (int v = 0; v < BWD_SLOTS; ++v) {
+        const int idx = tid + BWD_THREADS * v;
+        const bool isd = idx < nd4;
+        const int e = isd ? idx : idx - nd4;
+        const int q = isd ? dq4 : hq4;
+        const int r = e / q, c4 = e - r * q;
+        st[v] = idx < ntot ? (r << 8) | c4 : -1;
+        st_d |= (isd ? 1u : 0u) << v;
+    }
+    const float4* Dv = reinterpret_cast<const float4*>(D);
+    const float4* Hv = reinterpret_cast<const float4*>(H);
+    float4* dt4 = reinterpret_cast<float4*>(dt);
+    float4* ht4 = reinterpret_cast<float4*>(ht);
 #define VIHMC_BWD_LOAD(SUB)                                                                         \
-    _Pragma("unroll") for (int v = 0; v < 8; ++v) {                                                 \
-        const int idx = min(tid + 256 * v, ntot - 1);                                               \
-        const bool isd = idx < nd4;                                                                 \
-        const int e = isd ? idx : idx - nd4;                                                        \
-        const int q = isd ? dq4 : hq4;                                                              \
-        const int r = e / q, c4 = e - r * q;                                                        \
-        const int row = min((SUB) + r, P.M - 1);                                                    \
-        const float* src = isd ? D + (int64_t)row * P.ldd : H + (int64_t)row * P.ldh;               \
-        pf[v] = reinterpret_cast<const float4*>(src)[c4];                                           \
+    _Pragma("unroll") for (int v = 0; v < BWD_SLOTS; ++v) {                                         \
+        const int row = min((SUB) + (max(st[v], 0) >> 8), P.M - 1);                                 \
+        const int c4 = st[v] & 255;                                                                 \
+        pf[v] = ((st_d >> v) & 1) ? Dv[(int64_t)row * (P.ldd >> 2) + c4]                            \
+                                  : Hv[(int64_t)row * (P.ldh >> 2) + c4];                           \
     }
 #define VIHMC_BWD_STORE(SUB)                                                                        \
-    _Pragma("unroll") for (int v = 0; v < 8; ++v) {                                                 \
-        const int idx = tid + 256 * v;                                                              \
-        if (idx < ntot) {                                                                           \
-            const bool isd = idx < nd4;                                                             \
-            const int e = isd ? idx : idx - nd4;                                                    \
-            const int q = isd ? dq4 : hq4;                                                          \
-            const int r = e / q, c4 = e - r * q;                                                    \
+    _Pragma("unroll") for (int v = 0; v < BWD_SLOTS; ++v) {                                         \
+        if (st[v] >= 0) {                                                                           \
+            const int r = st[v] >> 8, c4 = st[v] & 255;                                             \
             const float4 val = ((SUB) + r < r1) ? pf[v] : float4{0.f, 0.f, 0.f, 0.f};               \
-            reinterpret_cast<float4*>(isd ? dt + r * LDT : ht + r * LDH)[c4] = val;                 \
+            if ((st_d >> v) & 1) dt4[r * (LDT >> 2) + c4] = val;                                    \
+            else ht4[r * (LDH >> 2) + c4] = val;                                                    \
         }                                                                                           \
     }
-
-    // dW accumulators: this wave's two 16-row output subtiles of dW
-    const int ns0 = 2 * wave, ns1 = 2 * wave + 1;
-    const bool dw0 = 16 * ns0 < P.n_out, dw1 = 16 * ns1 < P.n_out;
-    f32x4 acc_w[2][NTI];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int t = 0; t < NTI; ++t) acc_w[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float dsum[2] = {0.f, 0.f};
-    const int ncol0 = min(16 * ns0 + lr, P.n_out - 1), ncol1 = min(16 * ns1 + lr, P.n_out - 1);
-    int jcol[NTI];
-#pragma unroll
-    for (int t = 0; t < NTI; ++t) jcol[t] = min(16 * t + lr, P.n_in - 1);
-    // dX geometry
-    const int xh = wave & 1, xpar = wave >> 1;
-    const int kfull = n_out & ~15;
 
     if (r0 < r1) {
         VIHMC_BWD_LOAD(r0)
     }
+    // The two roles run separate sub-tile loops with the same barrier sequence (s_barrier counts waves),
+    // so each role's registers are allocated for its own loop only.
+    if (xrole) {
+        const int xh = rw & 1, xpar = rw >> 1;
+        const int kfull = n_out & ~15;
+        const float4* drow = reinterpret_cast<const float4*>(dt + (16 * xh + lr) * LDT);
+        const float* wrow[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) wrow[u] = wt + min(16 * (2 * u + xpar) + lr, P.n_in - 1) * LDW;
+        const float* hrow = ht + (16 * xh + lr) * LDH;
+        for (int sub = r0; sub < r1; sub += BWD_SUB) {
+            VIHMC_BWD_STORE(sub)
+            __syncthreads();
+            if (sub + BWD_SUB < r1) {
+                VIHMC_BWD_LOAD(sub + BWD_SUB)
+            }
+            if (P.has_dx) {
+                f32x4 acc_x[NU];
+#pragma unroll
+                for (int u = 0; u < NU; ++u) acc_x[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int kb = 0; kb < kfull; kb += 16) {
+                    const float4 dv = drow[(kb >> 2) + lg];
+                    float4 wv[NU];
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) wv[u] = reinterpret_cast<const float4*>(wrow[u])[(kb >> 2) + lg];
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].x, dv.x, acc_x[u]);
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].y, dv.y, acc_x[u]);
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].z, dv.z, acc_x[u]);
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].w, dv.w, acc_x[u]);
+                }
+                for (int kb = kfull; kb < NO4; kb += 4) {
+                    const float dv = dt[(16 * xh + lr) * LDT + kb + lg];
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wrow[u][kb + lg], dv, acc_x[u]);
+                }
+                const int m = sub + 16 * xh + lr;
+                if (m < r1) {
+                    float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        const int i = 16 * (2 * u + xpar) + 4 * lg;
+                        if (2 * u + xpar >= NTI || i >= NI4) continue;
+                        const float4 h = reinterpret_cast<const float4*>(hrow)[i >> 2];
+                        float4 o;
+                        o.x = (i + 0 < P.n_in) ? acc_x[u][0] * act_grad_from_out_l(P.act, h.x) : 0.f;
+                        o.y = (i + 1 < P.n_in) ? acc_x[u][1] * act_grad_from_out_l(P.act, h.y) : 0.f;
+                        o.z = (i + 2 < P.n_in) ? acc_x[u][2] * act_grad_from_out_l(P.act, h.z) : 0.f;
+                        o.w = (i + 3 < P.n_in) ? acc_x[u][3] * act_grad_from_out_l(P.act, h.w) : 0.f;
+                        reinterpret_cast<float4*>(orow)[i >> 2] = o;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
+
+    // dW role: this wave's two 16-row output subtiles of dW
+    const int ns0 = 2 * rw, ns1 = 2 * rw + 1;
+    const bool dw0 = 16 * ns0 < P.n_out, dw1 = 16 * ns1 < P.n_out;
+    f32x4 acc_w[2][NTI];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int t = 0; t < NTI; ++t) acc_w[s2][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dsum[2] = {0.f, 0.f};
+    const int ncol0 = min(16 * ns0 + lr, P.n_out - 1), ncol1 = min(16 * ns1 + lr, P.n_out - 1);
+    // h column of the last 16-wide tile, clamped (earlier tiles are always in range: NTI = ceil(n_in/16))
+    const int jlast = min(16 * (NTI - 1) + lr, P.n_in - 1) - lr;
     for (int sub = r0; sub < r1; sub += BWD_SUB) {
         VIHMC_BWD_STORE(sub)
         __syncthreads();
         if (sub + BWD_SUB < r1) {
             VIHMC_BWD_LOAD(sub + BWD_SUB)
         }
-        if (P.has_dx) {
-            f32x4 acc_x[NU];
-#pragma unroll
-            for (int u = 0; u < NU; ++u) acc_x[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-            const float4* drow = reinterpret_cast<const float4*>(dt + (16 * xh + lr) * LDT);
-            const float* wrow[NU];
-#pragma unroll
-            for (int u = 0; u < NU; ++u) wrow[u] = wt + min(16 * (2 * u + xpar) + lr, P.n_in - 1) * LDW;
-#pragma unroll
-            for (int kb = 0; kb < kfull; kb += 16) {
-                const float4 dv = drow[(kb >> 2) + lg];
-                float4 wv[NU];
-#pragma unroll
-                for (int u = 0; u < NU; ++u) wv[u] = reinterpret_cast<const float4*>(wrow[u])[(kb >> 2) + lg];
-#pragma unroll
-                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].x, dv.x, acc_x[u]);
-#pragma unroll
-                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].y, dv.y, acc_x[u]);
-#pragma unroll
-                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].z, dv.z, acc_x[u]);
-#pragma unroll
-                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].w, dv.w, acc_x[u]);
-            }
-            for (int kb = kfull; kb < NO4; kb += 4) {
-                const float dv = dt[(16 * xh + lr) * LDT + kb + lg];
-#pragma unroll
-                for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wrow[u][kb + lg], dv, acc_x[u]);
-            }
-            const int m = sub + 16 * xh + lr;
-            if (m < r1) {
-                const float* hrow = ht + (16 * xh + lr) * LDH;
-                float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
-#pragma unroll
-                for (int u = 0; u < NU; ++u) {
-                    const int i = 16 * (2 * u + xpar) + 4 * lg;
-                    if (2 * u + xpar >= NTI || i >= NI4) continue;
-                    const float4 h = reinterpret_cast<const float4*>(hrow)[i >> 2];
-                    float4 o;
-                    o.x = (i + 0 < P.n_in) ? acc_x[u][0] * act_grad_from_out_l(P.act, h.x) : 0.f;
-                    o.y = (i + 1 < P.n_in) ? acc_x[u][1] * act_grad_from_out_l(P.act, h.y) : 0.f;
-                    o.z = (i + 2 < P.n_in) ? acc_x[u][2] * act_grad_from_out_l(P.act, h.z) : 0.f;
-                    o.w = (i + 3 < P.n_in) ? acc_x[u][3] * act_grad_from_out_l(P.act, h.w) : 0.f;
-                    reinterpret_cast<float4*>(orow)[i >> 2] = o;
-                }
-            }
-        }
         if (dw0) {
+            // step i covers rows base + 2*lg (base = 0,1,8,9,16,17,24,25): the two rows one b32 lane group
+            // {0-31} touches are 2 apart, i.e. 2*LD == 16 (mod 32) banks apart -> conflict free.
+            // 4 waves/SIMD (2 dX + 2 dW) hide the LDS latency of the 2 + NTI reads of a step.
 #pragma unroll 2
-            for (int mm = 0; mm < BWD_SUB; mm += 4) {
-                const float* drw = dt + (mm + lg) * LDT;
-                const float* hrw = ht + (mm + lg) * LDH;
+            for (int mi = 0; mi < BWD_SUB / 4; ++mi) {
+                const int mrow = (mi & 1) + 8 * (mi >> 1) + 2 * lg;
+                const float* drw = dt + mrow * LDT;
+                const float* hrw = ht + mrow * LDH + lr;
                 const float a0 = drw[ncol0];
-                const float a1 = dw1 ? drw[ncol1] : 0.f;
+                const float a1v = drw[ncol1];
+                const float a1 = dw1 ? a1v : 0.f;
                 float hv[NTI];
 #pragma unroll
-                for (int t = 0; t < NTI; ++t) hv[t] = hrw[jcol[t]];
+                for (int t = 0; t < NTI - 1; ++t) hv[t] = hrw[16 * t];
+                hv[NTI - 1] = hrw[jlast];
 #pragma unroll
                 for (int t = 0; t < NTI; ++t) {
                     acc_w[0][t] = mfma(a0, hv[t], acc_w[0][t]);
@@ -463,8 +502,8 @@ __global__ __launch_bounds__(256, 2) void k_bwd_fused(BwdArgs args) {
     if (!dw0) return;
     float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const int ns = s == 0 ? ns0 : ns1;
+    for (int s2 = 0; s2 < 2; ++s2) {
+        const int ns = s2 == 0 ? ns0 : ns1;
 #pragma unroll
         for (int t = 0; t < NTI; ++t) {
             const int j = 16 * t + lr;
@@ -472,10 +511,10 @@ __global__ __launch_bounds__(256, 2) void k_bwd_fused(BwdArgs args) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int n = 16 * ns + 4 * lg + r;
-                if (n < P.n_out) part[(int64_t)n * NI4 + j] = (j < P.n_in) ? acc_w[s][t][r] : 0.f;
+                if (n < P.n_out) part[(int64_t)n * NI4 + j] = (j < P.n_in) ? acc_w[s2][t][r] : 0.f;
             }
         }
-        float v = dsum[s];
+        float v = dsum[s2];
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
         const int n = 16 * ns + lr;
@@ -538,18 +577,18 @@ size_t bwd_lds_bytes(const BwdArgs& a) {
 hipError_t launch_bwd(const BwdArgs& a, int nti, hipStream_t s) {
     const int blocks = a.C * a.p[0].n_wg + (a.nprob > 1 ? a.C * a.p[1].n_wg : 0);
     const size_t shm = bwd_lds_bytes(a);
-    dim3 g(blocks), blk(256);
+    dim3 g(blocks), blk(BWD_THREADS);
     const bool k100 = a.p[0].n_out == 100 && (a.nprob < 2 || a.p[1].n_out == 100);
-    if (k100 && nti == 7) VIHMC_LAUNCH_L((k_bwd_fused<7, 100>), g, blk, shm, s, a);
+    if (k100 && nti == 7) VIHMC_LAUNCH_L((k_bwd_ws<7, 100>), g, blk, shm, s, a);
     switch (nti) {
-        case 1: VIHMC_LAUNCH_L((k_bwd_fused<1, 0>), g, blk, shm, s, a);
-        case 2: VIHMC_LAUNCH_L((k_bwd_fused<2, 0>), g, blk, shm, s, a);
-        case 3: VIHMC_LAUNCH_L((k_bwd_fused<3, 0>), g, blk, shm, s, a);
-        case 4: VIHMC_LAUNCH_L((k_bwd_fused<4, 0>), g, blk, shm, s, a);
-        case 5: VIHMC_LAUNCH_L((k_bwd_fused<5, 0>), g, blk, shm, s, a);
-        case 6: VIHMC_LAUNCH_L((k_bwd_fused<6, 0>), g, blk, shm, s, a);
-        case 7: VIHMC_LAUNCH_L((k_bwd_fused<7, 0>), g, blk, shm, s, a);
-        case 8: VIHMC_LAUNCH_L((k_bwd_fused<8, 0>), g, blk, shm, s, a);
+        case 1: VIHMC_LAUNCH_L((k_bwd_ws<1, 0>), g, blk, shm, s, a);
+        case 2: VIHMC_LAUNCH_L((k_bwd_ws<2, 0>), g, blk, shm, s, a);
+        case 3: VIHMC_LAUNCH_L((k_bwd_ws<3, 0>), g, blk, shm, s, a);
+        case 4: VIHMC_LAUNCH_L((k_bwd_ws<4, 0>), g, blk, shm, s, a);
+        case 5: VIHMC_LAUNCH_L((k_bwd_ws<5, 0>), g, blk, shm, s, a);
+        case 6: VIHMC_LAUNCH_L((k_bwd_ws<6, 0>), g, blk, shm, s, a);
+        case 7: VIHMC_LAUNCH_L((k_bwd_ws<7, 0>), g, blk, shm, s, a);
+        case 8: VIHMC_LAUNCH_L((k_bwd_ws<8, 0>), g, blk, shm, s, a);
         default: return hipErrorInvalidValue;
     }
 }

@@ -312,7 +312,13 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         for (int b = 0; b < 2; ++b)
             if (int rc = p->alloc(&n.delta[b], n.delta_cs * C)) return rc;
         // weight-gradient partial slabs: one per row chunk
-        n.rows_per_chunk = C >= 8 ? 256 : 64;
+        // fused-backward row chunk: one workgroup per chunk, sized so a max_chains launch over both
+        // nets is ~one resident round (2 workgroups/CU x 256 CUs; the kernel needs ~68 KB of LDS)
+        {
+            const int64_t rows_all = (int64_t)p->nets[0].rows + p->nets[1].rows;
+            const int64_t want = cdiv((int64_t)C * rows_all, 512);
+            n.rows_per_chunk = (int)std::max<int64_t>(BWD_SUB, (want + BWD_SUB - 1) / BWD_SUB * BWD_SUB);
+        }
         int64_t po = 0;
         for (auto& L : n.L) {
             L.n_chunks = cdiv(n.rows, n.rows_per_chunk);
@@ -395,11 +401,11 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
 
 inline int nt_of(int n) { return (n + 15) / 16; }
 
-// row tiles per row-dot workgroup: amortise the weight staging while keeping >= ~3 workgroups per CU
-inline int rowdot_tpw(int ntiles, int C) {
-    int t = 1;
-    while (t < 4 && (int64_t)C * cdiv(ntiles, 2 * t) >= 768) t *= 2;
-    return t;
+// row tiles per row-dot workgroup: the whole launch (all problems, all chains) fits one resident round of
+// ~3 workgroups per CU (the staged 100x100 weight block is ~42 KB of LDS), so every workgroup stages its
+// weights once and no second, partly empty round is left
+inline int rowdot_tpw(int64_t total_tiles) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(8, cdiv(total_tiles, (int64_t)768)));
 }
 
 // Forward through both MLPs (grouped launches: branch + trunk layer j together).
@@ -415,6 +421,10 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
             if (j < (int)n.L.size()) wgs += (int64_t)C * cdiv(n.rows, ROWDOT_WAVES * 32);
         }
         const int ms = wgs >= 512 ? 2 : 1;
+        int64_t total_tiles = 0;
+        for (int net = 0; net < 2; ++net)
+            if (j < (int)p->nets[net].L.size()) total_tiles += (int64_t)C * cdiv(p->nets[net].rows, ROWDOT_WAVES * 16 * ms);
+        const int tpw = rowdot_tpw(total_tiles);
         for (int net = 0; net < 2; ++net) {
             Net& n = p->nets[net];
             if (j >= (int)n.L.size()) continue;
@@ -436,7 +446,7 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
             q.K = L.n_in;
             q.act = L.act;
             q.ntiles = cdiv(n.rows, ROWDOT_WAVES * 16 * ms);
-            q.tpw = rowdot_tpw(q.ntiles, C);
+            q.tpw = tpw;
             q.tiles = cdiv(q.ntiles, q.tpw);
             nt = std::max(nt, nt_of(L.n_out));
         }
