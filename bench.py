@@ -148,6 +148,13 @@ def main():
     avg_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = flops_contract / avg_s / 1e12 if k_n else None
     evals_per_s = world * grad_evals / T
+    traffic = None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic_contract.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("chains_per_gpu") == C:
+            traffic = tj["hbm_bytes_per_launch"]     # PMC-measured bytes per side-A launch (same config)
     line = {
         "metric": METRIC,
         "value": value,
@@ -168,9 +175,10 @@ def main():
         "hamiltorch_equiv_grad_evals_per_s": world * C * (args.L + 1) * args.steps / T,
         "eval_tflops_algorithmic": evals_per_s * spec.flops_per_grad_eval(prob.N, prob.P) / 1e12,
         "accept_rate": acc_rate,
-        "roofline": {"kernel": "k_contract<112,true> (fused branch x trunk contraction + NLL + dZ_trunk)",
+        "roofline": {"kernel": "k_contract2<112,6,1,true> side A (fused branch x trunk contraction + NLL + dZ_trunk)",
                      "bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None, "traffic": None,
+                     "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+                     "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE; profiles/traffic_contract.json)",
                      "avg_launch_ms": avg_s * 1e3, "launches": k_n,
                      "flops_per_launch": flops_contract},
     }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-end evidence on the GPU box: default bench line, its rocprofv3 kernel stats, and the two PMC
+# passes that give the roofline kernel's HBM traffic. Usage: bash profiles/round_profile.sh <tag>
+set -e
+TAG=${1:-r01}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$ROOT/gpurun_out
+timeout -k 10 600 python3 $ROOT/bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err
+cd /tmp && export TMPDIR=/tmp
+B="python3 $ROOT/bench.py --steps 5 --warmup 1 --cpu-seconds 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_stats -o s -- $B > $O/${TAG}_stats.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/${TAG}_fetch -o p -- $B > $O/${TAG}_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $O/${TAG}_write -o p -- $B > $O/${TAG}_write.log 2>&1

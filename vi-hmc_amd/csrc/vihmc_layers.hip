@@ -56,8 +56,55 @@ __host__ __device__ constexpr int rowdot_ldb(int k4) { return k4 + ((24 - (k4 & 
 // =============================================================================================
 // KF > 0: the contraction length is KF for every problem of the launch (hidden 100x100 layers), which
 // makes the k-loop a compile-time loop the compiler can software-pipeline; KF = 0 reads P.K.
+// Epilogue of one row tile: bias + activation (FWD) or * act'(h) (BWD), float4 stores; columns in
+// [Nn, ldo) are written as zeros (padding read by the next GEMM). (A branch-free variant templated on
+// the activation measured ~10% slower on the hidden layers; see profiles/README.md.)
+template <int NT, int MS, int MODE>
+__device__ __forceinline__ void rowdot_epilogue(const RowdotProb& P, int c, int m0, int lr, int lg,
+                                                const f32x4 (&acc)[MS][NT]) {
+    float* O = P.O + c * P.o_cs;
+    const float* H = P.H + c * P.h_cs;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int n = 16 * t + 4 * lg;
+        if (n >= P.ldo) continue;
+        float4 bv = {0.f, 0.f, 0.f, 0.f};
+        if (MODE == MODE_FWD && P.bias) bv = *reinterpret_cast<const float4*>(P.bias + c * P.bias_cs + n);
+#pragma unroll
+        for (int s = 0; s < MS; ++s) {
+            const int m = m0 + 16 * s + lr;
+            if (m >= P.M) continue;
+            float4 o;
+            if (MODE == MODE_FWD) {
+                o.x = act_apply_l(P.act, acc[s][t][0] + bv.x);
+                o.y = act_apply_l(P.act, acc[s][t][1] + bv.y);
+                o.z = act_apply_l(P.act, acc[s][t][2] + bv.z);
+                o.w = act_apply_l(P.act, acc[s][t][3] + bv.w);
+            } else {
+                const float4 h = *reinterpret_cast<const float4*>(H + (int64_t)m * P.ldh + n);
+                o.x = acc[s][t][0] * act_grad_from_out_l(P.act, h.x);
+                o.y = acc[s][t][1] * act_grad_from_out_l(P.act, h.y);
+                o.z = acc[s][t][2] * act_grad_from_out_l(P.act, h.z);
+                o.w = acc[s][t][3] * act_grad_from_out_l(P.act, h.w);
+            }
+            if (n + 3 >= P.Nn) {
+                if (n + 0 >= P.Nn) o.x = 0.f;
+                if (n + 1 >= P.Nn) o.y = 0.f;
+                if (n + 2 >= P.Nn) o.z = 0.f;
+                if (n + 3 >= P.Nn) o.w = 0.f;
+            }
+            *reinterpret_cast<float4*>(O + (int64_t)m * P.ldo + n) = o;
+        }
+    }
+}
+
+// KF > 0: the contraction length is KF for every problem of the launch (hidden 100x100 layers). The
+// wave's whole A tile (MS x 16 rows x KF, k-permuted float4 per lane) is then loaded into registers at
+// once, and the NEXT tile's loads are issued before the current tile's epilogue, so the HBM latency hides
+// under the activation math instead of stalling the MFMA stream. KF = 0 reads P.K and prefetches one
+// 16-wide k-block ahead.
 template <int NT, int MS, int MODE, int KF>
-__global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
+__global__ __launch_bounds__(256, 3) void k_rowdot2(RowdotArgs args) {
     extern __shared__ float bs[];
     int b = blockIdx.x;
     const int first = args.C * args.p[0].tiles;
@@ -83,115 +130,151 @@ __global__ __launch_bounds__(256) void k_rowdot2(RowdotArgs args) {
                 *reinterpret_cast<const float4*>(B + (int64_t)r * P.ldb + 4 * c4);
         }
     }
+    const float* br[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) br[t] = bs + min(16 * t + lr, P.Nn - 1) * LDB;
+    const int tile_end = min(P.ntiles, (grp + 1) * P.tpw);
+    // acc[s][t] holds the TRANSPOSED 16x16 tile O^T (MFMA A operand = weight rows n, B operand = data
+    // rows m): lane l, register r = O[m0 + 16s + (l&15)][16t + 4(l>>4) + r], i.e. 4 consecutive output
+    // columns of one row per lane -> float4 epilogue loads/stores.
+    f32x4 acc[MS][NT];
 
-    __syncthreads();
-    // the staged weights serve tpw consecutive 4-wave row tiles
-    for (int tile = grp * P.tpw; tile < (grp + 1) * P.tpw; ++tile) {
-        const int m0 = tile * (ROWDOT_WAVES * 16 * MS) + wave * 16 * MS;
-        if (tile >= P.ntiles) break;
-        const float* ar[MS];
-#pragma unroll
-        for (int s = 0; s < MS; ++s) ar[s] = A + (int64_t)min(m0 + 16 * s + lr, P.M - 1) * P.lda;
-        const float* br[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) br[t] = bs + min(16 * t + lr, P.Nn - 1) * LDB;
-
-        // acc[s][t] holds the TRANSPOSED 16x16 tile O^T (MFMA A operand = weight rows n, B operand = data
-        // rows m): lane l, register r = O[m0 + 16s + (l&15)][16t + 4(l>>4) + r], i.e. 4 consecutive output
-        // columns of one row per lane -> float4 epilogue loads/stores.
-        f32x4 acc[MS][NT];
-#pragma unroll
-        for (int s = 0; s < MS; ++s)
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-        const int kfull = KK & ~15;
-        float4 a_cur[MS];
-        if (kfull > 0) {
-#pragma unroll
-            for (int s = 0; s < MS; ++s) a_cur[s] = *reinterpret_cast<const float4*>(ar[s] + 4 * lg);
+    if constexpr (KF > 0) {
+        constexpr int NKB = KF / 16;
+        constexpr int NTL = ((KF & 15) + 3) / 4;     // 4-wide tail steps
+        float4 abuf[MS][NKB];
+        float atl[MS][NTL > 0 ? NTL : 1];
+#define VIHMC_RD_LOAD_A(TILE, K0, K1, TL)                                                           \
+        {                                                                                           \
+            const int mt = (TILE) * (ROWDOT_WAVES * 16 * MS) + wave * 16 * MS;                      \
+            _Pragma("unroll") for (int s = 0; s < MS; ++s) {                                        \
+                const float* ap = A + (int64_t)min(mt + 16 * s + lr, P.M - 1) * P.lda;              \
+                _Pragma("unroll") for (int k = (K0); k < (K1); ++k)                                 \
+                    abuf[s][k] = *reinterpret_cast<const float4*>(ap + 16 * k + 4 * lg);            \
+                if (TL) {                                                                           \
+                    _Pragma("unroll") for (int k = 0; k < NTL; ++k) atl[s][k] = ap[16 * NKB + 4 * k + lg]; \
+                }                                                                                   \
+            }                                                                                       \
         }
+        if (grp * P.tpw < tile_end) VIHMC_RD_LOAD_A(grp * P.tpw, 0, NKB, true)
+        __syncthreads();
+        for (int tile = grp * P.tpw; tile < tile_end; ++tile) {
+            const int m0 = tile * (ROWDOT_WAVES * 16 * MS) + wave * 16 * MS;
 #pragma unroll
-        for (int kb = 0; kb < kfull; kb += 16) {
-            float4 a_nxt[MS];
-            const bool more = kb + 16 < kfull;
-            if (more) {
+            for (int s = 0; s < MS; ++s)
 #pragma unroll
-                for (int s = 0; s < MS; ++s) a_nxt[s] = *reinterpret_cast<const float4*>(ar[s] + kb + 16 + 4 * lg);
-            }
-            float4 w[NT];
+                for (int t = 0; t < NT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // weights of k-block k+1 are read from LDS while the MFMAs of block k run; the scheduling
+            // barrier keeps the compiler from hoisting further blocks' reads (register pressure)
+            float4 wc[NT];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) w[t] = *reinterpret_cast<const float4*>(br[t] + kb + 4 * lg);
+            for (int t = 0; t < NT; ++t) wc[t] = *reinterpret_cast<const float4*>(br[t] + 4 * lg);
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
+            for (int k = 0; k < NKB; ++k) {
+                float4 w[NT];
 #pragma unroll
-                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].x, a_cur[s].x, acc[s][t]);
+                for (int t = 0; t < NT; ++t) w[t] = wc[t];
+                if (k + 1 < NKB) {
 #pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].y, a_cur[s].y, acc[s][t]);
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].z, a_cur[s].z, acc[s][t]);
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].w, a_cur[s].w, acc[s][t]);
-            if (more) {
-#pragma unroll
-                for (int s = 0; s < MS; ++s) a_cur[s] = a_nxt[s];
-            }
-        }
-        // tail: K rounded up to 4 (operand padding columns are zero)
-        for (int kb = kfull; kb < K4; kb += 4) {
-            float a[MS], w[NT];
-#pragma unroll
-            for (int s = 0; s < MS; ++s) a[s] = ar[s][kb + lg];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) w[t] = br[t][kb + lg];
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t], a[s], acc[s][t]);
-        }
-
-        float* O = P.O + c * P.o_cs;
-        const float* H = P.H + c * P.h_cs;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int n = 16 * t + 4 * lg;           // first of this lane's 4 output columns
-            if (n >= P.ldo) continue;                // ldo is a multiple of 4: groups are all-in or all-out
-            float4 bv = {0.f, 0.f, 0.f, 0.f};
-            if (MODE == MODE_FWD && P.bias) bv = *reinterpret_cast<const float4*>(P.bias + c * P.bias_cs + n);
-#pragma unroll
-            for (int s = 0; s < MS; ++s) {
-                const int m = m0 + 16 * s + lr;
-                if (m >= P.M) continue;
-                float4 o;
-                if (MODE == MODE_FWD) {
-                    o.x = act_apply_l(P.act, acc[s][t][0] + bv.x);
-                    o.y = act_apply_l(P.act, acc[s][t][1] + bv.y);
-                    o.z = act_apply_l(P.act, acc[s][t][2] + bv.z);
-                    o.w = act_apply_l(P.act, acc[s][t][3] + bv.w);
-                } else {
-                    const float4 h = *reinterpret_cast<const float4*>(H + (int64_t)m * P.ldh + n);
-                    o.x = acc[s][t][0] * act_grad_from_out_l(P.act, h.x);
-                    o.y = acc[s][t][1] * act_grad_from_out_l(P.act, h.y);
-                    o.z = acc[s][t][2] * act_grad_from_out_l(P.act, h.z);
-                    o.w = acc[s][t][3] * act_grad_from_out_l(P.act, h.w);
+                    for (int t = 0; t < NT; ++t) wc[t] = *reinterpret_cast<const float4*>(br[t] + 16 * (k + 1) + 4 * lg);
                 }
-                // columns in [Nn, ldo) are written as zeros (padding read by the next GEMM)
-                if (n + 3 >= P.Nn) {
-                    if (n + 0 >= P.Nn) o.x = 0.f;
-                    if (n + 1 >= P.Nn) o.y = 0.f;
-                    if (n + 2 >= P.Nn) o.z = 0.f;
-                    if (n + 3 >= P.Nn) o.w = 0.f;
-                }
-                *reinterpret_cast<float4*>(O + (int64_t)m * P.ldo + n) = o;
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].x, abuf[s][k].x, acc[s][t]);
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].y, abuf[s][k].y, acc[s][t]);
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].z, abuf[s][k].z, acc[s][t]);
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].w, abuf[s][k].w, acc[s][t]);
+                __builtin_amdgcn_sched_barrier(0);
             }
+#pragma unroll
+            for (int k = 0; k < NTL; ++k) {
+                float w[NT];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) w[t] = br[t][16 * NKB + 4 * k + lg];
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t], atl[s][k], acc[s][t]);
+            }
+            // first half of the next tile's A goes out before the epilogue (hidden under it), the rest
+            // after it (register budget: 3 waves/SIMD = 168 VGPRs)
+            if (tile + 1 < tile_end) VIHMC_RD_LOAD_A(tile + 1, 0, NKB / 2, false)
+            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc);
+            if (tile + 1 < tile_end) VIHMC_RD_LOAD_A(tile + 1, NKB / 2, NKB, true)
         }
-
+#undef VIHMC_RD_LOAD_A
+    } else {
+        __syncthreads();
+        for (int tile = grp * P.tpw; tile < tile_end; ++tile) {
+            const int m0 = tile * (ROWDOT_WAVES * 16 * MS) + wave * 16 * MS;
+            const float* ar[MS];
+#pragma unroll
+            for (int s = 0; s < MS; ++s) ar[s] = A + (int64_t)min(m0 + 16 * s + lr, P.M - 1) * P.lda;
+#pragma unroll
+            for (int s = 0; s < MS; ++s)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int kfull = KK & ~15;
+            float4 a_cur[MS];
+            if (kfull > 0) {
+#pragma unroll
+                for (int s = 0; s < MS; ++s) a_cur[s] = *reinterpret_cast<const float4*>(ar[s] + 4 * lg);
+            }
+            for (int kb = 0; kb < kfull; kb += 16) {
+                float4 a_nxt[MS];
+                const bool more = kb + 16 < kfull;
+                if (more) {
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) a_nxt[s] = *reinterpret_cast<const float4*>(ar[s] + kb + 16 + 4 * lg);
+                }
+                float4 w[NT];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) w[t] = *reinterpret_cast<const float4*>(br[t] + kb + 4 * lg);
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].x, a_cur[s].x, acc[s][t]);
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].y, a_cur[s].y, acc[s][t]);
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].z, a_cur[s].z, acc[s][t]);
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t].w, a_cur[s].w, acc[s][t]);
+                if (more) {
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) a_cur[s] = a_nxt[s];
+                }
+            }
+            // tail: K rounded up to 4 (operand padding columns are zero)
+            for (int kb = kfull; kb < K4; kb += 4) {
+                float a[MS], w[NT];
+#pragma unroll
+                for (int s = 0; s < MS; ++s) a[s] = ar[s][kb + lg];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) w[t] = br[t][kb + lg];
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t], a[s], acc[s][t]);
+            }
+            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc);
+        }
     }
 }
 

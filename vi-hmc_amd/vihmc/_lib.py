@@ -13,7 +13,8 @@ import threading
 
 import torch  # noqa: F401  (must be loaded before libvihmc.so, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvihmc.so")
+# VIHMC_LIB overrides the library (A/B builds of kernel variants); default: the in-tree build
+LIB_PATH = os.environ.get("VIHMC_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvihmc.so")
 
 c_int, c_int32, c_int64, c_float, c_double = ctypes.c_int, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double
 c_void_p, c_char_p = ctypes.c_void_p, ctypes.c_char_p
