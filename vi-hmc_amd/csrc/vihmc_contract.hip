@@ -36,7 +36,9 @@ __host__ __device__ constexpr int contract_ldq(int W) {
 
 // SNKB/SNTAIL >= 0 fix the k-block structure at compile time (the production width W = 100 is
 // SNKB = 6 full 16-wide blocks + SNTAIL = 1 four-wide step); -1 reads it from W at run time.
-template <int WMAX, int SNKB, int SNTAIL, bool GRAD>
+// LOADG (side B): G is read from Y (written by side A, already scaled) instead of recomputing S; the
+// owner rows are then not needed in registers.
+template <int WMAX, int SNKB, int SNTAIL, bool GRAD, bool LOADG>
 __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
     constexpr int NB = WMAX / 16;
     constexpr int QC = CONTRACT_QC;
@@ -56,6 +58,7 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
     const float* Own = P.Own + c * P.own_cs;
     const float* Q = P.Q + c * P.q_cs;
     const float b0 = P.b0[c * P.b0_cs];
+    const float* Yc = P.Y + c * P.y_cs;
     const int o0 = og * CONTRACT_OWN_PER_WG + wave * 32;
     const int nkb = SNKB >= 0 ? SNKB : (W >> 4);
     const int ntail = SNTAIL >= 0 ? SNTAIL : ((W4 - (nkb << 4)) >> 2);
@@ -65,6 +68,7 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
     float otl[2][3];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+        if (LOADG) break;
         const float* orow = Own + (int64_t)min(o0 + 16 * s + lr, P.Mo - 1) * P.ldown;
 #pragma unroll
         for (int bb = 0; bb < NB; ++bb)
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
             for (int s = 0; s < 2; ++s)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    yv[s][r] = P.Y[(int64_t)min(q0 + 16 * h + 4 * lg + r, P.Mq - 1) * P.ldy +
+                    yv[s][r] = Yc[(int64_t)min(q0 + 16 * h + 4 * lg + r, P.Mq - 1) * P.ldy +
                                    min(o0 + 16 * s + lr, P.Mo - 1)];
             if (more) {
                 VIHMC_LOAD_CHUNK(q0 + QC)
@@ -126,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
             const float4* qrow4 = reinterpret_cast<const float4*>(cur) + (16 * h + lr) * LDQ4;
 #pragma unroll
             for (int bb = 0; bb < NB; ++bb) {
-                if (bb < nkb) {
+                if (!LOADG && bb < nkb) {
                     const float4 qa = qrow4[4 * bb + lg];
                     sacc[0] = mfma_c(qa.x, ob[0][bb].x, sacc[0]);
                     sacc[1] = mfma_c(qa.x, ob[1][bb].x, sacc[1]);
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
             }
 #pragma unroll
             for (int ts = 0; ts < 3; ++ts) {
-                if (ts < ntail) {
+                if (!LOADG && ts < ntail) {
                     const float qa = qrow[16 * nkb + 4 * ts + lg];
                     sacc[0] = mfma_c(qa, otl[0][ts], sacc[0]);
                     sacc[1] = mfma_c(qa, otl[1][ts], sacc[1]);
@@ -154,6 +158,10 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
                     const int qq = q0 + 16 * h + 4 * lg + r;
                     const int oo = o0 + 16 * s + lr;
                     const bool ok = (qq < q_hi) && (oo < P.Mo);
+                    if (LOADG) {
+                        g[s][r] = ok ? yv[s][r] : 0.f;
+                        continue;
+                    }
                     const float sv = sacc[s][r] + b0;
                     if (!GRAD && P.write_s && ok) sout[(int64_t)qq * P.ldout + oo] = sv;
                     const float rv = sv - yv[s][r];
@@ -163,6 +171,24 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
                         gsum += (double)g[s][r];
                     }
                 }
+            if (GRAD && !LOADG && P.gout) {
+                // G^T[o][q .. q+3] for side B: 4 consecutive q of one o per lane -> one float4 store
+                float* gw = P.gout + c * P.gout_cs;
+                const int qq = q0 + 16 * h + 4 * lg;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int oo = o0 + 16 * s + lr;
+                    if (oo >= P.Mo) continue;
+                    float* dst = gw + (int64_t)oo * P.ldg + qq;
+                    if (qq + 3 < q_hi) {
+                        *reinterpret_cast<float4*>(dst) = float4{g[s][0], g[s][1], g[s][2], g[s][3]};
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (qq + r < q_hi) dst[r] = g[s][r];
+                    }
+                }
+            }
             if (GRAD) {
 #pragma unroll
                 for (int rr = 0; rr < 4; ++rr) {
@@ -218,22 +244,23 @@ size_t contract_lds_bytes(int W) { return sizeof(float) * 2 * CONTRACT_QC * cont
 #define VIHMC_LAUNCH_C(kern, grid, block, shm, s, ...) \
     do { hipLaunchKernelGGL(kern, grid, block, shm, s, __VA_ARGS__); return hipGetLastError(); } while (0)
 
-template <bool GRAD>
+template <bool GRAD, bool LOADG>
 static hipError_t launch_contract_t(const ContractProb& p, int C, hipStream_t s) {
     dim3 g(C * p.o_tiles * p.q_chunks), blk(256);
     const size_t shm = contract_lds_bytes(p.W);
     const int w = p.W;
-    if (w == 100) VIHMC_LAUNCH_C((k_contract2<112, 6, 1, GRAD>), g, blk, shm, s, p);
-    if (w <= 16) VIHMC_LAUNCH_C((k_contract2<16, -1, -1, GRAD>), g, blk, shm, s, p);
-    if (w <= 32) VIHMC_LAUNCH_C((k_contract2<32, -1, -1, GRAD>), g, blk, shm, s, p);
-    if (w <= 64) VIHMC_LAUNCH_C((k_contract2<64, -1, -1, GRAD>), g, blk, shm, s, p);
-    if (w <= 112) VIHMC_LAUNCH_C((k_contract2<112, -1, -1, GRAD>), g, blk, shm, s, p);
-    if (w <= 128) VIHMC_LAUNCH_C((k_contract2<128, -1, -1, GRAD>), g, blk, shm, s, p);
+    if (w == 100) VIHMC_LAUNCH_C((k_contract2<112, 6, 1, GRAD, LOADG>), g, blk, shm, s, p);
+    if (w <= 16) VIHMC_LAUNCH_C((k_contract2<16, -1, -1, GRAD, LOADG>), g, blk, shm, s, p);
+    if (w <= 32) VIHMC_LAUNCH_C((k_contract2<32, -1, -1, GRAD, LOADG>), g, blk, shm, s, p);
+    if (w <= 64) VIHMC_LAUNCH_C((k_contract2<64, -1, -1, GRAD, LOADG>), g, blk, shm, s, p);
+    if (w <= 112) VIHMC_LAUNCH_C((k_contract2<112, -1, -1, GRAD, LOADG>), g, blk, shm, s, p);
+    if (w <= 128) VIHMC_LAUNCH_C((k_contract2<128, -1, -1, GRAD, LOADG>), g, blk, shm, s, p);
     return hipErrorInvalidValue;
 }
 
 hipError_t launch_contract(const ContractProb& p, int C, bool with_grad, hipStream_t s) {
-    return with_grad ? launch_contract_t<true>(p, C, s) : launch_contract_t<false>(p, C, s);
+    if (p.load_g) return with_grad ? launch_contract_t<true, true>(p, C, s) : hipErrorInvalidValue;
+    return with_grad ? launch_contract_t<true, false>(p, C, s) : launch_contract_t<false, false>(p, C, s);
 }
 
 }  // namespace vihmc

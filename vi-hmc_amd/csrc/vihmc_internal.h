@@ -85,13 +85,15 @@ hipError_t launch_bwd(const BwdArgs& a, int nti, hipStream_t s);
 //   dOwn[o][j] = sum_q G[q][o] * Q[q][j]            (WITH_GRAD)
 // The wave owns 32 rows of `Own` and streams `Q` in 16-row steps; S is never stored.
 // Side A: Own = Z_trunk [P], Q = Z_branch [N], Y = y [N][P]   -> dZ_trunk (complete) + sum r^2, sum G
-// Side B: Own = Z_branch [N], Q = Z_trunk chunk, Y = y^T [P][N] -> dZ_branch partial per chunk
+// Side B: Own = Z_branch [N], Q = Z_trunk chunk, Y = G^T [P][N] written by side A (load_g: no S
+//         recompute; y^T with load_g = 0) -> dZ_branch partial per chunk
 // Forward-only (predict) writes out[q][o] = S into `out` (side A, o = p contiguous).
 // ---------------------------------------------------------------------------------------------
 struct ContractProb {
     const float* Own; int64_t own_cs; int32_t ldown;
     const float* Q;   int64_t q_cs;   int32_t ldq;
-    const float* Y;   int32_t ldy;
+    const float* Y;   int32_t ldy; int64_t y_cs;   // y_cs = 0: targets shared by all chains
+    float* gout;      int64_t gout_cs; int32_t ldg;  // side A (optional): G^T[o][q] written for side B
     const float* b0;  int64_t b0_cs;
     float* out;       int64_t out_cs; int32_t ldout; int64_t out_chunk_stride;
     double* stats;    int64_t stats_cs;   // 2 doubles per wave (sum r^2, sum G) when with_stats
@@ -99,6 +101,7 @@ struct ContractProb {
     int32_t Mo, Mq, W;
     int32_t o_tiles, q_chunks, q_per_chunk;   // o_tiles = ceil(Mo / CONTRACT_OWN_PER_WG)
     int32_t with_stats, write_s;
+    int32_t load_g;                       // side B: Y holds G (already scaled); no S recompute
     float gscale;
 };
 

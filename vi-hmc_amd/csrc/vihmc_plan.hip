@@ -87,7 +87,9 @@ struct vihmc_plan {
     float* packed = nullptr;
     float* gp = nullptr;
     int64_t dp = 0;
-    float *y = nullptr, *yT = nullptr;
+    float* y = nullptr;
+    float* gT = nullptr;        // per chain G^T [P][N] (side A -> side B); gT_cs floats per chain
+    int64_t gT_cs = 0;
     float* partB = nullptr;
     int64_t partB_cs = 0;
     int qchunksB = 1, qperB = 32;
@@ -289,12 +291,8 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     }
     const int64_t NP = (int64_t)p->N * p->P;
     if (int rc = p->upload(&p->y, y, NP)) return rc;
-    {
-        std::vector<float> yt((size_t)NP);
-        for (int64_t n = 0; n < p->N; ++n)
-            for (int64_t q = 0; q < p->P; ++q) yt[(size_t)(q * p->N + n)] = y[n * p->P + q];
-        if (int rc = p->upload(&p->yT, yt.data(), NP)) return rc;
-    }
+    p->gT_cs = r64(NP);
+    if (int rc = p->alloc(&p->gT, p->gT_cs * C)) return rc;
 
     // ---- per-chain work buffers ---------------------------------------------------------------------
     for (int net = 0; net < 2; ++net) {
@@ -475,6 +473,9 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
         q.out_cs = p->qchunksA > 1 ? p->partA_cs : t.delta_cs;
         q.ldout = p->ldz;
         q.out_chunk_stride = p->qchunksA > 1 ? (int64_t)p->P * p->ldz : 0;
+        q.gout = p->gT;
+        q.gout_cs = p->gT_cs;
+        q.ldg = p->N;
     } else {
         q.out = out ? out : p->lik_buf;   // dummy when not writing S
         q.out_cs = out ? (int64_t)p->N * p->P : 0;
@@ -520,8 +521,10 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         q.Q = t.act + t.h_off.back();
         q.q_cs = t.act_cs;
         q.ldq = p->ldz;
-        q.Y = p->yT;
+        q.Y = p->gT;           // G^T written by side A: no S recompute on this side
         q.ldy = p->N;
+        q.y_cs = p->gT_cs;
+        q.load_g = 1;
         q.b0 = p->packed;
         q.b0_cs = p->dp;
         q.out = p->partB;
