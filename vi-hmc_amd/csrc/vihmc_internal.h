@@ -128,6 +128,28 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
                                double* lp_part, hipStream_t s);
 
+// Fused hidden-layer forward (width 100 -> 100 layers of both nets, one launch): every wave keeps 16 rows
+// of activations in registers through all fused layers; per layer the weights + bias of the next layer
+// are prefetched into registers and written to the second of two LDS buffers. h_j of every layer is
+// stored (the backward needs it). Layer j's W block and bias are contiguous in the packed layout.
+constexpr int FUSED_MAXL = 16;
+constexpr int FUSED_WAVES = 12;
+struct FusedNet {
+    const float* in; int64_t in_cs; int32_t ldin;   // activations feeding the first fused layer
+    float* out; int64_t out_cs; int32_t ldo;        // per-chain activation buffer, row stride of h_j
+    int64_t h_off[FUSED_MAXL];                      // h_j offset inside the activation buffer
+    int64_t w_off[FUSED_MAXL];                      // packed offset of W_j [100][100] (+ bias right after)
+    int32_t act[FUSED_MAXL];
+    int32_t nl, rows, nblk;                         // nblk = ceil(rows / (16 * FUSED_WAVES))
+};
+struct FusedArgs {
+    FusedNet net[2];
+    const float* packed; int64_t dp;
+    int32_t C;
+};
+hipError_t launch_fwd_fused(const FusedArgs& a, hipStream_t s);
+size_t fwd_fused_lds_bytes();
+
 // BNN: one wave per chain, everything in registers / LDS.
 struct MlpLayer { int32_t w_off, b_off, n_out, n_in, act; };
 struct MlpArgs {

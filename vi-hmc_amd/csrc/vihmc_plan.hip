@@ -406,10 +406,61 @@ inline int rowdot_tpw(int64_t total_tiles) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(8, cdiv(total_tiles, (int64_t)768)));
 }
 
-// Forward through both MLPs (grouped launches: branch + trunk layer j together).
+#ifndef VIHMC_FUSED_FWD
+#define VIHMC_FUSED_FWD 1
+#endif
+
+// Layers 1..L-1 of both nets can run in the fused register-resident forward (vihmc_fused.hip) when they
+// are all 100 -> 100 with the packed [W | bias] block contiguous.
+bool fused_forward_ok(const vihmc_plan* p) {
+    if (!VIHMC_FUSED_FWD) return false;
+    for (int net = 0; net < 2; ++net) {
+        const Net& n = p->nets[net];
+        const int nl = (int)n.L.size();
+        if (nl < 2 || nl - 1 > FUSED_MAXL || n.L[0].ldo < 100) return false;
+        for (int j = 1; j < nl; ++j) {
+            const LayerPk& L = n.L[j];
+            if (L.n_in != 100 || L.n_out != 100 || L.ldi != 100 || L.ldo != 100 || L.bias != L.wp + 100 * 100)
+                return false;
+        }
+    }
+    return true;
+}
+
+int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s) {
+    FusedArgs a{};
+    a.C = C;
+    a.packed = p->packed;
+    a.dp = p->dp;
+    for (int net = 0; net < 2; ++net) {
+        Net& n = p->nets[net];
+        FusedNet& f = a.net[net];
+        f.in = n.act + n.h_off[0];
+        f.in_cs = n.act_cs;
+        f.ldin = n.L[0].ldo;
+        f.out = n.act;
+        f.out_cs = n.act_cs;
+        f.ldo = 100;
+        f.nl = (int)n.L.size() - 1;
+        for (int j = 1; j < (int)n.L.size(); ++j) {
+            f.h_off[j - 1] = n.h_off[j];
+            f.w_off[j - 1] = n.L[j].wp;
+            f.act[j - 1] = n.L[j].act;
+        }
+        f.rows = n.rows;
+        f.nblk = cdiv(n.rows, 16 * FUSED_WAVES);
+    }
+    HIPCHK(launch_fwd_fused(a, s));
+    return 0;
+}
+
+// Forward through both MLPs (grouped launches: branch + trunk layer j together); the hidden 100 -> 100
+// stack goes through the fused kernel when its shape allows.
 int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
     const int maxl = (int)std::max(p->nets[0].L.size(), p->nets[1].L.size());
+    const bool fused = fused_forward_ok(p);
     for (int j = 0; j < maxl; ++j) {
+        if (j == 1 && fused) return launch_forward_fused(p, C, s);
         RowdotArgs a{};
         a.C = C;
         int nt = 1;
