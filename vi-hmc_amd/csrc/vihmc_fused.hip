@@ -26,7 +26,7 @@ namespace {
 
 constexpr int FW = 100;                  // layer width (n_in == n_out)
 constexpr int FLDB = 104;                // LDS row stride (== 8 mod 16)
-constexpr int FBUF = FW * FLDB + 112;    // one weight buffer: 100 rows + bias (zero padded to 112)
+constexpr int FBUF = FW * FLDB + 116;    // one weight buffer: 100 rows + bias (zero padded to 112) + dump float4
 constexpr int FTHREADS = FUSED_WAVES * 64;
 constexpr int FBLK4 = (FW * FW + FW) / 4;                        // float4 in W + bias (2525)
 constexpr int FSLOTS = (FBLK4 + FTHREADS - 1) / FTHREADS;        // per thread (4)
@@ -148,20 +148,20 @@ __global__ __launch_bounds__(FTHREADS, 1) void k_fwd_fused(FusedArgs args) {
     for (int v = 0; v < FSLOTS; ++v) {
         const int i = tid + FTHREADS * v;
         sl[v] = i < FW * FW / 4 ? (i / (FW / 4)) * FLDB + 4 * (i % (FW / 4))
-                                : (i < FBLK4 ? FW * FLDB + 4 * (i - FW * FW / 4) : -1);
+                                : (i < FBLK4 ? FW * FLDB + 4 * (i - FW * FW / 4) : FW * FLDB + 112);  // idle: dump
     }
     // zero the bias padding (columns 100..111) of both buffers once
     if (tid < 24) fsm[(tid / 12) * FBUF + FW * FLDB + FW + (tid % 12)] = 0.f;
-    float4 pf[FSLOTS];
+    f32x4 pf[FSLOTS];   // native vector type: a HIP float4 struct array here was left in scratch (memcpy)
 #define VIHMC_FW_LOAD(J)                                                                              \
     {                                                                                                 \
-        const float4* src = reinterpret_cast<const float4*>(Wc + N.w_off[J]);                         \
+        const f32x4* src = reinterpret_cast<const f32x4*>(Wc + N.w_off[J]);                           \
         _Pragma("unroll") for (int v = 0; v < FSLOTS; ++v)                                            \
             pf[v] = src[min(tid + FTHREADS * v, FBLK4 - 1)];                                          \
     }
 #define VIHMC_FW_STORE(BUF)                                                                           \
     _Pragma("unroll") for (int v = 0; v < FSLOTS; ++v)                                                \
-        if (sl[v] >= 0) *reinterpret_cast<float4*>(fsm + (BUF) * FBUF + sl[v]) = pf[v];
+        *reinterpret_cast<f32x4*>(fsm + (BUF) * FBUF + sl[v]) = pf[v];
 
     VIHMC_FW_LOAD(0)
     // A operand of the first fused layer: k-permuted float4 per 16-wide k-block + the 4-wide tail
@@ -174,14 +174,19 @@ __global__ __launch_bounds__(FTHREADS, 1) void k_fwd_fused(FusedArgs args) {
         atl = ar[96 + lg];
     }
     VIHMC_FW_STORE(0)
+    // drain the entry loads here: otherwise the waitcnt pass, merging the loop-entry state (a[] still in
+    // flight) with the back edge, puts vmcnt waits before the MFMAs of EVERY layer -- which then also
+    // wait for the previous layer's h stores (stores count in vmcnt)
+    __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0) expcnt(7) lgkmcnt(15)
 
     const float* outc = N.out + c * N.out_cs;
     const uint32_t ooff = rok ? (uint32_t)row * (uint32_t)N.ldo * 4u : OOB;
     const uint32_t obytes = (uint32_t)N.rows * (uint32_t)N.ldo * 4u;
     for (int j = 0; j < N.nl; ++j) {
         __syncthreads();                        // buffer j&1 complete; buffer (j+1)&1 no longer read
-        const bool more = j + 1 < N.nl;
-        if (more) VIHMC_FW_LOAD(j + 1)
+        // unconditional prefetch (the last layer reloads its own block into the idle buffer): keeps pf in
+        // registers -- a conditional load/store pair around the layer body put it in scratch
+        VIHMC_FW_LOAD(min(j + 1, N.nl - 1))
         const float* wb = fsm + (j & 1) * FBUF;
         const __amdgpu_buffer_rsrc_t orsrc = make_rsrc(outc + N.h_off[j], obytes);
         float4 na[6];
@@ -190,7 +195,7 @@ __global__ __launch_bounds__(FTHREADS, 1) void k_fwd_fused(FusedArgs args) {
         if (act == ACT_TANH) fused_layer<ACT_TANH>(wb, a, atl, lr, lg, orsrc, ooff, na, h6);
         else if (act == ACT_RELU) fused_layer<ACT_RELU>(wb, a, atl, lr, lg, orsrc, ooff, na, h6);
         else fused_layer<ACT_ID>(wb, a, atl, lr, lg, orsrc, ooff, na, h6);
-        if (more) VIHMC_FW_STORE((j + 1) & 1)
+        VIHMC_FW_STORE((j + 1) & 1)
 #pragma unroll
         for (int kb = 0; kb < 6; ++kb) a[kb] = na[kb];
         // tail operand: lane (lr, lg) needs h[lr][96 + lg], held by lane lr (lg = 0) in component lg
