@@ -15,6 +15,10 @@
 // 4 apart (lane groups 0/1 and 2/3 of each half-wave) are 16 banks apart.
 #include "vihmc_internal.h"
 
+#ifndef VIHMC_CONTRACT_WS
+#define VIHMC_CONTRACT_WS 1
+#endif
+
 namespace vihmc {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -239,6 +243,198 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
 #undef VIHMC_LOAD_CHUNK
 #undef VIHMC_STORE_CHUNK
 
+// =============================================================================================
+// Side A (gradient), width 100, wave-specialised: a 512-thread workgroup = 4 S waves + 4 D waves for
+// the same 128 owner rows.
+//   S wave w : owns 32 rows of Own in registers; per 16-row Q chunk computes S, G = gscale (S + b0 - y),
+//              the likelihood sums, stores G^T for side B and hands G (its accumulator registers, as
+//              two float4 per lane) to D wave w through LDS.
+//   D wave w : one chunk behind, dOwn += G^T Q with G from LDS and Q[q][j] from the chunk's LDS image.
+// Each role fits in 128 VGPRs (4 waves/SIMD at 2 workgroups/CU) where the single-role kernel needs 184
+// (2 waves/SIMD). Q chunks rotate through 3 LDS buffers (S reads i, D reads i-1, the prefetch of i+1 is
+// written), G through 2; one barrier per step; the two roles run separate loops with the same barrier
+// sequence so each is register-allocated for its own work.
+// =============================================================================================
+namespace {
+constexpr int CWS_QBUF = CONTRACT_QC * 100;                 // floats per Q chunk image (LDQ = 100)
+constexpr int CWS_GBUF = 4 * 2 * 64;                        // float4 per G buffer (4 waves x 2 x 64 lanes)
+}
+
+__global__ __launch_bounds__(512, 2) void k_contract_ws(ContractProb P) {
+    constexpr int QC = CONTRACT_QC;
+    constexpr int LDQ = 100, LDQ4 = 25;
+    static_assert(QC == 16, "k_contract_ws: 16-row chunks");
+    extern __shared__ float sm[];
+    f32x4* qs4 = reinterpret_cast<f32x4*>(sm);
+    f32x4* gb = reinterpret_cast<f32x4*>(sm + 3 * CWS_QBUF);
+    int b = blockIdx.x;
+    const int per_chain = P.o_tiles * P.q_chunks;
+    const int c = b / per_chain;
+    b -= c * per_chain;
+    const int qc = b / P.o_tiles;
+    const int og = b - qc * P.o_tiles;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int w = wave & 3;
+    const float* Q = P.Q + c * P.q_cs;
+    const int o0 = og * CONTRACT_OWN_PER_WG + w * 32;
+    const int q_lo = qc * P.q_per_chunk;
+    const int q_hi = min(q_lo + P.q_per_chunk, P.Mq);
+    const int nchunks = q_hi > q_lo ? (q_hi - q_lo + QC - 1) / QC : 0;
+
+    // chunk staging: 16 x 25 float4, one per thread (threads >= 400 stage a duplicate into a dump slot)
+    const int sr = min(tid, 399) / 25, sc = min(tid, 399) % 25;
+    const int sdst = tid < 400 ? sr * LDQ4 + sc : -1;
+    f32x4 stg;
+#define VIHMC_CWS_LOAD(CI) \
+    stg = reinterpret_cast<const f32x4*>(Q + (int64_t)min(q_lo + (CI) * QC + sr, P.Mq - 1) * P.ldq)[sc];
+#define VIHMC_CWS_STORE(BUF) \
+    if (sdst >= 0) qs4[(BUF) * (CWS_QBUF / 4) + sdst] = stg;
+
+    if (nchunks > 0) {
+        VIHMC_CWS_LOAD(0)
+        VIHMC_CWS_STORE(0)
+        VIHMC_CWS_LOAD(min(1, nchunks - 1))
+    }
+
+    if (wave < 4) {
+        // ---------------- S role ----------------
+        const float* Own = P.Own + c * P.own_cs;
+        const float* Yc = P.Y + c * P.y_cs;
+        const float b0 = P.b0[c * P.b0_cs];
+        float4 ob[2][6];
+        float otl[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const float* orow = Own + (int64_t)min(o0 + 16 * s + lr, P.Mo - 1) * P.ldown;
+#pragma unroll
+            for (int bb = 0; bb < 6; ++bb) ob[s][bb] = *reinterpret_cast<const float4*>(orow + 16 * bb + 4 * lg);
+            otl[s] = orow[96 + lg];
+        }
+        double ssq = 0.0, gsum = 0.0;
+        float* gw = P.gout ? P.gout + c * P.gout_cs : nullptr;
+        for (int i = 0; i <= nchunks; ++i) {
+            __syncthreads();
+            if (i < nchunks) {
+                const int q0 = q_lo + i * QC;
+                const float* cur = sm + (i % 3) * CWS_QBUF;
+                float yv[2][4];
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        yv[s][r] = Yc[(int64_t)min(q0 + 4 * lg + r, P.Mq - 1) * P.ldy + min(o0 + 16 * s + lr, P.Mo - 1)];
+                f32x4 sacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+                const float4* qrow4 = reinterpret_cast<const float4*>(cur) + lr * LDQ4;
+#pragma unroll
+                for (int bb = 0; bb < 6; ++bb) {
+                    const float4 qa = qrow4[4 * bb + lg];
+                    sacc[0] = mfma_c(qa.x, ob[0][bb].x, sacc[0]);
+                    sacc[1] = mfma_c(qa.x, ob[1][bb].x, sacc[1]);
+                    sacc[0] = mfma_c(qa.y, ob[0][bb].y, sacc[0]);
+                    sacc[1] = mfma_c(qa.y, ob[1][bb].y, sacc[1]);
+                    sacc[0] = mfma_c(qa.z, ob[0][bb].z, sacc[0]);
+                    sacc[1] = mfma_c(qa.z, ob[1][bb].z, sacc[1]);
+                    sacc[0] = mfma_c(qa.w, ob[0][bb].w, sacc[0]);
+                    sacc[1] = mfma_c(qa.w, ob[1][bb].w, sacc[1]);
+                }
+                {
+                    const float qa = cur[lr * LDQ + 96 + lg];
+                    sacc[0] = mfma_c(qa, otl[0], sacc[0]);
+                    sacc[1] = mfma_c(qa, otl[1], sacc[1]);
+                }
+                f32x4 g[2];
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int qq = q0 + 4 * lg + r;
+                        const int oo = o0 + 16 * s + lr;
+                        const bool ok = (qq < q_hi) && (oo < P.Mo);
+                        const float rv = sacc[s][r] + b0 - yv[s][r];
+                        g[s][r] = ok ? P.gscale * rv : 0.f;
+                        if (ok) {
+                            ssq += (double)rv * (double)rv;
+                            gsum += (double)g[s][r];
+                        }
+                    }
+                f32x4* gdst = gb + ((i & 1) * 4 + w) * 128;
+                gdst[lane] = g[0];
+                gdst[64 + lane] = g[1];
+                if (gw) {
+                    const int qq = q0 + 4 * lg;
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int oo = o0 + 16 * s + lr;
+                        if (oo >= P.Mo) continue;
+                        float* dst = gw + (int64_t)oo * P.ldg + qq;
+                        if (qq + 3 < q_hi) {
+                            *reinterpret_cast<f32x4*>(dst) = g[s];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (qq + r < q_hi) dst[r] = g[s][r];
+                        }
+                    }
+                }
+            }
+            VIHMC_CWS_STORE((i + 1) % 3)
+            VIHMC_CWS_LOAD(max(min(i + 2, nchunks - 1), 0))
+        }
+        if (P.with_stats) {
+            ssq = wave_sum_c(ssq);
+            gsum = wave_sum_c(gsum);
+            if (lane == 0) {
+                double* st = P.stats + c * P.stats_cs + 2 * (int64_t)((qc * P.o_tiles + og) * 4 + w);
+                st[0] = ssq;
+                st[1] = gsum;
+            }
+        }
+        return;
+    }
+
+    // ---------------- D role ----------------
+    f32x4 dacc[2][7];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) dacc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i <= nchunks; ++i) {
+        __syncthreads();
+        if (i >= 1) {
+            const float* cur = sm + ((i - 1) % 3) * CWS_QBUF;
+            const f32x4* gsrc = gb + (((i - 1) & 1) * 4 + w) * 128;
+            const f32x4 g0 = gsrc[lane], g1 = gsrc[64 + lane];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const float* qr = cur + (4 * lg + rr) * LDQ;
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    const float bq = qr[min(16 * t + lr, 99)];
+                    dacc[0][t] = mfma_c(g0[rr], bq, dacc[0][t]);
+                    dacc[1][t] = mfma_c(g1[rr], bq, dacc[1][t]);
+                }
+            }
+        }
+        VIHMC_CWS_STORE((i + 1) % 3)
+        VIHMC_CWS_LOAD(max(min(i + 2, nchunks - 1), 0))
+    }
+    float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int j = 16 * t + lr;
+            if (j >= P.ldout) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int oo = o0 + 16 * s + 4 * lg + r;
+                if (oo < P.Mo) out[(int64_t)oo * P.ldout + j] = (j < 100) ? dacc[s][t][r] : 0.f;
+            }
+        }
+#undef VIHMC_CWS_LOAD
+#undef VIHMC_CWS_STORE
+}
+
 size_t contract_lds_bytes(int W) { return sizeof(float) * 2 * CONTRACT_QC * contract_ldq(W); }
 
 #define VIHMC_LAUNCH_C(kern, grid, block, shm, s, ...) \
@@ -249,6 +445,10 @@ static hipError_t launch_contract_t(const ContractProb& p, int C, hipStream_t s)
     dim3 g(C * p.o_tiles * p.q_chunks), blk(256);
     const size_t shm = contract_lds_bytes(p.W);
     const int w = p.W;
+    if (w == 100 && GRAD && !LOADG && VIHMC_CONTRACT_WS) {
+        dim3 blk2(512);
+        VIHMC_LAUNCH_C(k_contract_ws, g, blk2, sizeof(float) * 3 * CWS_QBUF + 16 * 2 * CWS_GBUF, s, p);
+    }
     if (w == 100) VIHMC_LAUNCH_C((k_contract2<112, 6, 1, GRAD, LOADG>), g, blk, shm, s, p);
     if (w <= 16) VIHMC_LAUNCH_C((k_contract2<16, -1, -1, GRAD, LOADG>), g, blk, shm, s, p);
     if (w <= 32) VIHMC_LAUNCH_C((k_contract2<32, -1, -1, GRAD, LOADG>), g, blk, shm, s, p);
