@@ -15,6 +15,9 @@
 // 4 apart (lane groups 0/1 and 2/3 of each half-wave) are 16 banks apart.
 #include "vihmc_internal.h"
 
+#ifndef VIHMC_CWS_YPF
+#define VIHMC_CWS_YPF 0     // A/B (profiles/README.md): draining right after the next chunk's y loads measured faster (0.64 vs 0.67 ms)
+#endif
 #ifndef VIHMC_CONTRACT_WS
 #define VIHMC_CONTRACT_WS 1
 #endif
@@ -112,6 +115,13 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
         VIHMC_LOAD_CHUNK(q_lo)
         VIHMC_STORE_CHUNK(qs4)
     }
+    // targets (side B: G) are loaded one chunk ahead so their HBM latency hides under the previous chunk
+    float yn[2][4];
+#define VIHMC_C2_YLOAD(QROW0)                                                                         \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                    \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r)                                                \
+            yn[s][r] = Yc[(int64_t)min((QROW0) + 4 * lg + r, P.Mq - 1) * P.ldy + min(o0 + 16 * s + lr, P.Mo - 1)];
+    VIHMC_C2_YLOAD(q_lo)
     __syncthreads();
     for (int ci = 0; ci < nchunks; ++ci) {
         const int q0 = q_lo + ci * QC;
@@ -123,9 +133,8 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
 #pragma unroll
             for (int s = 0; s < 2; ++s)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    yv[s][r] = Yc[(int64_t)min(q0 + 16 * h + 4 * lg + r, P.Mq - 1) * P.ldy +
-                                   min(o0 + 16 * s + lr, P.Mo - 1)];
+                for (int r = 0; r < 4; ++r) yv[s][r] = yn[s][r];
+            VIHMC_C2_YLOAD(min(q0 + QC, q_hi - 1))
             if (more) {
                 VIHMC_LOAD_CHUNK(q0 + QC)
             }
@@ -312,6 +321,14 @@ __global__ __launch_bounds__(512, 2) void k_contract_ws(ContractProb P) {
         }
         double ssq = 0.0, gsum = 0.0;
         float* gw = P.gout ? P.gout + c * P.gout_cs : nullptr;
+        // targets are loaded one chunk ahead (HBM latency hidden under a chunk of MFMAs)
+        float yn[2][4];
+#define VIHMC_CWS_YLOAD(CI)                                                                          \
+        _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                \
+            _Pragma("unroll") for (int r = 0; r < 4; ++r)                                            \
+                yn[s][r] = Yc[(int64_t)min(q_lo + (CI) * QC + 4 * lg + r, P.Mq - 1) * P.ldy +         \
+                              min(o0 + 16 * s + lr, P.Mo - 1)];
+        VIHMC_CWS_YLOAD(0)
         for (int i = 0; i <= nchunks; ++i) {
             __syncthreads();
             if (i < nchunks) {
@@ -321,8 +338,13 @@ __global__ __launch_bounds__(512, 2) void k_contract_ws(ContractProb P) {
 #pragma unroll
                 for (int s = 0; s < 2; ++s)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        yv[s][r] = Yc[(int64_t)min(q0 + 4 * lg + r, P.Mq - 1) * P.ldy + min(o0 + 16 * s + lr, P.Mo - 1)];
+                    for (int r = 0; r < 4; ++r) yv[s][r] = yn[s][r];
+                if (VIHMC_CWS_YPF) {
+                    VIHMC_CWS_YLOAD(min(i + 1, nchunks - 1))
+                } else {
+                    VIHMC_CWS_YLOAD(min(i + 1, nchunks - 1))
+                    __builtin_amdgcn_s_waitcnt(0x0F70);
+                }
                 f32x4 sacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
                 const float4* qrow4 = reinterpret_cast<const float4*>(cur) + lr * LDQ4;
 #pragma unroll
@@ -433,6 +455,7 @@ __global__ __launch_bounds__(512, 2) void k_contract_ws(ContractProb P) {
         }
 #undef VIHMC_CWS_LOAD
 #undef VIHMC_CWS_STORE
+#undef VIHMC_CWS_YLOAD
 }
 
 size_t contract_lds_bytes(int W) { return sizeof(float) * 2 * CONTRACT_QC * contract_ldq(W); }

@@ -18,6 +18,7 @@
 
 #include "vihmc.h"
 #include "vihmc_internal.h"
+#include <cstdlib>
 
 using namespace vihmc;
 
@@ -333,6 +334,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         // dZ_trunk slabs + fixed-order reduce) only when too few workgroups would fill the chip
         const int og_a = cdiv(p->P, CONTRACT_OWN_PER_WG), og_b = cdiv(p->N, CONTRACT_OWN_PER_WG);
         int qa = std::max(1, std::min(8, (int)std::lround(1024.0 / ((double)C * og_a))));
+        if (const char* e = std::getenv("VIHMC_QSPLIT_A")) qa = std::max(1, std::min(64, std::atoi(e)));
         p->qperA = (int)(((int64_t)cdiv(p->N, qa) + CONTRACT_QC - 1) / CONTRACT_QC * CONTRACT_QC);
         p->qchunksA = cdiv(p->N, p->qperA);
         if (p->qchunksA > 1) {
@@ -341,6 +343,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         }
         // side B: workgroups own 128 branch rows, the trunk sweep is split to match side A's grid
         int qc = std::max(1, (int)std::lround((double)og_a * p->qchunksA / og_b));
+        if (const char* e = std::getenv("VIHMC_QSPLIT_B")) qc = std::max(1, std::min(256, std::atoi(e)));
         p->qperB = (int)(((int64_t)cdiv(p->P, qc) + CONTRACT_QC - 1) / CONTRACT_QC * CONTRACT_QC);
         p->qchunksB = cdiv(p->P, p->qperB);
         p->partB_cs = r64((int64_t)p->qchunksB * p->N * p->ldz);
