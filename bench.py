@@ -175,7 +175,7 @@ def main():
         "hamiltorch_equiv_grad_evals_per_s": world * C * (args.L + 1) * args.steps / T,
         "eval_tflops_algorithmic": evals_per_s * spec.flops_per_grad_eval(prob.N, prob.P) / 1e12,
         "accept_rate": acc_rate,
-        "roofline": {"kernel": "k_contract2<112,6,1,true> side A (fused branch x trunk contraction + NLL + dZ_trunk)",
+        "roofline": {"kernel": "k_contract_ws: side-A contraction (branch x trunk S, Gaussian NLL, G, dZ_trunk)",
                      "bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
                      "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE; profiles/traffic_contract.json)",

@@ -3,7 +3,8 @@
 Usage: python profiles/traffic_from_pmc.py <fetch_dir> <write_dir> <out.json> [chains_per_gpu]
   <fetch_dir>: rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE  -- python3 bench.py ...
   <write_dir>: rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE  -- python3 bench.py ...
-Side-A contraction launches are the first k_contract2 dispatch of every evaluation (side B follows it).
+Side-A contraction launches are the k_contract_ws dispatches (the wave-specialised side-A kernel; side B
+runs k_contract2<..., LOADG>).
 gfx950 correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE reports 1/2 of the bytes of wide
 coalesced streaming reads -> doubled; WRITE_SIZE is exact for 16-B-per-lane stores. Both are KB.
 bench.py reads the resulting JSON into roofline.traffic when its config matches.
@@ -13,7 +14,7 @@ import glob
 import json
 import sys
 
-KERNEL = "k_contract2"
+KERNEL = "k_contract_ws"
 
 
 def side_a_values(d, counter):
@@ -24,7 +25,7 @@ def side_a_values(d, counter):
                 if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
                     rows.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     rows.sort()
-    return [v for i, (_, v) in enumerate(rows) if i % 2 == 0]
+    return [v for _, v in rows]
 
 
 def main():
@@ -34,7 +35,7 @@ def main():
     wa = side_a_values(wd, "WRITE_SIZE")
     fetch = 2.0 * 1024.0 * sum(fa) / len(fa)
     write = 1024.0 * sum(wa) / len(wa)
-    res = {"kernel": "k_contract2<112,6,1,true> side A", "chains_per_gpu": C, "launches_fetch": len(fa),
+    res = {"kernel": "k_contract_ws (side A)", "chains_per_gpu": C, "launches_fetch": len(fa),
            "launches_write": len(wa), "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": fetch + write,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over bench.py; FETCH x2 (gfx950)"}

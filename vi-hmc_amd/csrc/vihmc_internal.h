@@ -44,16 +44,7 @@ struct RowdotArgs {
 // plus the bias gradient part[chunk][n_out*ldh + n] = sum_m D[m][n]. One partial per row chunk,
 // reduced in fixed order by k_reduce_partials (deterministic, no atomics).
 // ---------------------------------------------------------------------------------------------
-struct ColsumProb {
-    const float* D; int64_t d_cs; int32_t ldd;
-    const float* H; int64_t h_cs; int32_t ldh;
-    float* part;    int64_t part_cs;   // per chain: n_chunks * (n_out*ldh + n_out_pad)
-    int32_t M, n_out, n_in, rows_per_chunk, n_chunks, n_pairs, part_stride;
-};
-struct ColsumArgs {
-    ColsumProb p[2];
-    int32_t nprob, C;
-};
+
 
 // ---------------------------------------------------------------------------------------------
 // Fused backward of one linear layer l (grouped branch + trunk):
@@ -107,7 +98,6 @@ struct ContractProb {
 
 // launchers (vihmc_kernels.hip)
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s);
-hipError_t launch_colsum(const ColsumArgs& a, int jt, hipStream_t s);
 hipError_t launch_contract(const ContractProb& p, int C, bool with_grad, hipStream_t s);
 size_t contract_lds_bytes(int W);
 hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* frozen, const int32_t* map_w,

@@ -1,8 +1,9 @@
 // Layer GEMMs of the two MLPs (branch: N rows, trunk: P rows), batched over chains and grouped
 // branch+trunk per launch.
-//   k_rowdot2 : forward layer  h = act(x W^T + b)                   (F.linear + tanh, my_make_func.py:52-77)
-//               backward input delta_{l-1} = (delta_l W) * act'(h)  (autograd of the same)
-//   k_colsum  : weight / bias gradients dW = delta^T h, db = sum delta, per row chunk (fixed-order reduce)
+//   k_rowdot2 : forward layer  h = act(x W^T + b)   (F.linear + tanh, my_make_func.py:52-77); used for the
+//               input layers (K = 101 / 5) and any shape the fused forward (vihmc_fused.hip) does not take
+//   k_bwd_ws  : layer backward (autograd of the same): delta_{l-1} = (delta_l W) * act'(h) and the dW / db
+//               partial slabs in one pass
 // fp32 MFMA v_mfma_f32_16x16x4_f32; operand maps and the float4 k-permutation: see vihmc_kernels.hip.
 #include "vihmc_internal.h"
 
@@ -279,110 +280,6 @@ __global__ __launch_bounds__(256, 3) void k_rowdot2(RowdotArgs args) {
 }
 
 // =============================================================================================
-// Column-sum GEMM (weight + bias gradients): one wave per (chain, row chunk, pair of 16-row
-// output sub-tiles); partial slabs are reduced in fixed order afterwards.
-// =============================================================================================
-template <int JT>
-__global__ __launch_bounds__(64) void k_colsum(ColsumArgs args) {
-    int b = blockIdx.x;
-    const int per0 = args.C * args.p[0].n_chunks * args.p[0].n_pairs;
-    const bool second = b >= per0;
-    const ColsumProb P = second ? args.p[1] : args.p[0];
-    if (second) b -= per0;
-    const int per_chain = P.n_chunks * P.n_pairs;
-    const int c = b / per_chain;
-    b -= c * per_chain;
-    const int chunk = b / P.n_pairs;
-    const int pair = b - chunk * P.n_pairs;
-    const int lane = threadIdx.x, lr = lane & 15, lg = lane >> 4;
-    const float* D = P.D + c * P.d_cs;
-    const float* H = P.H + c * P.h_cs;
-    const int r0 = chunk * P.rows_per_chunk;
-    const int r1 = min(r0 + P.rows_per_chunk, P.M);
-
-    int ncol[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) ncol[s] = min(32 * pair + 16 * s + lr, P.n_out - 1);
-    int jcol[JT];
-#pragma unroll
-    for (int t = 0; t < JT; ++t) jcol[t] = min(16 * t + lr, P.n_in - 1);
-
-    f32x4 acc[2][JT];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int t = 0; t < JT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float dsum[2] = {0.f, 0.f};
-
-    // operands for U row-steps of 4 rows are loaded one group ahead (register double buffer) so the
-    // L2 latency of group g+1 hides under the MFMAs of group g
-    constexpr int U = 2;
-    float a_c[U][2], h_c[U][JT], a_n[U][2], h_n[U][JT];
-#define VIHMC_COLSUM_LOAD(M0, AA, HH)                                                          \
-    _Pragma("unroll") for (int u = 0; u < U; ++u) {                                            \
-        const int mm = (M0) + 4 * u + lg;                                                      \
-        const bool mok = mm < r1;                                                              \
-        const int mr = mok ? mm : r0;                                                          \
-        const float* drow = D + (int64_t)mr * P.ldd;                                           \
-        const float* hrow = H + (int64_t)mr * P.ldh;                                           \
-        _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                        \
-            const float v = drow[ncol[s]];                                                     \
-            AA[u][s] = mok ? v : 0.f;                                                          \
-        }                                                                                      \
-        _Pragma("unroll") for (int t = 0; t < JT; ++t) HH[u][t] = hrow[jcol[t]];               \
-    }
-    VIHMC_COLSUM_LOAD(r0, a_c, h_c)
-    for (int m = r0; m < r1; m += 4 * U) {
-        const bool more = m + 4 * U < r1;
-        if (more) {
-            VIHMC_COLSUM_LOAD(m + 4 * U, a_n, h_n)
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-#pragma unroll
-            for (int t = 0; t < JT; ++t)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) acc[s][t] = mfma(a_c[u][s], h_c[u][t], acc[s][t]);
-            dsum[0] += a_c[u][0];
-            dsum[1] += a_c[u][1];
-        }
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                a_c[u][0] = a_n[u][0];
-                a_c[u][1] = a_n[u][1];
-#pragma unroll
-                for (int t = 0; t < JT; ++t) h_c[u][t] = h_n[u][t];
-            }
-        }
-    }
-#undef VIHMC_COLSUM_LOAD
-
-    float* part = P.part + c * P.part_cs + (int64_t)chunk * P.part_stride;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int t = 0; t < JT; ++t) {
-            const int j = 16 * t + lr;
-            if (j >= P.ldh) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int n = 32 * pair + 16 * s + 4 * lg + r;
-                if (n < P.n_out) part[(int64_t)n * P.ldh + j] = (j < P.n_in) ? acc[s][t][r] : 0.f;
-            }
-        }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        float v = dsum[s];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        const int n = 32 * pair + 16 * s + lr;
-        if (lg == 0 && n < P.n_out) part[(int64_t)P.n_out * P.ldh + n] = v;
-    }
-}
-
-
-// =============================================================================================
 // Fused layer backward (see BwdProb), wave-specialised: a 512-thread workgroup = 4 dX waves + 4 dW
 // waves sharing one LDS image of W^T (staged once) and of each 32-row sub-tile of delta_l and h_{l-1}
 // (register prefetch of the next sub-tile by all 8 waves while the current one is consumed).
@@ -641,8 +538,9 @@ static hipError_t rowdot_nt(const RowdotArgs& a, int nt, hipStream_t s) {
 }
 
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s) {
-    if (ms == 1) return mode == MODE_FWD ? rowdot_nt<1, MODE_FWD>(a, nt, s) : rowdot_nt<1, MODE_BWD>(a, nt, s);
-    return mode == MODE_FWD ? rowdot_nt<2, MODE_FWD>(a, nt, s) : rowdot_nt<2, MODE_BWD>(a, nt, s);
+    // only the forward mode is launched (the layer backward is k_bwd_ws)
+    if (mode != MODE_FWD) return hipErrorInvalidValue;
+    return ms == 1 ? rowdot_nt<1, MODE_FWD>(a, nt, s) : rowdot_nt<2, MODE_FWD>(a, nt, s);
 }
 
 size_t bwd_lds_bytes(const BwdArgs& a) {
@@ -672,23 +570,6 @@ hipError_t launch_bwd(const BwdArgs& a, int nti, hipStream_t s) {
         case 6: VIHMC_LAUNCH_L((k_bwd_ws<6, 0>), g, blk, shm, s, a);
         case 7: VIHMC_LAUNCH_L((k_bwd_ws<7, 0>), g, blk, shm, s, a);
         case 8: VIHMC_LAUNCH_L((k_bwd_ws<8, 0>), g, blk, shm, s, a);
-        default: return hipErrorInvalidValue;
-    }
-}
-
-hipError_t launch_colsum(const ColsumArgs& a, int jt, hipStream_t s) {
-    int blocks = a.C * a.p[0].n_chunks * a.p[0].n_pairs +
-                 (a.nprob > 1 ? a.C * a.p[1].n_chunks * a.p[1].n_pairs : 0);
-    dim3 g(blocks), blk(64);
-    switch (jt) {
-        case 1: VIHMC_LAUNCH_L(k_colsum<1>, g, blk, 0, s, a);
-        case 2: VIHMC_LAUNCH_L(k_colsum<2>, g, blk, 0, s, a);
-        case 3: VIHMC_LAUNCH_L(k_colsum<3>, g, blk, 0, s, a);
-        case 4: VIHMC_LAUNCH_L(k_colsum<4>, g, blk, 0, s, a);
-        case 5: VIHMC_LAUNCH_L(k_colsum<5>, g, blk, 0, s, a);
-        case 6: VIHMC_LAUNCH_L(k_colsum<6>, g, blk, 0, s, a);
-        case 7: VIHMC_LAUNCH_L(k_colsum<7>, g, blk, 0, s, a);
-        case 8: VIHMC_LAUNCH_L(k_colsum<8>, g, blk, 0, s, a);
         default: return hipErrorInvalidValue;
     }
 }
