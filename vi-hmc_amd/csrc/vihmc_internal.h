@@ -54,6 +54,7 @@ struct RowdotArgs {
 // once from HBM for both products), W^T is staged once per workgroup.
 // ---------------------------------------------------------------------------------------------
 constexpr int BWD_SUB = 32;
+
 constexpr int GATHER_SPLIT_MAX = 16;
 struct BwdProb {
     const float* D;  int64_t d_cs;  int32_t ldd;

@@ -315,8 +315,13 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         // nets is ~one resident round (2 workgroups/CU x 256 CUs; the kernel needs ~68 KB of LDS)
         {
             const int64_t rows_all = (int64_t)p->nets[0].rows + p->nets[1].rows;
-            const int64_t want = cdiv((int64_t)C * rows_all, 512);
-            n.rows_per_chunk = (int)std::max<int64_t>(BWD_SUB, (want + BWD_SUB - 1) / BWD_SUB * BWD_SUB);
+            // two 512-thread workgroups per CU, 32-row sub-tiles; the chunk R (a multiple of the sub-tile)
+            // is the smallest for which both nets' workgroups of all max_chains chains fit one resident round
+            const int slots = 512, sub = BWD_SUB;
+            const int64_t r_b = p->nets[0].rows, r_t = p->nets[1].rows;
+            int64_t R = std::max<int64_t>(sub, (cdiv((int64_t)C * rows_all, slots) + sub - 1) / sub * sub);
+            while ((int64_t)C * (cdiv(r_b, R) + cdiv(r_t, R)) > slots && R < rows_all) R += sub;
+            n.rows_per_chunk = (int)R;
         }
         int64_t po = 0;
         for (auto& L : n.L) {
