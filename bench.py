@@ -39,7 +39,9 @@ def parse():
     ap.add_argument("--L", type=int, default=7)
     ap.add_argument("--step-size", type=float, default=1e-4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
-    ap.add_argument("--ess", action="store_true", help="report ESS/s over the timed samples")
+    ap.add_argument("--ess-steps", type=int, default=100,
+                    help="HMC iterations of a separately timed phase after the timed region whose samples give "
+                         "ESS/s (Geyer initial monotone sequence; 0 = skip)")
     ap.add_argument("--gather", action="store_true", help="RCCL all-gather of the sample pool after timing")
     return ap.parse_args()
 
@@ -63,10 +65,55 @@ def cpu_baseline(prob, L, step_size, seconds):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), cpu)
+    except OSError:
+        pass
     return {"value": L * n / dt, "unit": "leapfrog-steps/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": cpu,
             "sample": f"1 chain x {n} HMC samples (L={L}; hamiltorch: L+1 grad + 2 value evals each) in {dt:.1f} s, "
                       f"oracle/deeponet_ref.TorchDeepONetRef (reference torch ops) + oracle/hamiltorch_ref.sample, "
                       f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
+
+
+def ess_phase(args, ev, runner, K, dev, chains, world):
+    """ESS/s: continue every chain for `ess_steps` HMC iterations (fresh per-chain seeds 2000 + c), timed
+    like the main region (barrier + sync, max over ranks); Geyer ESS of the log-prob trace and of every
+    sensitive coordinate over those samples, summed over all chains of the job."""
+    from vihmc.diagnostics import ess
+    from vihmc.samplers import ChainRNG, HMCRunner
+    C = len(chains)
+    idx = (runner.counts - 1).clamp(min=0)
+    theta = runner.samples[torch.arange(C, device=dev), idx].clone()
+    r2 = HMCRunner(ev, theta, args.ess_steps, args.L, args.step_size, burn=0,
+                   rng=ChainRNG(C, K, dev, seeds=[2000 + c for c in chains]))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.ess_steps):
+        r2.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    res = r2.result()
+    n = int(res.counts.min())
+    e_lp = ess(res.logp_trace.double()).sum().reshape(1)
+    e_coord = ess(res.samples[:, 1:n].double().transpose(1, 2)).sum(0)           # [K], summed over chains
+    if world > 1:
+        dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+        dist.all_reduce(e_lp)
+        dist.all_reduce(e_coord)
+    w = float(wall.item())
+    return {"ess_steps": args.ess_steps, "ess_wall_s": w, "ess_logp": float(e_lp.item()),
+            "ess_min": float(e_coord.min().item()), "ess_median": float(e_coord.median().item()),
+            "ess_logp_per_s": float(e_lp.item()) / w, "ess_min_per_s": float(e_coord.min().item()) / w,
+            "ess_median_per_s": float(e_coord.median().item()) / w,
+            "ess_note": "whole job; Geyer IMSE over post-timing samples, summed over chains; "
+                        "eps=1e-4 trajectories are short, so coordinate ESS is low"}
 
 
 def main():
@@ -133,10 +180,8 @@ def main():
         extra["allgather_bytes"] = pool.numel() * 4
     res = runner.result()
     acc_rate = float(res.accepted[:, args.warmup:].float().mean())
-    if args.ess:
-        from vihmc.diagnostics import summarize
-        s = res.samples[:, 1 + args.warmup:int(res.counts.min())]
-        extra.update(summarize(s, res.trace[:, args.warmup:], T))
+    if args.ess_steps > 0:
+        extra.update(ess_phase(args, ev, runner, eng.K, dev, chains, world))
 
     if rank != 0:
         if world > 1:
