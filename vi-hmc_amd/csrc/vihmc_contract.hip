@@ -56,6 +56,13 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
     const int LDQ4 = LDQ >> 2;
     float4* qs4 = reinterpret_cast<float4*>(qs);
     int b = blockIdx.x;
+    if (P.xcd_group) {
+        // workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8): send the o_tiles workgroups of
+        // one (chain, Q chunk) group to one XCD so the chunk is fetched into one L2 once
+        const int xcd = b & 7, k = b >> 3;
+        const int gx = k / P.o_tiles, og = k - gx * P.o_tiles;
+        b = (gx * 8 + xcd) * P.o_tiles + og;
+    }
     const int per_chain = P.o_tiles * P.q_chunks;
     const int c = b / per_chain;
     b -= c * per_chain;

@@ -11,7 +11,7 @@
 // separate memory and MFMA phases disappear. Only the 4-wide k tail (columns 96..99) needs a cross-lane
 // move (4 ds_bpermute).
 //
-// Workgroup = 12 waves (192 rows); the weights + bias of layer j sit in LDS buffer j&1 (row stride 104:
+// Workgroup = 12 waves (192 rows; 4 waves for small chain batches); the weights + bias of layer j sit in LDS buffer j&1 (row stride 104:
 // conflict-free b128 row reads, see rowdot_ldb), layer j+1's are prefetched into registers by all 768
 // threads while layer j computes and stored into the other buffer: one barrier per layer.
 // Blocks are chain-fastest (c = blockIdx % C) so, with C a multiple of 8, all blocks of one chain run on
@@ -27,9 +27,7 @@ namespace {
 constexpr int FW = 100;                  // layer width (n_in == n_out)
 constexpr int FLDB = 104;                // LDS row stride (== 8 mod 16)
 constexpr int FBUF = FW * FLDB + 116;    // one weight buffer: 100 rows + bias (zero padded to 112) + dump float4
-constexpr int FTHREADS = FUSED_WAVES * 64;
 constexpr int FBLK4 = (FW * FW + FW) / 4;                        // float4 in W + bias (2525)
-constexpr int FSLOTS = (FBLK4 + FTHREADS - 1) / FTHREADS;        // per thread (4)
 
 __device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -128,7 +126,12 @@ __device__ __forceinline__ void fused_layer(const float* wb, const float4 (&a)[6
 
 }  // namespace
 
-__global__ __launch_bounds__(FTHREADS, 1) void k_fwd_fused(FusedArgs args) {
+// NW waves per workgroup (16 NW rows): 12 for a full-chip batch of chains, 4 when the 12-wave grid
+// would leave most CUs idle (single chain: 60 workgroups)
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused(FusedArgs args) {
+    constexpr int FTHREADS = NW * 64;
+    constexpr int FSLOTS = (FBLK4 + FTHREADS - 1) / FTHREADS;
     extern __shared__ float fsm[];       // 2 x FBUF
     const int C = args.C;
     const int c = blockIdx.x % C;
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(FTHREADS, 1) void k_fwd_fused(FusedArgs args) {
     if (net) item -= args.net[0].nblk;
     const FusedNet& N = args.net[net];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-    const int row = item * (16 * FUSED_WAVES) + wave * 16 + lr;
+    const int row = item * (16 * NW) + wave * 16 + lr;
     const int rowc = min(row, N.rows - 1);
     const bool rok = row < N.rows;
     const float* Wc = args.packed + c * args.dp;
@@ -211,9 +214,11 @@ __global__ __launch_bounds__(FTHREADS, 1) void k_fwd_fused(FusedArgs args) {
 
 size_t fwd_fused_lds_bytes() { return sizeof(float) * 2 * FBUF; }
 
-hipError_t launch_fwd_fused(const FusedArgs& a, hipStream_t s) {
-    dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk)), blk(FTHREADS);
-    hipLaunchKernelGGL(k_fwd_fused, g, blk, fwd_fused_lds_bytes(), s, a);
+hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s) {
+    dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk));
+    if (nwaves == 12) hipLaunchKernelGGL(k_fwd_fused<12>, g, dim3(12 * 64), fwd_fused_lds_bytes(), s, a);
+    else if (nwaves == 4) hipLaunchKernelGGL(k_fwd_fused<4>, g, dim3(4 * 64), fwd_fused_lds_bytes(), s, a);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

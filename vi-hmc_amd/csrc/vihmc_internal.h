@@ -94,6 +94,8 @@ struct ContractProb {
     int32_t o_tiles, q_chunks, q_per_chunk;   // o_tiles = ceil(Mo / CONTRACT_OWN_PER_WG)
     int32_t with_stats, write_s;
     int32_t load_g;                       // side B: Y holds G (already scaled); no S recompute
+    int32_t xcd_group;                    // 1: the o_tiles workgroups sharing one Q chunk run on one XCD
+                                          //    (requires C * q_chunks % 8 == 0; speed only)
     float gscale;
 };
 
@@ -124,21 +126,20 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
 // are prefetched into registers and written to the second of two LDS buffers. h_j of every layer is
 // stored (the backward needs it). Layer j's W block and bias are contiguous in the packed layout.
 constexpr int FUSED_MAXL = 16;
-constexpr int FUSED_WAVES = 12;
 struct FusedNet {
     const float* in; int64_t in_cs; int32_t ldin;   // activations feeding the first fused layer
     float* out; int64_t out_cs; int32_t ldo;        // per-chain activation buffer, row stride of h_j
     int64_t h_off[FUSED_MAXL];                      // h_j offset inside the activation buffer
     int64_t w_off[FUSED_MAXL];                      // packed offset of W_j [100][100] (+ bias right after)
     int32_t act[FUSED_MAXL];
-    int32_t nl, rows, nblk;                         // nblk = ceil(rows / (16 * FUSED_WAVES))
+    int32_t nl, rows, nblk;                         // nblk = ceil(rows / (16 * waves per workgroup))
 };
 struct FusedArgs {
     FusedNet net[2];
     const float* packed; int64_t dp;
     int32_t C;
 };
-hipError_t launch_fwd_fused(const FusedArgs& a, hipStream_t s);
+hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 size_t fwd_fused_lds_bytes();
 
 // BNN: one wave per chain, everything in registers / LDS.
