@@ -130,6 +130,12 @@ int64_t vihmc_plan_device_bytes(const vihmc_plan* p);
 int vihmc_timing_enable(vihmc_plan* p, int which, int on);
 int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches);
 
+/* hipGraph replay of vihmc_logp_grad (gradient evaluations only): one graph per chain count, captured
+ * on first use, over plan-owned theta/logp/grad buffers that the call copies in / out on `stream`.
+ * Off by default (measured slightly slower than direct launches here); the VIHMC_GRAPH=1 environment
+ * variable turns it on for every plan. (New; no reference counterpart.) */
+int vihmc_graph_enable(vihmc_plan* p, int on);
+
 void        vihmc_plan_destroy(vihmc_plan* p);
 const char* vihmc_last_error(void);
 const char* vihmc_version(void);

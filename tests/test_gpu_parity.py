@@ -93,6 +93,31 @@ def test_deeponet_engine_deterministic(cuda_device):
     assert torch.equal(eng.logp(th), a[0])
 
 
+@pytest.mark.parametrize("kind", ["deeponet", "bnn"])
+def test_graph_replay_bitwise_equal_to_direct_launches(kind, cuda_device):
+    """vihmc_graph_enable: the captured-graph evaluation (plan-owned buffers, copy in / out) returns
+    exactly the direct-launch results, for every chain count it has captured, and across replays."""
+    if kind == "deeponet":
+        c = deeponet_case("deeponet_refshape")
+        eng = engine_for(c, max_chains=4)
+    else:
+        from vihmc.engine import MLPEngine
+        c = bnn_case("bnn_vi_hmc")
+        eng = MLPEngine(c.spec, c.data["x_train"], c.data["y_train"], c.g["mu"], c.idx, c.prior_mu, c.prior_sd,
+                        c.loss, c.tau_out, max_chains=4, device=cuda_device)
+    base = torch.tensor(np.stack(c.thetas), device=cuda_device)
+    for C in (1, 2, 4):
+        th = base[torch.arange(C, device=cuda_device) % base.shape[0]].clone()
+        th[1:] += 1e-3 * torch.arange(1, C, device=cuda_device, dtype=th.dtype)[:, None]
+        eng.graph(False)
+        ref = eng.logp_grad(th)
+        eng.graph(True)
+        for _ in range(2):
+            got = eng.logp_grad(th)
+            assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    eng.graph(False)
+
+
 def test_deeponet_split_shards_engine(cuda_device):
     from vihmc.engine import DeepONetEngine, trunk_features
     g = load("deeponet_split")

@@ -121,6 +121,7 @@ struct vihmc_plan {
     std::vector<std::pair<int, hipGraphExec_t>> graphs;
     hipStream_t cap_stream = nullptr;
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
+    int graph_on = -1;          // -1: follow VIHMC_GRAPH
 
     template <typename T>
     int alloc(T** p, int64_t n) {
@@ -857,7 +858,8 @@ int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float
     return guarded([&]() -> int {
         if (!p || !theta || !logp) return fail("null argument");
         hipStream_t s = static_cast<hipStream_t>(stream);
-        if (grad && !p->timing_on && graphs_enabled()) return eval_graph(p, theta, C, logp, grad, s);
+        const bool g_on = p->graph_on < 0 ? graphs_enabled() : p->graph_on != 0;
+        if (grad && !p->timing_on && g_on) return eval_graph(p, theta, C, logp, grad, s);
         return p->kind == 0 ? deeponet_eval(p, theta, C, logp, grad, nullptr, s)
                             : mlp_eval(p, theta, C, logp, grad, nullptr, s);
     });
@@ -898,6 +900,12 @@ int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches) {
     *total_ms = t;
     *launches = (int64_t)(p->ev_used / 2);
     p->ev_used = 0;
+    return 0;
+}
+
+int vihmc_graph_enable(vihmc_plan* p, int on) {
+    if (!p) return fail("null plan");
+    p->graph_on = on ? 1 : 0;
     return 0;
 }
 

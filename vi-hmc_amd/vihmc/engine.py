@@ -120,6 +120,10 @@ class _Engine:
     def timing(self, which: int = 0, on: bool = True):
         _lib.check(self.L.vihmc_timing_enable(self._plan, which, int(on)), "vihmc_timing_enable")
 
+    def graph(self, on: bool = True):
+        """hipGraph replay of the gradient evaluation (vihmc_graph_enable)."""
+        _lib.check(self.L.vihmc_graph_enable(self._plan, int(on)), "vihmc_graph_enable")
+
     def timing_read(self):
         ms, n = ctypes.c_double(), ctypes.c_int64()
         _lib.check(self.L.vihmc_timing_read(self._plan, ctypes.byref(ms), ctypes.byref(n)), "vihmc_timing_read")
