@@ -218,6 +218,7 @@ hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s) {
     dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk));
     if (nwaves == 12) hipLaunchKernelGGL(k_fwd_fused<12>, g, dim3(12 * 64), fwd_fused_lds_bytes(), s, a);
     else if (nwaves == 4) hipLaunchKernelGGL(k_fwd_fused<4>, g, dim3(4 * 64), fwd_fused_lds_bytes(), s, a);
+    else if (nwaves == 16) hipLaunchKernelGGL(k_fwd_fused<16>, g, dim3(16 * 64), fwd_fused_lds_bytes(), s, a);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

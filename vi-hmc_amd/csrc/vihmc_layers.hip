@@ -294,6 +294,88 @@ __global__ __launch_bounds__(256, 3) void k_rowdot2(RowdotArgs args) {
 constexpr int BWD_THREADS = 512;
 constexpr int BWD_SLOTS = 4;   // staged float4 per thread per sub-tile (2 x 32 rows x <= 32 float4)
 
+// dX of one 32-row sub-tile for one wave: 16 rows (half xh) x NUV column tiles of parity xpar
+// (NUV = the tiles that exist: with n_in = 100 -> 7 tiles, parity 0 has 4 and parity 1 has 3; the
+// 8th tile would be all padding)
+template <int NUV, int KF>
+__device__ __forceinline__ void bwd_dx_sub(const BwdProb& P, const float* dt, const float* wt, const float* ht,
+                                           int LDT, int LDW, int LDH, int NO4, int NI4, int xh, int xpar,
+                                           int lr, int lg, int sub, int r1, int c) {
+    const int n_out = KF > 0 ? KF : P.n_out;
+    const int kfull = n_out & ~15;
+    const float4* drow = reinterpret_cast<const float4*>(dt + (16 * xh + lr) * LDT);
+    const float* wrow[NUV];
+#pragma unroll
+    for (int u = 0; u < NUV; ++u) wrow[u] = wt + min(16 * (2 * u + xpar) + lr, P.n_in - 1) * LDW;
+    f32x4 acc_x[NUV];
+#pragma unroll
+    for (int u = 0; u < NUV; ++u) acc_x[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < kfull; kb += 16) {
+        const float4 dv = drow[(kb >> 2) + lg];
+        float4 wv[NUV];
+#pragma unroll
+        for (int u = 0; u < NUV; ++u) wv[u] = reinterpret_cast<const float4*>(wrow[u])[(kb >> 2) + lg];
+#pragma unroll
+        for (int u = 0; u < NUV; ++u) acc_x[u] = mfma(wv[u].x, dv.x, acc_x[u]);
+#pragma unroll
+        for (int u = 0; u < NUV; ++u) acc_x[u] = mfma(wv[u].y, dv.y, acc_x[u]);
+#pragma unroll
+        for (int u = 0; u < NUV; ++u) acc_x[u] = mfma(wv[u].z, dv.z, acc_x[u]);
+#pragma unroll
+        for (int u = 0; u < NUV; ++u) acc_x[u] = mfma(wv[u].w, dv.w, acc_x[u]);
+    }
+    for (int kb = kfull; kb < NO4; kb += 4) {
+        const float dv = dt[(16 * xh + lr) * LDT + kb + lg];
+#pragma unroll
+        for (int u = 0; u < NUV; ++u) acc_x[u] = mfma(wrow[u][kb + lg], dv, acc_x[u]);
+    }
+    const int m = sub + 16 * xh + lr;
+    if (m < r1) {
+        const float* hrow = ht + (16 * xh + lr) * LDH;
+        float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
+#pragma unroll
+        for (int u = 0; u < NUV; ++u) {
+            const int i = 16 * (2 * u + xpar) + 4 * lg;
+            if (i >= NI4) continue;
+            const float4 h = reinterpret_cast<const float4*>(hrow)[i >> 2];
+            float4 o;
+            o.x = (i + 0 < P.n_in) ? acc_x[u][0] * act_grad_from_out_l(P.act, h.x) : 0.f;
+            o.y = (i + 1 < P.n_in) ? acc_x[u][1] * act_grad_from_out_l(P.act, h.y) : 0.f;
+            o.z = (i + 2 < P.n_in) ? acc_x[u][2] * act_grad_from_out_l(P.act, h.z) : 0.f;
+            o.w = (i + 3 < P.n_in) ? acc_x[u][3] * act_grad_from_out_l(P.act, h.w) : 0.f;
+            reinterpret_cast<float4*>(orow)[i >> 2] = o;
+        }
+    }
+}
+
+// dW of one 32-row sub-tile for one wave: NS (1 or 2) 16-row output subtiles (rows ncol0/ncol1 of delta^T)
+template <int NS, int NTI>
+__device__ __forceinline__ void bwd_dw_sub(const float* dt, const float* ht, int LDT, int LDH, int ncol0, int ncol1,
+                                           int jlast, int lr, int lg, f32x4 (&acc_w)[2][NTI], float (&dsum)[2]) {
+    // step i covers rows base + 2*lg (base = 0,1,8,9,16,17,24,25): the two rows one b32 lane group
+    // {0-31} touches are 2 apart, i.e. 2*LD == 16 (mod 32) banks apart -> conflict free.
+#pragma unroll 2
+    for (int mi = 0; mi < BWD_SUB / 4; ++mi) {
+        const int mrow = (mi & 1) + 8 * (mi >> 1) + 2 * lg;
+        const float* drw = dt + mrow * LDT;
+        const float* hrw = ht + mrow * LDH + lr;
+        const float a0 = drw[ncol0];
+        const float a1 = NS > 1 ? drw[ncol1] : 0.f;
+        float hv[NTI];
+#pragma unroll
+        for (int t = 0; t < NTI - 1; ++t) hv[t] = hrw[16 * t];
+        hv[NTI - 1] = hrw[jlast];
+#pragma unroll
+        for (int t = 0; t < NTI; ++t) {
+            acc_w[0][t] = mfma(a0, hv[t], acc_w[0][t]);
+            if (NS > 1) acc_w[1][t] = mfma(a1, hv[t], acc_w[1][t]);
+        }
+        dsum[0] += a0;
+        if (NS > 1) dsum[1] += a1;
+    }
+}
+
 template <int NTI, int KF>
 __global__ __launch_bounds__(BWD_THREADS, 4) void k_bwd_ws(BwdArgs args) {
     constexpr int NU = (NTI + 1) / 2;          // dX column tiles per wave (parity split)
@@ -372,62 +454,26 @@ __global__ __launch_bounds__(BWD_THREADS, 4) void k_bwd_ws(BwdArgs args) {
     // The two roles run separate sub-tile loops with the same barrier sequence (s_barrier counts waves),
     // so each role's registers are allocated for its own loop only.
     if (xrole) {
+        // the parity is fixed per wave, so each parity gets its own loop (one dispatch, not one per sub-tile:
+        // a per-sub-tile choice kept both variants' loop invariants live and spilled)
         const int xh = rw & 1, xpar = rw >> 1;
-        const int kfull = n_out & ~15;
-        const float4* drow = reinterpret_cast<const float4*>(dt + (16 * xh + lr) * LDT);
-        const float* wrow[NU];
-#pragma unroll
-        for (int u = 0; u < NU; ++u) wrow[u] = wt + min(16 * (2 * u + xpar) + lr, P.n_in - 1) * LDW;
-        const float* hrow = ht + (16 * xh + lr) * LDH;
-        for (int sub = r0; sub < r1; sub += BWD_SUB) {
-            VIHMC_BWD_STORE(sub)
-            __syncthreads();
-            if (sub + BWD_SUB < r1) {
-                VIHMC_BWD_LOAD(sub + BWD_SUB)
-            }
-            if (P.has_dx) {
-                f32x4 acc_x[NU];
-#pragma unroll
-                for (int u = 0; u < NU; ++u) acc_x[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int kb = 0; kb < kfull; kb += 16) {
-                    const float4 dv = drow[(kb >> 2) + lg];
-                    float4 wv[NU];
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) wv[u] = reinterpret_cast<const float4*>(wrow[u])[(kb >> 2) + lg];
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].x, dv.x, acc_x[u]);
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].y, dv.y, acc_x[u]);
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].z, dv.z, acc_x[u]);
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wv[u].w, dv.w, acc_x[u]);
-                }
-                for (int kb = kfull; kb < NO4; kb += 4) {
-                    const float dv = dt[(16 * xh + lr) * LDT + kb + lg];
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) acc_x[u] = mfma(wrow[u][kb + lg], dv, acc_x[u]);
-                }
-                const int m = sub + 16 * xh + lr;
-                if (m < r1) {
-                    float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
-#pragma unroll
-                    for (int u = 0; u < NU; ++u) {
-                        const int i = 16 * (2 * u + xpar) + 4 * lg;
-                        if (2 * u + xpar >= NTI || i >= NI4) continue;
-                        const float4 h = reinterpret_cast<const float4*>(hrow)[i >> 2];
-                        float4 o;
-                        o.x = (i + 0 < P.n_in) ? acc_x[u][0] * act_grad_from_out_l(P.act, h.x) : 0.f;
-                        o.y = (i + 1 < P.n_in) ? acc_x[u][1] * act_grad_from_out_l(P.act, h.y) : 0.f;
-                        o.z = (i + 2 < P.n_in) ? acc_x[u][2] * act_grad_from_out_l(P.act, h.z) : 0.f;
-                        o.w = (i + 3 < P.n_in) ? acc_x[u][3] * act_grad_from_out_l(P.act, h.w) : 0.f;
-                        reinterpret_cast<float4*>(orow)[i >> 2] = o;
-                    }
-                }
-            }
-            __syncthreads();
+#define VIHMC_BWD_XLOOP(NUV)                                                                          \
+        for (int sub = r0; sub < r1; sub += BWD_SUB) {                                                \
+            VIHMC_BWD_STORE(sub)                                                                      \
+            __syncthreads();                                                                          \
+            if (sub + BWD_SUB < r1) {                                                                 \
+                VIHMC_BWD_LOAD(sub + BWD_SUB)                                                         \
+            }                                                                                         \
+            if (P.has_dx)                                                                             \
+                bwd_dx_sub<NUV, KF>(P, dt, wt, ht, LDT, LDW, LDH, NO4, NI4, xh, xpar, lr, lg, sub, r1, c); \
+            __syncthreads();                                                                          \
         }
+        if (xpar == 0 || (NTI & 1) == 0) {
+            VIHMC_BWD_XLOOP(NU)
+        } else {
+            VIHMC_BWD_XLOOP((NTI / 2 > 0 ? NTI / 2 : 1))
+        }
+#undef VIHMC_BWD_XLOOP
         return;
     }
 
@@ -449,31 +495,8 @@ __global__ __launch_bounds__(BWD_THREADS, 4) void k_bwd_ws(BwdArgs args) {
         if (sub + BWD_SUB < r1) {
             VIHMC_BWD_LOAD(sub + BWD_SUB)
         }
-        if (dw0) {
-            // step i covers rows base + 2*lg (base = 0,1,8,9,16,17,24,25): the two rows one b32 lane group
-            // {0-31} touches are 2 apart, i.e. 2*LD == 16 (mod 32) banks apart -> conflict free.
-            // 4 waves/SIMD (2 dX + 2 dW) hide the LDS latency of the 2 + NTI reads of a step.
-#pragma unroll 2
-            for (int mi = 0; mi < BWD_SUB / 4; ++mi) {
-                const int mrow = (mi & 1) + 8 * (mi >> 1) + 2 * lg;
-                const float* drw = dt + mrow * LDT;
-                const float* hrw = ht + mrow * LDH + lr;
-                const float a0 = drw[ncol0];
-                const float a1v = drw[ncol1];
-                const float a1 = dw1 ? a1v : 0.f;
-                float hv[NTI];
-#pragma unroll
-                for (int t = 0; t < NTI - 1; ++t) hv[t] = hrw[16 * t];
-                hv[NTI - 1] = hrw[jlast];
-#pragma unroll
-                for (int t = 0; t < NTI; ++t) {
-                    acc_w[0][t] = mfma(a0, hv[t], acc_w[0][t]);
-                    acc_w[1][t] = mfma(a1, hv[t], acc_w[1][t]);
-                }
-                dsum[0] += a0;
-                dsum[1] += a1;
-            }
-        }
+        if (dw1) bwd_dw_sub<2, NTI>(dt, ht, LDT, LDH, ncol0, ncol1, jlast, lr, lg, acc_w, dsum);
+        else if (dw0) bwd_dw_sub<1, NTI>(dt, ht, LDT, LDH, ncol0, ncol1, jlast, lr, lg, acc_w, dsum);
         __syncthreads();
     }
 #undef VIHMC_BWD_LOAD
@@ -484,6 +507,7 @@ __global__ __launch_bounds__(BWD_THREADS, 4) void k_bwd_ws(BwdArgs args) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
         const int ns = s2 == 0 ? ns0 : ns1;
+        if (s2 == 1 && !dw1) continue;
 #pragma unroll
         for (int t = 0; t < NTI; ++t) {
             const int j = 16 * t + lr;

@@ -469,7 +469,11 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s) {
     }
     // 12-wave workgroups (one per CU, 84 KB LDS) unless that grid would leave most of the 256 CUs idle
     const int64_t blocks12 = (int64_t)C * (cdiv(p->nets[0].rows, 192) + cdiv(p->nets[1].rows, 192));
-    const int nw = blocks12 >= 192 ? 12 : 4;
+    int nw = blocks12 >= 192 ? 12 : 4;
+    if (const char* e = std::getenv("VIHMC_FWD_WAVES")) {
+        const int v = std::atoi(e);
+        if (v == 4 || v == 12 || v == 16) nw = v;
+    }
     for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * nw);
     HIPCHK(launch_fwd_fused(a, nw, s));
     return 0;
