@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--ess-steps", type=int, default=100,
                     help="HMC iterations of a separately timed phase after the timed region whose samples give "
                          "ESS/s (Geyer initial monotone sequence; 0 = skip)")
-    ap.add_argument("--gather", action="store_true", help="RCCL all-gather of the sample pool after timing")
+    ap.add_argument("--no-gather", dest="gather", action="store_false",
+                    help="skip the RCCL all-gather of the sample pool after the timed region (N > 1)")
     return ap.parse_args()
 
 
