@@ -136,6 +136,12 @@ int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches);
  * variable turns it on for every plan. (New; no reference counterpart.) */
 int vihmc_graph_enable(vihmc_plan* p, int on);
 
+/* Plan options (new; no reference counterpart): "fwd_bf16x6" (default 1) computes the hidden 100->100
+ * layers of the forward with every fp32 product split exactly into three bf16 parts on the bf16 MFMA
+ * (six products, fp32 accumulation: fp32-level results, ~4 % faster evaluation); 0 = fp32 MFMA.
+ * "graph" = vihmc_graph_enable. Returns nonzero for an unknown key. */
+int vihmc_plan_option(vihmc_plan* p, const char* key, int value);
+
 void        vihmc_plan_destroy(vihmc_plan* p);
 const char* vihmc_last_error(void);
 const char* vihmc_version(void);

@@ -60,6 +60,27 @@ def test_deeponet_engine_matches_golden(name, cuda_device):
             check_logp(float(lpf[0]), float(c.g[f"logp{t}"]))
 
 
+@pytest.mark.parametrize("C,fwd_bf16x6", [(1, 1), (4, 1), (16, 1), (16, 0)])
+def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, cuda_device):
+    """Burgers shape at the chain counts that select different launch geometries (fused forward 4- vs
+    12-wave workgroups, fp32 or bf16x6 hidden-layer products, contraction q-splits, backward row chunks):
+    every chain (replicated golden thetas) must match the reference closure's golden."""
+    c = deeponet_case("deeponet_burgers")
+    eng = engine_for(c, max_chains=C)
+    eng.option("fwd_bf16x6", fwd_bf16x6)
+    n = len(c.thetas)
+    th = torch.tensor(np.stack([c.thetas[i % n] for i in range(C)]), device=cuda_device)
+    lp, g = eng.logp_grad(th)
+    lp, g = lp.cpu().numpy(), g.cpu().numpy()
+    sub = c.g["grad_subsample"]
+    for i in range(C):
+        t = i % n
+        check_logp(float(lp[i]), float(c.g[f"logp{t}"]))
+        gs = c.g[f"grad{t}_sub"]
+        np.testing.assert_allclose(g[i][sub], gs, rtol=2e-3, atol=2e-4 * np.abs(gs).max())
+        assert np.linalg.norm(g[i].astype(np.float64)) == pytest.approx(float(c.g[f"grad{t}_norm"]), rel=2e-4)
+
+
 @pytest.mark.parametrize("name", ["deeponet_small", "deeponet_odd_full"])
 def test_deeponet_engine_vs_fp64_oracle_many_chains(name, cuda_device):
     """C chains with independent thetas in one launch == each chain against the fp64 oracle."""
@@ -142,6 +163,13 @@ def test_deeponet_nonfinite_is_not_an_error(cuda_device):
     lp = lp.cpu().numpy()
     check_logp(float(lp[0]), float(c.g["logp0"]))
     assert not np.isfinite(lp[1])
+
+
+def test_plan_option_rejects_unknown_key(cuda_device):
+    c = deeponet_case("deeponet_small")
+    eng = engine_for(c, max_chains=1)
+    with pytest.raises(RuntimeError, match="unknown plan option"):
+        eng.option("no_such_option", 1)
 
 
 def test_engine_rejects_bad_shapes(cuda_device):

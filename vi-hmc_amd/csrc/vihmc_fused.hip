@@ -212,6 +212,236 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused(FusedArgs args) {
 #undef VIHMC_FW_STORE
 }
 
+// =============================================================================================
+// bf16x6 variant: the same register-resident layer walk with every product done on the bf16 MFMA.
+// Each fp32 operand is split exactly into three bf16 planes x = x0 + x1 + x2 and W.h keeps the six
+// terms of order <= 2 (w2h0, w1h1, w0h2, w1h0, w0h1, w0h0, smallest first), accumulated in fp32: as
+// accurate as an fp32 dot product (profiles/bf16x6_precision.py) at 6/16 of the fp32 MFMA cycles.
+//   k order: 16x16x32 k-block kb covers the column tiles t0 = 2kb, t1 = 2kb + 1; lane (l&15, g = l>>4)
+//   holds slots 8g..8g+7 = h[m][16 t0 + 4g + 0..3] and h[m][16 t1 + 4g + 0..3] -- exactly registers
+//   0..3 of accumulators t0 and t1 of the previous layer, so activations need no lane movement. The
+//   weights are stored in LDS in that permuted order (one b128 per plane per fragment). Tile 6 (columns
+//   96..111, 96..99 real) uses the 16x16x16 bf16 MFMA, whose k layout 4g + j is the accumulator's.
+// =============================================================================================
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BROW = 112;                         // bf16 per plane row (3 k-blocks x 32 + tile 6 x 16)
+constexpr int BPLANE = FW * BROW;                 // bf16 per plane
+constexpr int BBUF = 3 * BPLANE * 2 + 112 * 4;    // bytes per buffer: 3 planes + fp32 bias [112]
+
+__device__ __forceinline__ void split3(float x, __bf16& a, __bf16& b, __bf16& c) {
+    a = (__bf16)x;
+    const float r = x - (float)a;
+    b = (__bf16)r;
+    c = (__bf16)(r - (float)b);
+}
+
+__device__ __forceinline__ f32x4 mfma32(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(bf16x4 a, bf16x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c,
+                                                      0, 0, 0);
+}
+
+// one 16-row output tile t: acc += W[16t + lr][:] . h (six bf16 products per k-block)
+__device__ __forceinline__ f32x4 bf_tile(const __bf16* wb, int t, int lr, int lg, const bf16x8 (&hp)[3][3],
+                                         const bf16x4 (&h6)[3]) {
+    const int n = min(16 * t + lr, FW - 1);
+    const __bf16* row0 = wb + n * BROW;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 3; ++kb) {
+        const int o = kb * 32 + lg * 8;
+        const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(row0 + o);
+        const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(row0 + BPLANE + o);
+        const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(row0 + 2 * BPLANE + o);
+        acc = mfma32(w2, hp[0][kb], acc);
+        acc = mfma32(w1, hp[1][kb], acc);
+        acc = mfma32(w0, hp[2][kb], acc);
+        acc = mfma32(w1, hp[0][kb], acc);
+        acc = mfma32(w0, hp[1][kb], acc);
+        acc = mfma32(w0, hp[0][kb], acc);
+    }
+    // the K = 16 tail accumulates into its own registers: no accumulator chain crosses the two MFMA shapes.
+    // (Chaining a 16x16x32 result straight into a 16x16x16 MFMA's C operand gave wrong tiles with the
+    // ROCm 7.2 compiler -- which tile depended on the schedule; scripts/diag/fused_bf_vs_fp32.hip.)
+    f32x4 acc6 = {0.f, 0.f, 0.f, 0.f};
+    {
+        const int o = 96 + lg * 4;
+        const bf16x4 w0 = *reinterpret_cast<const bf16x4*>(row0 + o);
+        const bf16x4 w1 = *reinterpret_cast<const bf16x4*>(row0 + BPLANE + o);
+        const bf16x4 w2 = *reinterpret_cast<const bf16x4*>(row0 + 2 * BPLANE + o);
+        acc6 = mfma16(w2, h6[0], acc6);
+        acc6 = mfma16(w1, h6[1], acc6);
+        acc6 = mfma16(w0, h6[2], acc6);
+        acc6 = mfma16(w1, h6[0], acc6);
+        acc6 = mfma16(w0, h6[1], acc6);
+        acc6 = mfma16(w0, h6[0], acc6);
+    }
+    return acc + acc6;
+}
+
+template <int ACT>
+__device__ __forceinline__ float4 bf_epi(const float* bias, int t, int lg, const f32x4& acc,
+                                         __amdgpu_buffer_rsrc_t orsrc, uint32_t ooff) {
+    const int n = 16 * t + 4 * lg;
+    const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+    float4 h;
+    h.x = n + 0 < FW ? act_t<ACT>(acc[0] + bv.x) : 0.f;
+    h.y = n + 1 < FW ? act_t<ACT>(acc[1] + bv.y) : 0.f;
+    h.z = n + 2 < FW ? act_t<ACT>(acc[2] + bv.z) : 0.f;
+    h.w = n + 3 < FW ? act_t<ACT>(acc[3] + bv.w) : 0.f;
+    const uint32_t off = (t < 6 || lg == 0) ? ooff + 4u * n : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), orsrc, off, 0, 0);
+    return h;
+}
+
+template <int ACT>
+__device__ __forceinline__ void bf_layer(const __bf16* wb, const float* bias, const bf16x8 (&hp)[3][3],
+                                         const bf16x4 (&h6)[3], int lr, int lg, __amdgpu_buffer_rsrc_t orsrc,
+                                         uint32_t ooff, float4 (&hn)[7]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const f32x4 a0 = bf_tile(wb, 2 * p, lr, lg, hp, h6);
+        const f32x4 a1 = bf_tile(wb, 2 * p + 1, lr, lg, hp, h6);
+        hn[2 * p] = bf_epi<ACT>(bias, 2 * p, lg, a0, orsrc, ooff);
+        hn[2 * p + 1] = bf_epi<ACT>(bias, 2 * p + 1, lg, a1, orsrc, ooff);
+    }
+    const f32x4 a6 = bf_tile(wb, 6, lr, lg, hp, h6);
+    hn[6] = bf_epi<ACT>(bias, 6, lg, a6, orsrc, ooff);
+}
+
+// fp32 h tiles (this lane: 4 columns 16t + 4lg of its row) -> the three bf16 B-operand planes
+__device__ __forceinline__ void bf_split_operand(const float4 (&h)[7], bf16x8 (&hp)[3][3], bf16x4 (&h6)[3]) {
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        const float v[4] = {h[t].x, h[t].y, h[t].z, h[t].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            __bf16 a, b, c;
+            split3(v[j], a, b, c);
+            if (t < 6) {
+                hp[0][t >> 1][(t & 1) * 4 + j] = a;
+                hp[1][t >> 1][(t & 1) * 4 + j] = b;
+                hp[2][t >> 1][(t & 1) * 4 + j] = c;
+            } else {
+                h6[0][j] = a;
+                h6[1][j] = b;
+                h6[2][j] = c;
+            }
+        }
+    }
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
+    constexpr int FTHREADS = NW * 64;
+    constexpr int FSLOTS = (FBLK4 + FTHREADS - 1) / FTHREADS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char fsmb[];      // 2 x BBUF
+    const int C = args.C;
+    const int c = blockIdx.x % C;
+    int item = blockIdx.x / C;
+    const int net = item < args.net[0].nblk ? 0 : 1;
+    if (net) item -= args.net[0].nblk;
+    const FusedNet& N = args.net[net];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int row = item * (16 * NW) + wave * 16 + lr;
+    const int rowc = min(row, N.rows - 1);
+    const bool rok = row < N.rows;
+    const float* Wc = args.packed + c * args.dp;
+
+    // zero the never-written tail columns 100..111 of every plane row and the bias pad, both buffers
+    for (int i = tid; i < 2 * 3 * FW; i += FTHREADS) {
+        __bf16* r = reinterpret_cast<__bf16*>(fsmb + (i / (3 * FW)) * BBUF) + (i % (3 * FW)) * BROW + 100;
+#pragma unroll
+        for (int z = 0; z < 12; ++z) r[z] = (__bf16)0.f;
+    }
+    if (tid < 24) reinterpret_cast<float*>(fsmb + (tid / 12) * BBUF + 3 * BPLANE * 2)[100 + tid % 12] = 0.f;
+
+    // staging slot v: float4 i of [W | bias] -> (plane row position) or bias position
+    int sdst[FSLOTS];
+#pragma unroll
+    for (int v = 0; v < FSLOTS; ++v) {
+        const int i = tid + FTHREADS * v;
+        if (i < FW * FW / 4) {
+            const int n = i / (FW / 4), c4 = i % (FW / 4), tq = c4 >> 2, g = c4 & 3;
+            const int pos = tq < 6 ? (tq >> 1) * 32 + g * 8 + (tq & 1) * 4 : 96 + g * 4;
+            sdst[v] = n * BROW + pos;                     // bf16 index within a plane
+        } else {
+            sdst[v] = i < FBLK4 ? -1 - 4 * (i - FW * FW / 4) : INT32_MIN;   // bias float index, encoded
+        }
+    }
+    f32x4 pf[FSLOTS];
+#define VIHMC_FB_LOAD(J)                                                                              \
+    {                                                                                                 \
+        const f32x4* src = reinterpret_cast<const f32x4*>(Wc + N.w_off[J]);                           \
+        _Pragma("unroll") for (int v = 0; v < FSLOTS; ++v)                                            \
+            pf[v] = src[min(tid + FTHREADS * v, FBLK4 - 1)];                                          \
+    }
+#define VIHMC_FB_STORE(BUF)                                                                           \
+    _Pragma("unroll") for (int v = 0; v < FSLOTS; ++v) {                                              \
+        unsigned char* bb = fsmb + (BUF) * BBUF;                                                      \
+        if (sdst[v] >= 0) {                                                                           \
+            bf16x4 a, b, cc;                                                                          \
+            _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                           \
+                __bf16 x0, x1, x2;                                                                    \
+                split3(pf[v][j], x0, x1, x2);                                                         \
+                a[j] = x0; b[j] = x1; cc[j] = x2;                                                     \
+            }                                                                                         \
+            __bf16* pl = reinterpret_cast<__bf16*>(bb) + sdst[v];                                     \
+            *reinterpret_cast<bf16x4*>(pl) = a;                                                       \
+            *reinterpret_cast<bf16x4*>(pl + BPLANE) = b;                                              \
+            *reinterpret_cast<bf16x4*>(pl + 2 * BPLANE) = cc;                                         \
+        } else if (sdst[v] != INT32_MIN) {                                                            \
+            *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(bb + 3 * BPLANE * 2) + (-1 - sdst[v])) = pf[v]; \
+        }                                                                                             \
+    }
+
+    VIHMC_FB_LOAD(0)
+    float4 h[7];
+    {
+        const float* ar = N.in + c * N.in_cs + (int64_t)rowc * N.ldin;
+#pragma unroll
+        for (int t = 0; t < 6; ++t) h[t] = *reinterpret_cast<const float4*>(ar + 16 * t + 4 * lg);
+        h[6] = lg == 0 ? *reinterpret_cast<const float4*>(ar + 96) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();                            // zero fill done before the staging writes
+    VIHMC_FB_STORE(0)
+    __builtin_amdgcn_s_waitcnt(0x0F70);         // see k_fwd_fused: no vmcnt waits inside the layer loop
+    const float* outc = N.out + c * N.out_cs;
+    const uint32_t ooff = rok ? (uint32_t)row * (uint32_t)N.ldo * 4u : OOB;
+    const uint32_t obytes = (uint32_t)N.rows * (uint32_t)N.ldo * 4u;
+    for (int j = 0; j < N.nl; ++j) {
+        __syncthreads();
+        VIHMC_FB_LOAD(min(j + 1, N.nl - 1))
+        const unsigned char* bbuf = fsmb + (j & 1) * BBUF;
+        const __bf16* wb = reinterpret_cast<const __bf16*>(bbuf);
+        const float* bias = reinterpret_cast<const float*>(bbuf + 3 * BPLANE * 2);
+        const __amdgpu_buffer_rsrc_t orsrc = make_rsrc(outc + N.h_off[j], obytes);
+        bf16x8 hp[3][3];
+        bf16x4 h6[3];
+        bf_split_operand(h, hp, h6);
+        const int act = N.act[j];
+        if (act == ACT_TANH) bf_layer<ACT_TANH>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
+        else if (act == ACT_RELU) bf_layer<ACT_RELU>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
+        else bf_layer<ACT_ID>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
+        VIHMC_FB_STORE((j + 1) & 1)
+    }
+#undef VIHMC_FB_LOAD
+#undef VIHMC_FB_STORE
+}
+
+size_t fwd_fused_bf_lds_bytes() { return 2 * (size_t)BBUF; }
+
+hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s) {
+    dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk));
+    hipLaunchKernelGGL(k_fwd_fused_bf<12>, g, dim3(12 * 64), fwd_fused_bf_lds_bytes(), s, a);
+    return hipGetLastError();
+}
+
 size_t fwd_fused_lds_bytes() { return sizeof(float) * 2 * FBUF; }
 
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s) {

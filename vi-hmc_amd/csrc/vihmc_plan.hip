@@ -122,6 +122,12 @@ struct vihmc_plan {
     hipStream_t cap_stream = nullptr;
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
     int graph_on = -1;          // -1: follow VIHMC_GRAPH
+    // hidden-layer forward products as exact 3-way bf16 splits (6 bf16 MFMA products, fp32 accumulate;
+    // fp32-level accuracy, vihmc_fused.hip); VIHMC_FWD_BF16=0 or vihmc_plan_option turns it off
+    int fwd_bf16x6 = [] {
+        const char* e = std::getenv("VIHMC_FWD_BF16");
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+    }();
 
     template <typename T>
     int alloc(T** p, int64_t n) {
@@ -473,6 +479,11 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s) {
     if (const char* e = std::getenv("VIHMC_FWD_WAVES")) {
         const int v = std::atoi(e);
         if (v == 4 || v == 12 || v == 16) nw = v;
+    }
+    if (p->fwd_bf16x6 && nw == 12) {
+        for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * 12);
+        HIPCHK(launch_fwd_fused_bf(a, s));
+        return 0;
     }
     for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * nw);
     HIPCHK(launch_fwd_fused(a, nw, s));
@@ -904,6 +915,15 @@ int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches) {
     *total_ms = t;
     *launches = (int64_t)(p->ev_used / 2);
     p->ev_used = 0;
+    return 0;
+}
+
+int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
+    if (!p || !key) return fail("null argument");
+    const std::string k(key);
+    if (k == "fwd_bf16x6") p->fwd_bf16x6 = value ? 1 : 0;
+    else if (k == "graph") p->graph_on = value ? 1 : 0;
+    else return fail("unknown plan option '" + k + "' (fwd_bf16x6, graph)");
     return 0;
 }
 

@@ -124,6 +124,11 @@ class _Engine:
         """hipGraph replay of the gradient evaluation (vihmc_graph_enable)."""
         _lib.check(self.L.vihmc_graph_enable(self._plan, int(on)), "vihmc_graph_enable")
 
+    def option(self, key: str, value: int):
+        """vihmc_plan_option: "fwd_bf16x6" (hidden-layer forward on the bf16 MFMA with exact 3-way splits),
+        "graph"."""
+        _lib.check(self.L.vihmc_plan_option(self._plan, key.encode(), int(value)), f"vihmc_plan_option({key})")
+
     def timing_read(self):
         ms, n = ctypes.c_double(), ctypes.c_int64()
         _lib.check(self.L.vihmc_timing_read(self._plan, ctypes.byref(ms), ctypes.byref(n)), "vihmc_timing_read")
