@@ -139,7 +139,9 @@ int vihmc_graph_enable(vihmc_plan* p, int on);
 /* Plan options (new; no reference counterpart): "fwd_bf16x6" (default 1) computes the hidden 100->100
  * layers of the forward with every fp32 product split exactly into three bf16 parts on the bf16 MFMA
  * (six products, fp32 accumulation: fp32-level results, ~4 % faster evaluation); 0 = fp32 MFMA.
- * "graph" = vihmc_graph_enable. Returns nonzero for an unknown key. */
+ * "contract_bf16x6" (default 1): the same for the side-A contraction (branch x trunk S, likelihood,
+ * G, dZ_trunk; width 100). "graph" = vihmc_graph_enable. Changing an option drops captured graphs.
+ * Returns nonzero for an unknown key. */
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value);
 
 void        vihmc_plan_destroy(vihmc_plan* p);

@@ -60,14 +60,16 @@ def test_deeponet_engine_matches_golden(name, cuda_device):
             check_logp(float(lpf[0]), float(c.g[f"logp{t}"]))
 
 
-@pytest.mark.parametrize("C,fwd_bf16x6", [(1, 1), (4, 1), (16, 1), (16, 0)])
-def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, cuda_device):
+@pytest.mark.parametrize("C,fwd_bf16x6,contract_bf16x6", [(1, 1, 1), (4, 1, 1), (16, 1, 1), (16, 0, 0), (16, 1, 0),
+                                                         (3, 0, 1)])
+def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, contract_bf16x6, cuda_device):
     """Burgers shape at the chain counts that select different launch geometries (fused forward 4- vs
     12-wave workgroups, fp32 or bf16x6 hidden-layer products, contraction q-splits, backward row chunks):
     every chain (replicated golden thetas) must match the reference closure's golden."""
     c = deeponet_case("deeponet_burgers")
     eng = engine_for(c, max_chains=C)
     eng.option("fwd_bf16x6", fwd_bf16x6)
+    eng.option("contract_bf16x6", contract_bf16x6)
     n = len(c.thetas)
     th = torch.tensor(np.stack([c.thetas[i % n] for i in range(C)]), device=cuda_device)
     lp, g = eng.logp_grad(th)
@@ -79,6 +81,31 @@ def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, cuda_device):
         gs = c.g[f"grad{t}_sub"]
         np.testing.assert_allclose(g[i][sub], gs, rtol=2e-3, atol=2e-4 * np.abs(gs).max())
         assert np.linalg.norm(g[i].astype(np.float64)) == pytest.approx(float(c.g[f"grad{t}_norm"]), rel=2e-4)
+
+
+def test_bf16x6_paths_match_fp32_mfma_paths(cuda_device):
+    """Burgers shape, 16 perturbed chains: the bf16x6 forward + side-A contraction (exact 3-way bf16 split,
+    six products, fp32 accumulation) against the fp32-MFMA kernels on the same inputs. Both are fp32-level
+    computations, so they agree far inside the golden tolerance: logp to 2e-6 relative, the gradient to
+    2e-5 of its norm (measured r01: see the printed values)."""
+    c = deeponet_case("deeponet_burgers")
+    rng = np.random.default_rng(5)
+    C = 16
+    base = c.thetas[0]
+    th = torch.tensor(np.stack([base + 0.01 * rng.standard_normal(base.size).astype(np.float32) for _ in range(C)]),
+                      device=cuda_device)
+    eng = engine_for(c, max_chains=C)
+    res = {}
+    for on in (0, 1):
+        eng.option("fwd_bf16x6", on)
+        eng.option("contract_bf16x6", on)
+        lp, g = eng.logp_grad(th)
+        res[on] = (lp.double().cpu().numpy(), g.double().cpu().numpy())
+    dlp = np.abs(res[1][0] - res[0][0]) / np.abs(res[0][0])
+    dg = np.linalg.norm(res[1][1] - res[0][1], axis=1) / np.linalg.norm(res[0][1], axis=1)
+    print(f"bf16x6 vs fp32 MFMA: logp rel max {dlp.max():.2e}, grad rel-norm max {dg.max():.2e}")
+    assert dlp.max() < 2e-6
+    assert dg.max() < 2e-5
 
 
 @pytest.mark.parametrize("name", ["deeponet_small", "deeponet_odd_full"])

@@ -1,0 +1,375 @@
+// Side-A contraction (branch x trunk S, Gaussian NLL, G, dZ_trunk) with fp32 products emulated on the
+// bf16 MFMA: the "bf16x6" form of k_contract_ws (vihmc_contract.hip), same ContractProb, same outputs.
+//
+// Replaces torch.einsum("...i,...i->...", xb, xtr) + b (Operator_network/VI_HMC/my_make_func.py:79-82),
+// GaussianNLLLoss / regression ll (main_VI_HMC_burgers.py:157-163) and their autograd backward.
+//
+// Every fp32 operand x is split exactly into three bf16 planes x = x0 + x1 + x2 (x0 = bf16(x),
+// x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)); a.b keeps the six products of order <= 2
+// (a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0, small first) accumulated in fp32: the dropped terms are
+// < 2^-24 |a||b|, so the result is as accurate as the sequential fp32 dot product
+// (profiles/bf16x6_precision.py). Six 16x16x32 bf16 MFMAs (16 cycles each) replace eight 16x16x4 f32
+// MFMAs (32 cycles each) per 32-long k-block: 2.7x fewer matrix-core cycles. The 4-long k tail
+// (features 96..99) is one exact 16x16x4 f32 MFMA.
+//
+// Workgroup = 4 S waves + 4 D waves (one of each per SIMD, 1 workgroup per CU, 256 VGPRs a wave) for
+// 128 owner (trunk) rows; the branch rows stream through LDS in 32-row chunks:
+//   Q image  (3 rotating buffers): the chunk's three bf16 planes, row-major [32 q][112 j], 224-B rows,
+//            plus the fp32 tail [32 q][4]. S waves read it by rows (ds_read_b128, the A operand of
+//            S = Q Own^T); D waves read it by columns (ds_read_b64_tr_b16, the B operand of G^T Q).
+//            224 B = 32 * 7 (odd multiple of 32 B): the transposed reads of 8 consecutive rows are
+//            bank-conflict free.
+//   G image  (2 buffers): each S wave's G (fp32, its accumulator registers) for its D partner, lane-
+//            linear. The D role's k order is chosen so that its A operand IS that register layout:
+//            lane (lr, lg) element jj <-> branch row 4lg + jj (jj < 4) or 16 + 4lg + jj - 4 (jj >= 4),
+//            and the two transposed reads fetch exactly those rows.
+//   S wave w: 32 owner rows, their three planes in registers (72 VGPRs) as the B operand; per chunk two
+//             16-row S tiles, G = gscale (S + b0 - y), likelihood sums, G^T stores for side B.
+//   D wave w: one chunk behind: splits G, dOwn[32 rows][112] += G^T Q over the chunk's 32 rows.
+#include "vihmc_internal.h"
+
+#ifndef CB_DRAIN
+#define CB_DRAIN 0
+#endif
+#ifndef CB_YBUF
+#define CB_YBUF 1
+#endif
+#ifndef CB_GBUF
+#define CB_GBUF 1
+#endif
+
+namespace vihmc {
+
+namespace {
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+constexpr int CB_QC = 32;                          // branch rows per chunk
+constexpr int CB_PITCH = 224;                      // bytes per bf16 image row (112 features)
+constexpr int CB_PLANE = CB_QC * CB_PITCH;         // 7168
+constexpr int CB_TAIL = 3 * CB_PLANE;              // fp32 [32][4] tail image offset
+constexpr int CB_QIMG = CB_TAIL + CB_QC * 16;      // 22016 bytes per Q buffer
+constexpr int CB_GIMG = 4 * 4 * 64 * 16;           // 4 S waves x 4 f32x4 x 64 lanes = 16384
+constexpr int CB_LDS = 3 * CB_QIMG + 2 * CB_GIMG;  // 98816
+constexpr int CB_SLOTS = CB_QC * 25;               // f32x4 per chunk (25 per 100-wide row)
+
+typedef unsigned int u32x4_c __attribute__((ext_vector_type(4)));
+constexpr uint32_t OOB_C = 0x80000000u;
+
+// buffer resource over [p, p + bytes) from wave-uniform inputs (out-of-range loads read 0, stores drop)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_c(const void* p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ f32x4 mfma_bf(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// exact three-way split of 4 values into bf16 planes
+__device__ __forceinline__ void split4(f32x4 x, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const __bf16 a = (__bf16)x[j];
+        const float r = x[j] - (float)a;
+        const __bf16 b = (__bf16)r;
+        p0[j] = a;
+        p1[j] = b;
+        p2[j] = (__bf16)(r - (float)b);
+    }
+}
+
+__device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// acc += a.b over one 32-long k-block, six products, small terms first
+__device__ __forceinline__ f32x4 six(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 acc) {
+    acc = mfma_bf(a[2], b[0], acc);
+    acc = mfma_bf(a[1], b[1], acc);
+    acc = mfma_bf(a[0], b[2], acc);
+    acc = mfma_bf(a[1], b[0], acc);
+    acc = mfma_bf(a[0], b[1], acc);
+    acc = mfma_bf(a[0], b[0], acc);
+    return acc;
+}
+}  // namespace
+
+__global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smc[];
+    int b = blockIdx.x;
+    const int per_chain = P.o_tiles * P.q_chunks;
+    const int c = b / per_chain;
+    b -= c * per_chain;
+    const int qc = b / P.o_tiles;
+    const int og = b - qc * P.o_tiles;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int w = wave & 3;
+    const float* Q = P.Q + c * P.q_cs;
+    const int o0 = og * CONTRACT_OWN_PER_WG + w * 32;
+    const int q_lo = qc * P.q_per_chunk;
+    const int q_hi = min(q_lo + P.q_per_chunk, P.Mq);
+    const int nchunks = q_hi > q_lo ? (q_hi - q_lo + CB_QC - 1) / CB_QC : 0;
+
+    // chunk staging: 800 f32x4 (32 rows x 25), slots tid and tid + 512; the second slot of threads
+    // >= 288 duplicates a valid one and is not stored
+    const int v0 = tid, v1 = min(tid + 512, CB_SLOTS - 1);
+    const bool st1 = tid + 512 < CB_SLOTS;
+    const int r0s = v0 / 25, c0s = v0 - r0s * 25, r1s = v1 / 25, c1s = v1 - r1s * 25;
+    f32x4 stg0, stg1;
+#define VIHMC_CB_LOAD(CI)                                                                                   \
+    stg0 = reinterpret_cast<const f32x4*>(Q + (int64_t)min(q_lo + (CI) * CB_QC + r0s, P.Mq - 1) * P.ldq)[c0s]; \
+    stg1 = reinterpret_cast<const f32x4*>(Q + (int64_t)min(q_lo + (CI) * CB_QC + r1s, P.Mq - 1) * P.ldq)[c1s];
+#define VIHMC_CB_STORE1(BUF, X, R, CC)                                                                      \
+    {                                                                                                       \
+        unsigned char* img = smc + (BUF) * CB_QIMG;                                                         \
+        bf16x4 p0, p1, p2;                                                                                  \
+        split4(X, p0, p1, p2);                                                                              \
+        unsigned char* d = img + (R) * CB_PITCH + (CC) * 8;                                                 \
+        *reinterpret_cast<bf16x4*>(d) = p0;                                                                 \
+        *reinterpret_cast<bf16x4*>(d + CB_PLANE) = p1;                                                      \
+        *reinterpret_cast<bf16x4*>(d + 2 * CB_PLANE) = p2;                                                  \
+        if ((CC) == 24) *reinterpret_cast<f32x4*>(img + CB_TAIL + (R) * 16) = X;                            \
+    }
+#define VIHMC_CB_STORE(BUF)                           \
+    VIHMC_CB_STORE1(BUF, stg0, r0s, c0s)              \
+    if (st1) VIHMC_CB_STORE1(BUF, stg1, r1s, c1s)
+
+    if (nchunks > 0) {
+        VIHMC_CB_LOAD(0)
+        VIHMC_CB_STORE(0)
+        VIHMC_CB_LOAD(min(1, nchunks - 1))
+    }
+
+    if (wave < 4) {
+        // ---------------- S role ----------------
+        const float* Own = P.Own + c * P.own_cs;
+        const float* Yc = P.Y + c * P.y_cs;
+        const float b0 = P.b0[c * P.b0_cs];
+        bf16x8 ob[2][3][3];     // [s][kb][plane]: Own[o0 + 16s + lr][32kb + 8lg + j]
+        float otl[2];           // Own[o0 + 16s + lr][96 + lg]
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const float* orow = Own + (int64_t)min(o0 + 16 * s + lr, P.Mo - 1) * P.ldown;
+#pragma unroll
+            for (int kb = 0; kb < 3; ++kb) {
+                const f32x4 x0 = *reinterpret_cast<const f32x4*>(orow + 32 * kb + 8 * lg);
+                const f32x4 x1 = *reinterpret_cast<const f32x4*>(orow + 32 * kb + 8 * lg + 4);
+                bf16x4 a0, a1, a2, c0, c1, c2;
+                split4(x0, a0, a1, a2);
+                split4(x1, c0, c1, c2);
+                ob[s][kb][0] = cat8(a0, c0);
+                ob[s][kb][1] = cat8(a1, c1);
+                ob[s][kb][2] = cat8(a2, c2);
+            }
+            otl[s] = orow[96 + lg];
+        }
+        double ssq = 0.0, gsum = 0.0;
+        // targets and G^T through buffer resources: 32-bit offsets, rows past the end read 0 and owner
+        // rows past Mo are dropped by the hardware range check (no exec-mask branches per element)
+        const __amdgpu_buffer_rsrc_t yrs = make_rsrc_c(Yc, (uint32_t)((int64_t)P.Mq * P.ldy * 4));
+        const __amdgpu_buffer_rsrc_t grs =
+            make_rsrc_c(P.gout ? P.gout + c * P.gout_cs : P.Y, P.gout ? (uint32_t)((int64_t)P.Mo * P.ldg * 4) : 0u);
+        bool ovalid[2];
+        uint32_t yoff[2], goff[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int oo = o0 + 16 * s + lr;
+            ovalid[s] = oo < P.Mo;
+            yoff[s] = (uint32_t)((4 * lg) * P.ldy + min(oo, P.Mo - 1)) * 4u;
+            goff[s] = ovalid[s] ? (uint32_t)(oo * P.ldg + q_lo + 4 * lg) * 4u : OOB_C;
+        }
+        const uint32_t ystep = (uint32_t)P.ldy * 4u;
+        float yn[2][2][4];      // [sub][s][r], one chunk ahead
+#define VIHMC_CB_YLOAD(CI)                                                                               \
+        _Pragma("unroll") for (int sub = 0; sub < 2; ++sub)                                              \
+            _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                \
+                _Pragma("unroll") for (int r = 0; r < 4; ++r)                                            \
+                    yn[sub][s][r] = CB_YBUF ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32( \
+                        yrs, yoff[s], (uint32_t)(q_lo + (CI) * CB_QC + 16 * sub + r) * ystep, 0))             \
+                        : Yc[(int64_t)min(q_lo + (CI) * CB_QC + 16 * sub + 4 * lg + r, P.Mq - 1) * P.ldy +    \
+                             min(o0 + 16 * s + lr, P.Mo - 1)];
+        VIHMC_CB_YLOAD(0)
+        for (int i = 0; i <= nchunks; ++i) {
+            __syncthreads();
+            if (i < nchunks) {
+                const int q0 = q_lo + i * CB_QC;
+                const bool full = q0 + CB_QC <= q_hi;
+                const unsigned char* img = smc + (i % 3) * CB_QIMG;
+                float yv[2][2][4];
+#pragma unroll
+                for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) yv[sub][s][r] = yn[sub][s][r];
+                VIHMC_CB_YLOAD(min(i + 1, nchunks - 1))
+                if (CB_DRAIN) __builtin_amdgcn_s_waitcnt(0x0F70);
+                f32x4* gdst = reinterpret_cast<f32x4*>(smc + 3 * CB_QIMG + (i & 1) * CB_GIMG) + w * 256;
+                float ps = 0.f;
+#pragma unroll
+                for (int sub = 0; sub < 2; ++sub) {
+                    const unsigned char* row = img + (16 * sub + lr) * CB_PITCH + 16 * lg;
+                    f32x4 sacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+                    for (int kb = 0; kb < 3; ++kb) {
+                        bf16x8 qa[3];
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            qa[p] = *reinterpret_cast<const bf16x8*>(row + p * CB_PLANE + 64 * kb);
+                        sacc[0] = six(qa, ob[0][kb], sacc[0]);
+                        sacc[1] = six(qa, ob[1][kb], sacc[1]);
+                    }
+                    const float qt = reinterpret_cast<const float*>(img + CB_TAIL)[(16 * sub + lr) * 4 + lg];
+                    f32x4 tacc[2];
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+                        tacc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(qt, otl[s], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                    f32x4 g[2];
+#pragma unroll
+                    for (int s = 0; s < 2; ++s)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int qq = q0 + 16 * sub + 4 * lg + r;
+                            const bool ok = ovalid[s] && (full || qq < q_hi);
+                            float rv = (sacc[s][r] + tacc[s][r]) + b0 - yv[sub][s][r];
+                            rv = ok ? rv : 0.f;
+                            g[s][r] = P.gscale * rv;
+                            ps = fmaf(rv, rv, ps);
+                            gsum += (double)g[s][r];  // G terms cancel: exact-order fp64, not fp32 partials
+                        }
+                    gdst[(2 * sub + 0) * 64 + lane] = g[0];
+                    gdst[(2 * sub + 1) * 64 + lane] = g[1];
+                    if (P.gout && !CB_GBUF) {
+                        float* gw = P.gout + c * P.gout_cs;
+                        const int qq = q0 + 16 * sub + 4 * lg;
+#pragma unroll
+                        for (int s = 0; s < 2; ++s) {
+                            const int oo = o0 + 16 * s + lr;
+                            if (oo >= P.Mo) continue;
+                            float* dst = gw + (int64_t)oo * P.ldg + qq;
+                            if (qq + 3 < q_hi) {
+                                *reinterpret_cast<f32x4*>(dst) = g[s];
+                            } else {
+#pragma unroll
+                                for (int r = 0; r < 4; ++r)
+                                    if (qq + r < q_hi) dst[r] = g[s][r];
+                            }
+                        }
+                    }
+                    if (P.gout && CB_GBUF) {
+                        const uint32_t qofs = (uint32_t)(q0 - q_lo + 16 * sub) * 4u;
+                        if (full) {
+#pragma unroll
+                            for (int s = 0; s < 2; ++s)
+                                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, g[s]), grs,
+                                                                       goff[s] + qofs, 0, 0);
+                        } else {
+                            const int qq = q0 + 16 * sub + 4 * lg;
+#pragma unroll
+                            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    // copy the element out first: __builtin_bit_cast of an ext-vector
+                                    // element subscript compiled to element 0 for every r (hipcc, ROCm 7.2)
+                                    const float gv = g[s][r];
+                                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs,
+                                        qq + r < q_hi ? goff[s] + qofs + 4u * r : OOB_C, 0, 0);
+                                }
+                        }
+                    }
+                }
+                // sum r^2 (no cancellation): per-chunk fp32 partial of 16 terms per lane, then fp64
+                ssq += (double)ps;
+            }
+            VIHMC_CB_STORE((i + 1) % 3)
+            VIHMC_CB_LOAD(max(min(i + 2, nchunks - 1), 0))
+        }
+        if (P.with_stats) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                ssq += __shfl_xor(ssq, o, 64);
+                gsum += __shfl_xor(gsum, o, 64);
+            }
+            if (lane == 0) {
+                double* st = P.stats + c * P.stats_cs + 2 * (int64_t)((qc * P.o_tiles + og) * 4 + w);
+                st[0] = ssq;
+                st[1] = gsum;
+            }
+        }
+        return;
+    }
+
+    // ---------------- D role ----------------
+    f32x4 dacc[2][7];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) dacc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // transposed-read lane address: group lg reads rows 4lg .. 4lg+3 (and 16 + those), lane 4qq+pp
+    // supplies row 4lg + qq, features 16t + 4pp .. +3
+    const int tr_off = (4 * lg + (lr >> 2)) * CB_PITCH + 8 * (lr & 3);
+    for (int i = 0; i <= nchunks; ++i) {
+        __syncthreads();
+        if (i >= 1) {
+            const unsigned char* img = smc + ((i - 1) % 3) * CB_QIMG;
+            const f32x4* gsrc = reinterpret_cast<const f32x4*>(smc + 3 * CB_QIMG + ((i - 1) & 1) * CB_GIMG) + w * 256;
+            bf16x8 ga[2][3];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                bf16x4 l0, l1, l2, h0, h1, h2;
+                split4(gsrc[s * 64 + lane], l0, l1, l2);          // sub 0
+                split4(gsrc[(2 + s) * 64 + lane], h0, h1, h2);    // sub 1
+                ga[s][0] = cat8(l0, h0);
+                ga[s][1] = cat8(l1, h1);
+                ga[s][2] = cat8(l2, h2);
+            }
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                bf16x8 qb[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    const unsigned char* a = img + p * CB_PLANE + tr_off + 32 * t;
+                    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));
+                    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 16 * CB_PITCH));
+                    qb[p] = cat8(lo, hi);
+                }
+                dacc[0][t] = six(ga[0], qb, dacc[0][t]);
+                dacc[1][t] = six(ga[1], qb, dacc[1][t]);
+            }
+        }
+        VIHMC_CB_STORE((i + 1) % 3)
+        VIHMC_CB_LOAD(max(min(i + 2, nchunks - 1), 0))
+    }
+    float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int j = 16 * t + lr;
+            if (j >= P.ldout) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int oo = o0 + 16 * s + 4 * lg + r;
+                if (oo < P.Mo) out[(int64_t)oo * P.ldout + j] = (j < 100) ? dacc[s][t][r] : 0.f;
+            }
+        }
+#undef VIHMC_CB_LOAD
+#undef VIHMC_CB_STORE1
+#undef VIHMC_CB_STORE
+#undef VIHMC_CB_YLOAD
+}
+
+hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s) {
+    if (p.W != 100 || p.load_g) return hipErrorInvalidValue;
+    dim3 g(C * p.o_tiles * p.q_chunks), blk(512);
+    hipLaunchKernelGGL(k_contract_bf, g, blk, CB_LDS, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace vihmc

@@ -96,12 +96,15 @@ struct ContractProb {
     int32_t load_g;                       // side B: Y holds G (already scaled); no S recompute
     int32_t xcd_group;                    // 1: the o_tiles workgroups sharing one Q chunk run on one XCD
                                           //    (requires C * q_chunks % 8 == 0; speed only)
+    int32_t bf16x6;                       // side A, W = 100: products on the bf16 MFMA, 3-way split
+                                          //    operands, six products (k_contract_bf)
     float gscale;
 };
 
 // launchers (vihmc_kernels.hip)
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s);
 hipError_t launch_contract(const ContractProb& p, int C, bool with_grad, hipStream_t s);
+hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s);
 size_t contract_lds_bytes(int W);
 hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* frozen, const int32_t* map_w,
                               const int32_t* map_wt, int64_t D, hipStream_t s);

@@ -128,6 +128,11 @@ struct vihmc_plan {
         const char* e = std::getenv("VIHMC_FWD_BF16");
         return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
     }();
+    // side-A contraction in the same bf16x6 form (k_contract_bf); VIHMC_CONTRACT_BF16=0 turns it off
+    int contract_bf16x6 = [] {
+        const char* e = std::getenv("VIHMC_CONTRACT_BF16");
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+    }();
 
     template <typename T>
     int alloc(T** p, int64_t n) {
@@ -578,6 +583,7 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
     q.q_chunks = p->qchunksA;
     q.q_per_chunk = p->qperA;
     q.with_stats = 1;
+    q.bf16x6 = grad && p->W == 100 ? p->contract_bf16x6 : 0;
     const float v = std::max(p->lik.tau_out, 1e-6f);
     q.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
     (void)C;
@@ -922,8 +928,12 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
     const std::string k(key);
     if (k == "fwd_bf16x6") p->fwd_bf16x6 = value ? 1 : 0;
+    else if (k == "contract_bf16x6") p->contract_bf16x6 = value ? 1 : 0;
     else if (k == "graph") p->graph_on = value ? 1 : 0;
-    else return fail("unknown plan option '" + k + "' (fwd_bf16x6, graph)");
+    else return fail("unknown plan option '" + k + "' (fwd_bf16x6, contract_bf16x6, graph)");
+    // captured graphs embed the kernel choice
+    for (auto& g : p->graphs) (void)hipGraphExecDestroy(g.second);
+    p->graphs.clear();
     return 0;
 }
 
