@@ -140,7 +140,9 @@ int vihmc_graph_enable(vihmc_plan* p, int on);
  * layers of the forward with every fp32 product split exactly into three bf16 parts on the bf16 MFMA
  * (six products, fp32 accumulation: fp32-level results, ~4 % faster evaluation); 0 = fp32 MFMA.
  * "contract_bf16x6" (default 1): the same for the side-A contraction (branch x trunk S, likelihood,
- * G, dZ_trunk; width 100). "graph" = vihmc_graph_enable. Changing an option drops captured graphs.
+ * G, dZ_trunk; width 100) and side B. "bwd_bf16x6" (default 1): the same for the layer backward (dX,
+ * dW, db of layers with 100 outputs); its default (environment VIHMC_BWD_BF16) also sizes the backward
+ * row chunks at plan creation. "graph" = vihmc_graph_enable. Changing an option drops captured graphs.
  * Returns nonzero for an unknown key. */
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value);
 

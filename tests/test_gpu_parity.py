@@ -60,9 +60,9 @@ def test_deeponet_engine_matches_golden(name, cuda_device):
             check_logp(float(lpf[0]), float(c.g[f"logp{t}"]))
 
 
-@pytest.mark.parametrize("C,fwd_bf16x6,contract_bf16x6", [(1, 1, 1), (4, 1, 1), (16, 1, 1), (16, 0, 0), (16, 1, 0),
-                                                         (3, 0, 1)])
-def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, contract_bf16x6, cuda_device):
+@pytest.mark.parametrize("C,fwd_bf16x6,contract_bf16x6,bwd_bf16x6", [(1, 1, 1, 1), (4, 1, 1, 1), (16, 1, 1, 1),
+                                                                    (16, 0, 0, 0), (16, 1, 0, 1), (3, 0, 1, 0)])
+def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, contract_bf16x6, bwd_bf16x6, cuda_device):
     """Burgers shape at the chain counts that select different launch geometries (fused forward 4- vs
     12-wave workgroups, fp32 or bf16x6 hidden-layer products, contraction q-splits, backward row chunks):
     every chain (replicated golden thetas) must match the reference closure's golden."""
@@ -70,6 +70,7 @@ def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, contract_bf16x6, 
     eng = engine_for(c, max_chains=C)
     eng.option("fwd_bf16x6", fwd_bf16x6)
     eng.option("contract_bf16x6", contract_bf16x6)
+    eng.option("bwd_bf16x6", bwd_bf16x6)
     n = len(c.thetas)
     th = torch.tensor(np.stack([c.thetas[i % n] for i in range(C)]), device=cuda_device)
     lp, g = eng.logp_grad(th)
@@ -84,8 +85,8 @@ def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, contract_bf16x6, 
 
 
 def test_bf16x6_paths_match_fp32_mfma_paths(cuda_device):
-    """Burgers shape, 16 perturbed chains: the bf16x6 forward + side-A contraction (exact 3-way bf16 split,
-    six products, fp32 accumulation) against the fp32-MFMA kernels on the same inputs. Both are fp32-level
+    """Burgers shape, 16 perturbed chains: the bf16x6 forward, contraction and layer backward (exact 3-way
+    bf16 split, six products, fp32 accumulation) against the fp32-MFMA kernels on the same inputs. Both are fp32-level
     computations, so they agree far inside the golden tolerance: logp to 2e-6 relative, the gradient to
     2e-5 of its norm (measured r01: see the printed values)."""
     c = deeponet_case("deeponet_burgers")
@@ -97,8 +98,8 @@ def test_bf16x6_paths_match_fp32_mfma_paths(cuda_device):
     eng = engine_for(c, max_chains=C)
     res = {}
     for on in (0, 1):
-        eng.option("fwd_bf16x6", on)
-        eng.option("contract_bf16x6", on)
+        for key in ("fwd_bf16x6", "contract_bf16x6", "bwd_bf16x6"):
+            eng.option(key, on)
         lp, g = eng.logp_grad(th)
         res[on] = (lp.double().cpu().numpy(), g.double().cpu().numpy())
     dlp = np.abs(res[1][0] - res[0][0]) / np.abs(res[0][0])

@@ -1,0 +1,301 @@
+// Fused layer backward with fp32 products on the bf16 MFMA (bf16x6, vihmc_bf16x6.h): the same BwdProb
+// contract and outputs as k_bwd_ws (vihmc_layers.hip), for layers with n_out = 100 and n_in <= 112.
+//
+// Replaces the autograd backward of one nn.Linear + activation of the branch / trunk MLPs
+// (Operator_network/VI_HMC/my_make_func.py:53-82, torch autograd through F.linear and tanh):
+//   Dout[m][i] = (sum_k D[m][k] W[k][i]) * act'(H[m][i])        (dX, when has_dx)
+//   part[n][j] = sum_m D[m][n] H[m][j],  part[n_out][n] = sum_m D[m][n]   (dW, db partial of this chunk)
+//
+// One 1024-thread workgroup per CU (16 waves, 4 per SIMD, <= 128 VGPRs) per row chunk; 32-row sub-tiles
+// of D and H are split into bf16 planes by all threads (register prefetch one sub-tile ahead, two LDS
+// buffers, one barrier per sub-tile). LDS (150 KB):
+//   2 x [D planes [3][32][224 B], H planes [3][32][224 B], D fp32 tail [32][4] (features 96..99)]
+//   W^T planes [3][100][208 B] + fp32 tail [100][4], split once per workgroup
+//   dX waves (8): i-tiles {2p, 2p+1} x 16-row half h. A = W^T rows, B = D rows (ds_read_b128 of the
+//                 planes); the 4-long k tail is one exact f32 MFMA that seeds the accumulator.
+//                 Epilogue: act'(h) from the H planes (exact reconstruction h = h2 + h1 + h0), float4 stores.
+//   dW waves (8): output row tiles {2q, 2q+1} x column tiles 0..3 or 4..6; A = D^T and B = H, both by
+//                 transposed reads (k = the 32 rows of the sub-tile).
+//   db: summed from the staged D values by the staging threads (fixed slot -> column map), reduced
+//       in a fixed order at the end. Deterministic: every partial slab has exactly one writer.
+#include "vihmc_internal.h"
+#include "vihmc_bf16x6.h"
+
+#ifndef BB_ABL
+#define BB_ABL 0    // timing-only ablations (wrong results): 1 no loads after the first sub-tile, 2 no dX
+                    // MFMAs, 3 no dW MFMAs
+#endif
+
+namespace vihmc {
+
+namespace {
+using bf6::f32x4;
+using bf6::bf16x8;
+using bf6::bf16x4;
+using bf6::split4;
+using bf6::cat8;
+using bf6::six;
+using bf6::tr_frag;
+
+constexpr int BB_SUB = BWD_SUB;                        // 32 rows per sub-tile
+constexpr int BB_PITCH = bf6::PITCH;                   // D / H plane rows (transposed reads: 7 x 32 B)
+constexpr int BB_PLANE = BB_SUB * BB_PITCH;            // 7168
+constexpr int BB_DP = 0;                               // D planes
+constexpr int BB_HP = 3 * BB_PLANE;                    // H planes
+constexpr int BB_DT = 6 * BB_PLANE;                    // D fp32 tail [32][4]
+constexpr int BB_BUF = BB_DT + BB_SUB * 16;            // 43520 bytes per buffer
+constexpr int BB_WPITCH = 208;                         // W^T plane rows: 13 x 16 B (odd) -> row reads conflict free
+constexpr int BB_WPLANE = 100 * BB_WPITCH;             // 20800 (rows 0..99; tile-6 reads clamp to row 99)
+constexpr int BB_W = 2 * BB_BUF;                       // W^T planes after the two sub-tile buffers
+constexpr int BB_WT = BB_W + 3 * BB_WPLANE;            // W^T fp32 tail [100][4]
+constexpr int BB_LDS = BB_WT + 100 * 16;               // 150080
+constexpr int BB_THREADS = 1024;                       // 8 dX + 8 dW waves, 4 per SIMD
+constexpr int BB_SLOTS = 2;                            // staged float4 per thread (<= 800 D + 896 H)
+
+__device__ __forceinline__ float act_grad_bf(int act, float h) {
+    // derivative from the activation's output (tanh: 1 - h^2, relu: h > 0), as act_grad_from_out_l
+    if (act == ACT_TANH) return 1.f - h * h;
+    if (act == ACT_RELU) return h > 0.f ? 1.f : 0.f;
+    return 1.f;
+}
+}  // namespace
+
+__global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
+    int b = blockIdx.x;
+    const int per0 = args.C * args.p[0].n_wg;
+    const bool second = b >= per0;
+    const BwdProb P = second ? args.p[1] : args.p[0];
+    if (second) b -= per0;
+    const int c = b / P.n_wg;
+    const int wg = b - c * P.n_wg;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int NI4 = (P.n_in + 3) & ~3;
+    const int hq4 = NI4 >> 2;                          // H float4 per row (<= 28)
+    const float* D = P.D + c * P.d_cs;
+    const float* H = P.H + c * P.h_cs;
+    const int r0 = wg * P.rows_per_wg;
+    const int r1 = min(P.M, r0 + P.rows_per_wg);
+
+    // ---- W^T planes (once per workgroup): rows i < n_in, features k < 100 ----
+    if (P.has_dx) {
+        const float* WT = P.WT + c * P.wt_cs;
+        for (int idx = tid; idx < P.n_in * 25; idx += BB_THREADS) {
+            const int r = idx / 25, c4 = idx - r * 25;
+            const f32x4 x = *reinterpret_cast<const f32x4*>(WT + (int64_t)r * P.ldw + 4 * c4);
+            bf16x4 p0, p1, p2;
+            split4(x, p0, p1, p2);
+            unsigned char* o = smw + BB_W + r * BB_WPITCH + 8 * c4;
+            *reinterpret_cast<bf16x4*>(o) = p0;
+            *reinterpret_cast<bf16x4*>(o + BB_WPLANE) = p1;
+            *reinterpret_cast<bf16x4*>(o + 2 * BB_WPLANE) = p2;
+            if (c4 == 24) *reinterpret_cast<f32x4*>(smw + BB_WT + r * 16) = x;
+        }
+    }
+
+    // ---- staging geometry: slot v of this thread moves float4 (row, c4) of D (idx < 800) or H ----
+    const int ntot = BB_SUB * 25 + BB_SUB * hq4;
+    int st[BB_SLOTS];                                  // (row << 8) | c4, -1 idle
+    unsigned st_d = 0;
+#pragma unroll
+    for (int v = 0; v < BB_SLOTS; ++v) {
+        const int idx = tid + BB_THREADS * v;
+        const bool isd = idx < BB_SUB * 25;
+        const int e = isd ? idx : idx - BB_SUB * 25;
+        const int q = isd ? 25 : hq4;
+        const int r = e / q, c4 = e - r * q;
+        st[v] = idx < ntot ? (r << 8) | c4 : -1;
+        st_d |= (isd ? 1u : 0u) << v;
+    }
+    f32x4 pf[BB_SLOTS];
+    f32x4 dcol = {0.f, 0.f, 0.f, 0.f};                 // db partial of this thread's D slot (slot 0 only:
+                                                       // idx < 800 < 1024)
+#define VIHMC_BB_LOAD(SUB)                                                                              \
+    _Pragma("unroll") for (int v = 0; v < BB_SLOTS; ++v) {                                              \
+        const int row = min((SUB) + (max(st[v], 0) >> 8), P.M - 1);                                     \
+        const int c4 = st[v] & 255;                                                                     \
+        pf[v] = ((st_d >> v) & 1) ? reinterpret_cast<const f32x4*>(D + (int64_t)row * P.ldd)[c4]        \
+                                  : reinterpret_cast<const f32x4*>(H + (int64_t)row * P.ldh)[c4];       \
+    }
+#define VIHMC_BB_STORE(SUB, BUF)                                                                        \
+    _Pragma("unroll") for (int v = 0; v < BB_SLOTS; ++v) {                                              \
+        if (st[v] >= 0) {                                                                               \
+            const int r = st[v] >> 8, c4 = st[v] & 255;                                                 \
+            const f32x4 x = ((SUB) + r < r1) ? pf[v] : f32x4{0.f, 0.f, 0.f, 0.f};                       \
+            const bool isd = (st_d >> v) & 1;                                                           \
+            unsigned char* base = smw + (BUF) * BB_BUF + (isd ? BB_DP : BB_HP) + r * BB_PITCH + 8 * c4; \
+            bf16x4 p0, p1, p2;                                                                          \
+            split4(x, p0, p1, p2);                                                                      \
+            *reinterpret_cast<bf16x4*>(base) = p0;                                                      \
+            *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;                                           \
+            *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;                                       \
+            if (isd) {                                                                                  \
+                if (v == 0) dcol += x;                                                                  \
+                if (c4 == 24) *reinterpret_cast<f32x4*>(smw + (BUF) * BB_BUF + BB_DT + r * 16) = x;     \
+            }                                                                                           \
+        }                                                                                               \
+    }
+
+    const int nsub = r1 > r0 ? (r1 - r0 + BB_SUB - 1) / BB_SUB : 0;
+    if (nsub > 0) {
+        VIHMC_BB_LOAD(r0)
+        VIHMC_BB_STORE(r0, 0)
+        if (nsub > 1) {
+            VIHMC_BB_LOAD(r0 + BB_SUB)
+        }
+    }
+
+    if (wave < 8) {
+        // ---------------- dX role: i-tiles {2p, 2p+1} x row half h ----------------
+        const int h = wave & 1, p2 = wave >> 1;
+        const int t0 = 2 * p2;
+        const bool two = t0 + 1 < 7;
+        const unsigned char* wrow0 = smw + BB_W + min(16 * t0 + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
+        const unsigned char* wrow1 = smw + BB_W + min(16 * (t0 + 1) + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
+        const float* wtl = reinterpret_cast<const float*>(smw + BB_WT);
+        const int wr0 = min(16 * t0 + lr, P.n_in - 1), wr1 = min(16 * (t0 + 1) + lr, P.n_in - 1);
+        for (int i = 0; i < nsub; ++i) {
+            const int sub = r0 + i * BB_SUB;
+            __syncthreads();                           // buffer i&1 holds sub-tile i
+            if (i + 1 < nsub) {
+                VIHMC_BB_STORE(sub + BB_SUB, (i + 1) & 1)
+                if (i + 2 < nsub && BB_ABL != 1) {
+                    VIHMC_BB_LOAD(sub + 2 * BB_SUB)
+                }
+            }
+            if (!P.has_dx) continue;
+            const unsigned char* buf = smw + (i & 1) * BB_BUF;
+            const unsigned char* drow = buf + BB_DP + (16 * h + lr) * BB_PITCH + 16 * lg;
+            // the exact f32 tail (features 96..99) seeds each accumulator
+            const float dtl = reinterpret_cast<const float*>(buf + BB_DT)[(16 * h + lr) * 4 + lg];
+            f32x4 acc[2];
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wtl[wr0 * 4 + lg], dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            acc[1] = two ? __builtin_amdgcn_mfma_f32_16x16x4f32(wtl[wr1 * 4 + lg], dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kb = 0; kb < 3; ++kb) {
+                bf16x8 db[3], wa[3], wb[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) {
+                    db[p] = *reinterpret_cast<const bf16x8*>(drow + p * BB_PLANE + 64 * kb);
+                    wa[p] = *reinterpret_cast<const bf16x8*>(wrow0 + p * BB_WPLANE + 64 * kb);
+                    wb[p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
+                }
+                if (BB_ABL != 2) {
+                    acc[0] = six(wa, db, acc[0]);
+                    if (two) acc[1] = six(wb, db, acc[1]);
+                }
+            }
+            const int m = sub + 16 * h + lr;
+            if (m < r1) {
+                const unsigned char* hrow = buf + BB_HP + (16 * h + lr) * BB_PITCH;
+                float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int col = 16 * (t0 + u) + 4 * lg;
+                    if ((u == 1 && !two) || col >= NI4) continue;
+                    const bf16x4 h0 = *reinterpret_cast<const bf16x4*>(hrow + 2 * col);
+                    const bf16x4 h1 = *reinterpret_cast<const bf16x4*>(hrow + BB_PLANE + 2 * col);
+                    const bf16x4 h2 = *reinterpret_cast<const bf16x4*>(hrow + 2 * BB_PLANE + 2 * col);
+                    f32x4 o;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float hv = ((float)h2[r] + (float)h1[r]) + (float)h0[r];
+                        o[r] = (col + r < P.n_in) ? acc[u][r] * act_grad_bf(P.act, hv) : 0.f;
+                    }
+                    *reinterpret_cast<f32x4*>(orow + col) = o;
+                }
+            }
+        }
+    } else {
+        // ---------------- dW role: row tiles {2q, 2q+1} x column tiles 0..3 or 4..6 ----------------
+        const int v8 = wave - 8;
+        const int tn0 = 2 * (v8 >> 1);
+        const bool two = tn0 + 1 < 7;
+        const int tj0 = (v8 & 1) ? 4 : 0;
+        const int ntj = (v8 & 1) ? 3 : 4;
+        f32x4 acc[2][4];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[s2][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int tro = bf6::tr_lane_off(lr, lg);
+        for (int i = 0; i < nsub; ++i) {
+            const int sub = r0 + i * BB_SUB;
+            __syncthreads();
+            if (i + 1 < nsub) {
+                VIHMC_BB_STORE(sub + BB_SUB, (i + 1) & 1)
+                if (i + 2 < nsub && BB_ABL != 1) {
+                    VIHMC_BB_LOAD(sub + 2 * BB_SUB)
+                }
+            }
+            const unsigned char* buf = smw + (i & 1) * BB_BUF;
+            bf16x8 da[2][3];
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) da[s2][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * (tn0 + (two ? s2 : 0)));
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (t >= ntj) break;
+                bf16x8 hb[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) hb[p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 16 * (tj0 + t));
+                if (BB_ABL != 3) {
+                    acc[0][t] = six(da[0], hb, acc[0][t]);
+                    if (two) acc[1][t] = six(da[1], hb, acc[1][t]);
+                }
+            }
+        }
+        float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            if (s2 == 1 && !two) continue;
+            const int tn = tn0 + s2;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int j = 16 * (tj0 + t) + lr;
+                if (t >= ntj || j >= NI4) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = 16 * tn + 4 * lg + r;
+                    if (n < P.n_out) part[(int64_t)n * NI4 + j] = (j < P.n_in) ? acc[s2][t][r] : 0.f;
+                }
+            }
+        }
+    }
+#undef VIHMC_BB_LOAD
+#undef VIHMC_BB_STORE
+
+    // ---- db: per-slot column partials -> LDS [32 rows][25 float4] -> fixed-order sum over rows ----
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smw);
+    if (st[0] >= 0 && (st_d & 1)) red[(st[0] >> 8) * 25 + (st[0] & 255)] = dcol;
+    __syncthreads();
+    if (tid < 25) {
+        f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < BB_SUB; ++r) sacc += red[r * 25 + tid];
+        float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride + (int64_t)P.n_out * NI4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (4 * tid + e < P.n_out) part[4 * tid + e] = sacc[e];
+    }
+}
+
+bool bwd_bf_ok(const BwdArgs& a) {
+    for (int i = 0; i < a.nprob; ++i) {
+        const BwdProb& p = a.p[i];
+        if (p.n_out != 100 || p.n_in > 112 || (p.has_dx && p.n_in != 100)) return false;
+        if ((p.ldd & 3) || (p.ldh & 3) || (p.has_dx && (p.ldw & 3))) return false;
+    }
+    return true;
+}
+
+hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s) {
+    if (!bwd_bf_ok(a)) return hipErrorInvalidValue;
+    const int blocks = a.C * a.p[0].n_wg + (a.nprob > 1 ? a.C * a.p[1].n_wg : 0);
+    hipLaunchKernelGGL(k_bwd_bf, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace vihmc

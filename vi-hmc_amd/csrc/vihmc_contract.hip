@@ -476,6 +476,7 @@ static hipError_t launch_contract_t(const ContractProb& p, int C, hipStream_t s)
     const size_t shm = contract_lds_bytes(p.W);
     const int w = p.W;
     if (w == 100 && GRAD && !LOADG && p.bf16x6) return launch_contract_bf(p, C, s);
+    if (w == 100 && GRAD && LOADG && p.bf16x6) return launch_contract_bf_b(p, C, s);
     if (w == 100 && GRAD && !LOADG && VIHMC_CONTRACT_WS) {
         dim3 blk2(512);
         VIHMC_LAUNCH_C(k_contract_ws, g, blk2, sizeof(float) * 3 * CWS_QBUF + 16 * 2 * CWS_GBUF, s, p);

@@ -27,9 +27,10 @@
 //             16-row S tiles, G = gscale (S + b0 - y), likelihood sums, G^T stores for side B.
 //   D wave w: one chunk behind: splits G, dOwn[32 rows][112] += G^T Q over the chunk's 32 rows.
 #include "vihmc_internal.h"
+#include "vihmc_bf16x6.h"
 
-#ifndef CB_DRAIN
-#define CB_DRAIN 0
+#ifndef CB_ABL
+#define CB_ABL 0        // timing-only ablations: 1 no G^T stores, 2 no D MFMAs, 3 no S MFMAs (wrong results)
 #endif
 #ifndef CB_YBUF
 #define CB_YBUF 1
@@ -41,63 +42,30 @@
 namespace vihmc {
 
 namespace {
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+using bf6::f32x4;
+using bf6::bf16x8;
+using bf6::bf16x4;
+using bf6::lds_bf16x4;
+using bf6::split4;
+using bf6::cat8;
+using bf6::six;
+typedef bf6::u32x4 u32x4_c;
+constexpr uint32_t OOB_C = bf6::OOB;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_c(const void* p, uint32_t bytes) {
+    return bf6::make_rsrc(p, bytes);
+}
 
-constexpr int CB_QC = 32;                          // branch rows per chunk
-constexpr int CB_PITCH = 224;                      // bytes per bf16 image row (112 features)
+constexpr int CB_QC = CONTRACT_SPLIT_ROWS;         // branch rows per chunk (32)
+constexpr int CB_PITCH = bf6::PITCH;               // bytes per bf16 image row (112 features)
 constexpr int CB_PLANE = CB_QC * CB_PITCH;         // 7168
 constexpr int CB_TAIL = 3 * CB_PLANE;              // fp32 [32][4] tail image offset
-constexpr int CB_QIMG = CB_TAIL + CB_QC * 16;      // 22016 bytes per Q buffer
+constexpr int CB_BLOCK = CONTRACT_SPLIT_BLOCK;     // 22528: 3 planes + tail, padded to 22 KB
+static_assert(CB_TAIL + CB_QC * 16 <= CB_BLOCK && CB_BLOCK % 1024 == 0, "split block layout");
+constexpr int CB_QIMG = CB_BLOCK;                  // bytes per Q buffer (one pre-split block)
 constexpr int CB_GIMG = 4 * 4 * 64 * 16;           // 4 S waves x 4 f32x4 x 64 lanes = 16384
 constexpr int CB_LDS = 3 * CB_QIMG + 2 * CB_GIMG;  // 98816
-constexpr int CB_SLOTS = CB_QC * 25;               // f32x4 per chunk (25 per 100-wide row)
+constexpr int CB_GLDS = CB_BLOCK / 1024;           // 22 wave-wide 16-B-per-lane DMA copies per block
 
-typedef unsigned int u32x4_c __attribute__((ext_vector_type(4)));
-constexpr uint32_t OOB_C = 0x80000000u;
-
-// buffer resource over [p, p + bytes) from wave-uniform inputs (out-of-range loads read 0, stores drop)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_c(const void* p, uint32_t bytes) {
-    const uint64_t a = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    void* q = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-    return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
-__device__ __forceinline__ f32x4 mfma_bf(bf16x8 a, bf16x8 b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-// exact three-way split of 4 values into bf16 planes
-__device__ __forceinline__ void split4(f32x4 x, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const __bf16 a = (__bf16)x[j];
-        const float r = x[j] - (float)a;
-        const __bf16 b = (__bf16)r;
-        p0[j] = a;
-        p1[j] = b;
-        p2[j] = (__bf16)(r - (float)b);
-    }
-}
-
-__device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
-    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-
-// acc += a.b over one 32-long k-block, six products, small terms first
-__device__ __forceinline__ f32x4 six(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 acc) {
-    acc = mfma_bf(a[2], b[0], acc);
-    acc = mfma_bf(a[1], b[1], acc);
-    acc = mfma_bf(a[0], b[2], acc);
-    acc = mfma_bf(a[1], b[0], acc);
-    acc = mfma_bf(a[0], b[1], acc);
-    acc = mfma_bf(a[0], b[0], acc);
-    return acc;
-}
 }  // namespace
 
 __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
@@ -116,34 +84,16 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
     const int q_hi = min(q_lo + P.q_per_chunk, P.Mq);
     const int nchunks = q_hi > q_lo ? (q_hi - q_lo + CB_QC - 1) / CB_QC : 0;
 
-    // chunk staging: 800 f32x4 (32 rows x 25), slots tid and tid + 512; the second slot of threads
-    // >= 288 duplicates a valid one and is not stored
-    const int v0 = tid, v1 = min(tid + 512, CB_SLOTS - 1);
-    const bool st1 = tid + 512 < CB_SLOTS;
-    const int r0s = v0 / 25, c0s = v0 - r0s * 25, r1s = v1 / 25, c1s = v1 - r1s * 25;
-    f32x4 stg0, stg1;
-#define VIHMC_CB_LOAD(CI)                                                                                   \
-    stg0 = reinterpret_cast<const f32x4*>(Q + (int64_t)min(q_lo + (CI) * CB_QC + r0s, P.Mq - 1) * P.ldq)[c0s]; \
-    stg1 = reinterpret_cast<const f32x4*>(Q + (int64_t)min(q_lo + (CI) * CB_QC + r1s, P.Mq - 1) * P.ldq)[c1s];
-#define VIHMC_CB_STORE1(BUF, X, R, CC)                                                                      \
-    {                                                                                                       \
-        unsigned char* img = smc + (BUF) * CB_QIMG;                                                         \
-        bf16x4 p0, p1, p2;                                                                                  \
-        split4(X, p0, p1, p2);                                                                              \
-        unsigned char* d = img + (R) * CB_PITCH + (CC) * 8;                                                 \
-        *reinterpret_cast<bf16x4*>(d) = p0;                                                                 \
-        *reinterpret_cast<bf16x4*>(d + CB_PLANE) = p1;                                                      \
-        *reinterpret_cast<bf16x4*>(d + 2 * CB_PLANE) = p2;                                                  \
-        if ((CC) == 24) *reinterpret_cast<f32x4*>(img + CB_TAIL + (R) * 16) = X;                            \
-    }
-#define VIHMC_CB_STORE(BUF)                           \
-    VIHMC_CB_STORE1(BUF, stg0, r0s, c0s)              \
-    if (st1) VIHMC_CB_STORE1(BUF, stg1, r1s, c1s)
-
-    if (nchunks > 0) {
-        VIHMC_CB_LOAD(0)
-        VIHMC_CB_STORE(0)
-        VIHMC_CB_LOAD(min(1, nchunks - 1))
+    // Q chunks: blocks of the pre-split image (vihmc_split_blocks), copied global -> LDS by the D waves
+    // with wave-wide DMA (global_load_lds_dwordx4: 1 KB per instruction, no VGPRs, no VALU)
+    const unsigned char* qblk = P.qimg + c * P.qimg_cs + (int64_t)(q_lo / CB_QC) * CB_BLOCK;
+#define VIHMC_CB_GLDS(CI, BUF)                                                                              \
+    for (int k = wave - 4; k < CB_GLDS; k += 4)                                                             \
+        __builtin_amdgcn_global_load_lds(                                                                   \
+            reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
+            (__attribute__((address_space(3))) void*)(smc + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
+    if (wave >= 4 && nchunks > 0) {
+        VIHMC_CB_GLDS(0, 0)
     }
 
     if (wave < 4) {
@@ -185,31 +135,26 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
             goff[s] = ovalid[s] ? (uint32_t)(oo * P.ldg + q_lo + 4 * lg) * 4u : OOB_C;
         }
         const uint32_t ystep = (uint32_t)P.ldy * 4u;
-        float yn[2][2][4];      // [sub][s][r], one chunk ahead
-#define VIHMC_CB_YLOAD(CI)                                                                               \
+        // targets [sub][s][r] one chunk ahead in two register sets used alternately (the loop is unrolled
+        // by two), so no register copy forces a wait on the newest loads and the G^T stores
+        float ya[2][2][4], yb[2][2][4];
+#define VIHMC_CB_YLOAD(YN, CI)                                                                           \
         _Pragma("unroll") for (int sub = 0; sub < 2; ++sub)                                              \
             _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                \
                 _Pragma("unroll") for (int r = 0; r < 4; ++r)                                            \
-                    yn[sub][s][r] = CB_YBUF ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32( \
+                    YN[sub][s][r] = CB_YBUF ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32( \
                         yrs, yoff[s], (uint32_t)(q_lo + (CI) * CB_QC + 16 * sub + r) * ystep, 0))             \
                         : Yc[(int64_t)min(q_lo + (CI) * CB_QC + 16 * sub + 4 * lg + r, P.Mq - 1) * P.ldy +    \
                              min(o0 + 16 * s + lr, P.Mo - 1)];
-        VIHMC_CB_YLOAD(0)
-        for (int i = 0; i <= nchunks; ++i) {
+        VIHMC_CB_YLOAD(ya, 0)
+        auto s_chunk = [&](int i, float (&yv)[2][2][4], float (&yn)[2][2][4]) __attribute__((always_inline)) {
+            if (i > nchunks) return;                // same barrier count as the D role
             __syncthreads();
             if (i < nchunks) {
                 const int q0 = q_lo + i * CB_QC;
                 const bool full = q0 + CB_QC <= q_hi;
                 const unsigned char* img = smc + (i % 3) * CB_QIMG;
-                float yv[2][2][4];
-#pragma unroll
-                for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-                    for (int s = 0; s < 2; ++s)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) yv[sub][s][r] = yn[sub][s][r];
-                VIHMC_CB_YLOAD(min(i + 1, nchunks - 1))
-                if (CB_DRAIN) __builtin_amdgcn_s_waitcnt(0x0F70);
+                VIHMC_CB_YLOAD(yn, min(i + 1, nchunks - 1))
                 f32x4* gdst = reinterpret_cast<f32x4*>(smc + 3 * CB_QIMG + (i & 1) * CB_GIMG) + w * 256;
                 float ps = 0.f;
 #pragma unroll
@@ -222,8 +167,10 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
 #pragma unroll
                         for (int p = 0; p < 3; ++p)
                             qa[p] = *reinterpret_cast<const bf16x8*>(row + p * CB_PLANE + 64 * kb);
-                        sacc[0] = six(qa, ob[0][kb], sacc[0]);
-                        sacc[1] = six(qa, ob[1][kb], sacc[1]);
+                        if (CB_ABL != 3) {
+                            sacc[0] = six(qa, ob[0][kb], sacc[0]);
+                            sacc[1] = six(qa, ob[1][kb], sacc[1]);
+                        }
                     }
                     const float qt = reinterpret_cast<const float*>(img + CB_TAIL)[(16 * sub + lr) * 4 + lg];
                     f32x4 tacc[2];
@@ -262,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
                             }
                         }
                     }
-                    if (P.gout && CB_GBUF) {
+                    if (P.gout && CB_GBUF && CB_ABL != 1) {
                         const uint32_t qofs = (uint32_t)(q0 - q_lo + 16 * sub) * 4u;
                         if (full) {
 #pragma unroll
@@ -287,8 +234,10 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
                 // sum r^2 (no cancellation): per-chunk fp32 partial of 16 terms per lane, then fp64
                 ssq += (double)ps;
             }
-            VIHMC_CB_STORE((i + 1) % 3)
-            VIHMC_CB_LOAD(max(min(i + 2, nchunks - 1), 0))
+        };
+        for (int i = 0; i <= nchunks; i += 2) {
+            s_chunk(i, ya, yb);
+            s_chunk(i + 1, yb, ya);
         }
         if (P.with_stats) {
 #pragma unroll
@@ -316,6 +265,11 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
     const int tr_off = (4 * lg + (lr >> 2)) * CB_PITCH + 8 * (lr & 3);
     for (int i = 0; i <= nchunks; ++i) {
         __syncthreads();
+        // chunk i+1 -> buffer (i+1)%3 (last read by this role in iteration i-1, by S in i-2); the copies
+        // land while this iteration computes and are drained by the next barrier (vmcnt(0))
+        if (i + 1 < nchunks) {
+            VIHMC_CB_GLDS(i + 1, (i + 1) % 3)
+        }
         if (i >= 1) {
             const unsigned char* img = smc + ((i - 1) % 3) * CB_QIMG;
             const f32x4* gsrc = reinterpret_cast<const f32x4*>(smc + 3 * CB_QIMG + ((i - 1) & 1) * CB_GIMG) + w * 256;
@@ -339,12 +293,12 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
                     const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 16 * CB_PITCH));
                     qb[p] = cat8(lo, hi);
                 }
-                dacc[0][t] = six(ga[0], qb, dacc[0][t]);
-                dacc[1][t] = six(ga[1], qb, dacc[1][t]);
+                if (CB_ABL != 2) {
+                    dacc[0][t] = six(ga[0], qb, dacc[0][t]);
+                    dacc[1][t] = six(ga[1], qb, dacc[1][t]);
+                }
             }
         }
-        VIHMC_CB_STORE((i + 1) % 3)
-        VIHMC_CB_LOAD(max(min(i + 2, nchunks - 1), 0))
     }
     float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
 #pragma unroll
@@ -359,14 +313,167 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
                 if (oo < P.Mo) out[(int64_t)oo * P.ldout + j] = (j < 100) ? dacc[s][t][r] : 0.f;
             }
         }
-#undef VIHMC_CB_LOAD
-#undef VIHMC_CB_STORE1
-#undef VIHMC_CB_STORE
+#undef VIHMC_CB_GLDS
 #undef VIHMC_CB_YLOAD
 }
 
+// Split rows [rows][ld] (width 100) of every chain into the blocked bf16x6 image: block b holds rows
+// 32b .. 32b+31 as planes [3][32][112] bf16 (features 100..111 and rows past `rows` zero) followed by the
+// fp32 tail [32][4] (features 96..99), CONTRACT_SPLIT_BLOCK bytes per block.
+__global__ __launch_bounds__(256) void k_split_blocks(const float* src, int64_t src_cs, int ld, int rows,
+                                                     unsigned char* dst, int64_t dst_cs, int nblk) {
+    const int c = blockIdx.x / nblk, blk = blockIdx.x - c * nblk;
+    const float* sc = src + c * src_cs;
+    unsigned char* d = dst + c * dst_cs + (int64_t)blk * CB_BLOCK;
+    for (int it = threadIdx.x; it < CB_QC * 28; it += blockDim.x) {
+        const int r = it / 28, g = it - r * 28, row = blk * CB_QC + r;
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        if (g < 25 && row < rows) x = *reinterpret_cast<const f32x4*>(sc + (int64_t)row * ld + 4 * g);
+        bf16x4 p0, p1, p2;
+        split4(x, p0, p1, p2);
+        unsigned char* o = d + r * CB_PITCH + 8 * g;
+        *reinterpret_cast<bf16x4*>(o) = p0;
+        *reinterpret_cast<bf16x4*>(o + CB_PLANE) = p1;
+        *reinterpret_cast<bf16x4*>(o + 2 * CB_PLANE) = p2;
+        if (g == 24) *reinterpret_cast<f32x4*>(d + CB_TAIL + r * 16) = x;
+    }
+}
+
+hipError_t launch_split_blocks(const float* src, int64_t src_cs, int ld, int rows, unsigned char* dst,
+                               int64_t dst_cs, int C, hipStream_t s) {
+    const int nblk = (rows + CB_QC - 1) / CB_QC;
+    hipLaunchKernelGGL(k_split_blocks, dim3(C * nblk), dim3(256), 0, s, src, src_cs, ld, rows, dst, dst_cs, nblk);
+    return hipGetLastError();
+}
+
+
+// =============================================================================================
+// Side B (load-G), bf16x6: dOwn[o][j] += sum_q G[q][o] Q[q][j] with G read from side A's G^T (P.Y,
+// [q][o] with ldy) and Q = the trunk outputs pre-split into blocks. No S role: all 8 waves are alike,
+// 32 owner (branch) rows each (256 per workgroup); per 32-row chunk each wave loads its G (one chunk
+// ahead, two register sets), splits it into the A operand (same k order as the side-A D role) and runs
+// 7 column tiles x 2 row tiles x 6 products against transposed reads of the shared chunk image.
+// =============================================================================================
+constexpr int CBB_OWN = 256;        // owner rows per workgroup (8 waves x 32)
+
+__global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smb[];
+    int b = blockIdx.x;
+    if (P.xcd_group) {
+        const int xcd = b & 7, k = b >> 3;
+        const int gx = k / P.o_tiles, og = k - gx * P.o_tiles;
+        b = (gx * 8 + xcd) * P.o_tiles + og;
+    }
+    const int per_chain = P.o_tiles * P.q_chunks;
+    const int c = b / per_chain;
+    b -= c * per_chain;
+    const int qc = b / P.o_tiles;
+    const int og = b - qc * P.o_tiles;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int o0 = og * CBB_OWN + wave * 32;
+    const int q_lo = qc * P.q_per_chunk;
+    const int q_hi = min(q_lo + P.q_per_chunk, P.Mq);
+    const int nchunks = q_hi > q_lo ? (q_hi - q_lo + CB_QC - 1) / CB_QC : 0;
+    const unsigned char* qblk = P.qimg + c * P.qimg_cs + (int64_t)(q_lo / CB_QC) * CB_BLOCK;
+#define VIHMC_CBB_GLDS(CI, BUF)                                                                             \
+    for (int k = wave; k < CB_GLDS; k += 8)                                                                 \
+        __builtin_amdgcn_global_load_lds(                                                                   \
+            reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
+            (__attribute__((address_space(3))) void*)(smb + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
+
+    // G[q][o] for this lane: rows 4lg + jj (jj < 4) and 16 + 4lg + jj - 4 of the chunk, column o0+16s+lr;
+    // buffer loads with the whole offset in the range-checked VGPR: rows past Mq read 0, rows past q_hi
+    // (another workgroup's range, only in a partial last chunk) are sent out of range
+    const float* Gc = P.Y + c * P.y_cs;
+    const __amdgpu_buffer_rsrc_t grs = make_rsrc_c(Gc, (uint32_t)((int64_t)P.Mq * P.ldy * 4));
+    uint32_t gcol[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) gcol[s] = (uint32_t)min(o0 + 16 * s + lr, P.Mo - 1) * 4u;
+    const uint32_t ystep = (uint32_t)P.ldy * 4u;
+    float ga_[2][8], gb_[2][8];
+#define VIHMC_CBB_GLOAD(GN, CI)                                                                             \
+    {                                                                                                       \
+        const int qb0 = q_lo + (CI) * CB_QC;                                                                \
+        _Pragma("unroll") for (int jj = 0; jj < 8; ++jj) {                                                  \
+            const int qq = qb0 + (jj < 4 ? 4 * lg + jj : 12 + 4 * lg + jj);                                 \
+            const uint32_t roff = qq < q_hi ? (uint32_t)qq * ystep : OOB_C;                                 \
+            _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                   \
+                GN[s][jj] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, roff + gcol[s], 0, 0)); \
+        }                                                                                                   \
+    }
+
+    if (nchunks > 0) {
+        VIHMC_CBB_GLDS(0, 0)
+        VIHMC_CBB_GLOAD(ga_, 0)
+    }
+    f32x4 dacc[2][7];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) dacc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int tr_off = (4 * lg + (lr >> 2)) * CB_PITCH + 8 * (lr & 3);
+    auto chunk = [&](int i, float (&gv)[2][8], float (&gn)[2][8]) __attribute__((always_inline)) {
+        if (i >= nchunks) return;
+        __syncthreads();                      // chunk i landed (vmcnt(0)); buffer (i+1)%3 free
+        if (i + 1 < nchunks) {
+            VIHMC_CBB_GLDS(i + 1, (i + 1) % 3)
+            VIHMC_CBB_GLOAD(gn, i + 1)
+        }
+        const unsigned char* img = smb + (i % 3) * CB_QIMG;
+        bf16x8 ga[2][3];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x4 l0, l1, l2, h0, h1, h2;
+            split4(f32x4{gv[s][0], gv[s][1], gv[s][2], gv[s][3]}, l0, l1, l2);
+            split4(f32x4{gv[s][4], gv[s][5], gv[s][6], gv[s][7]}, h0, h1, h2);
+            ga[s][0] = cat8(l0, h0);
+            ga[s][1] = cat8(l1, h1);
+            ga[s][2] = cat8(l2, h2);
+        }
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            bf16x8 qb[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                const unsigned char* a = img + p * CB_PLANE + tr_off + 32 * t;
+                const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));
+                const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 16 * CB_PITCH));
+                qb[p] = cat8(lo, hi);
+            }
+            dacc[0][t] = six(ga[0], qb, dacc[0][t]);
+            dacc[1][t] = six(ga[1], qb, dacc[1][t]);
+        }
+    };
+    for (int i = 0; i < nchunks; i += 2) {
+        chunk(i, ga_, gb_);
+        chunk(i + 1, gb_, ga_);
+    }
+    float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int j = 16 * t + lr;
+            if (j >= P.ldout) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int oo = o0 + 16 * s + 4 * lg + r;
+                if (oo < P.Mo) out[(int64_t)oo * P.ldout + j] = (j < 100) ? dacc[s][t][r] : 0.f;
+            }
+        }
+#undef VIHMC_CBB_GLDS
+#undef VIHMC_CBB_GLOAD
+}
+
+hipError_t launch_contract_bf_b(const ContractProb& p, int C, hipStream_t s) {
+    if (p.W != 100 || !p.load_g || !p.qimg || p.q_per_chunk % CB_QC) return hipErrorInvalidValue;
+    dim3 g(C * p.o_tiles * p.q_chunks), blk(512);
+    hipLaunchKernelGGL(k_contract_bf_b, g, blk, 3 * CB_QIMG, s, p);
+    return hipGetLastError();
+}
+
 hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s) {
-    if (p.W != 100 || p.load_g) return hipErrorInvalidValue;
+    if (p.W != 100 || p.load_g || !p.qimg || p.q_per_chunk % CB_QC) return hipErrorInvalidValue;
     dim3 g(C * p.o_tiles * p.q_chunks), blk(512);
     hipLaunchKernelGGL(k_contract_bf, g, blk, CB_LDS, s, p);
     return hipGetLastError();

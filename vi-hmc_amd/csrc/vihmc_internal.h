@@ -12,6 +12,8 @@ enum { MODE_FWD = 0, MODE_BWD = 1 };
 // contraction geometry (vihmc_contract.hip): 4 waves x 32 owner rows per workgroup, 16-row Q chunks
 constexpr int CONTRACT_OWN_PER_WG = 128;
 constexpr int CONTRACT_QC = 16;
+constexpr int CONTRACT_SPLIT_ROWS = 32;      // rows per block of the pre-split (bf16x6) contraction image
+constexpr int CONTRACT_SPLIT_BLOCK = 22528;  // bytes per block: 3 x [32][112] bf16 + [32][4] fp32, padded
 // row-dot geometry (vihmc_layers.hip): 4 waves per workgroup, 16*MS rows per wave
 constexpr int ROWDOT_WAVES = 4;
 
@@ -70,6 +72,8 @@ struct BwdArgs {
     int32_t nprob, C;
 };
 hipError_t launch_bwd(const BwdArgs& a, int nti, hipStream_t s);
+bool bwd_bf_ok(const BwdArgs& a);                       // k_bwd_bf handles every problem of the launch
+hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // Fused branch x trunk contraction with the Gaussian likelihood, owner form.
@@ -98,6 +102,7 @@ struct ContractProb {
                                           //    (requires C * q_chunks % 8 == 0; speed only)
     int32_t bf16x6;                       // side A, W = 100: products on the bf16 MFMA, 3-way split
                                           //    operands, six products (k_contract_bf)
+    const unsigned char* qimg; int64_t qimg_cs;   // bf16x6: Q pre-split into blocks (launch_split_blocks)
     float gscale;
 };
 
@@ -105,6 +110,10 @@ struct ContractProb {
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s);
 hipError_t launch_contract(const ContractProb& p, int C, bool with_grad, hipStream_t s);
 hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s);
+hipError_t launch_contract_bf_b(const ContractProb& p, int C, hipStream_t s);
+constexpr int CONTRACT_BF_B_OWN = 256;       // side-B bf16x6 owner rows per workgroup
+hipError_t launch_split_blocks(const float* src, int64_t src_cs, int ld, int rows, unsigned char* dst,
+                               int64_t dst_cs, int C, hipStream_t s);
 size_t contract_lds_bytes(int W);
 hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* frozen, const int32_t* map_w,
                               const int32_t* map_wt, int64_t D, hipStream_t s);

@@ -91,6 +91,10 @@ struct vihmc_plan {
     float* y = nullptr;
     float* gT = nullptr;        // per chain G^T [P][N] (side A -> side B); gT_cs floats per chain
     int64_t gT_cs = 0;
+    unsigned char* qsplitA = nullptr;   // per chain: branch outputs pre-split for k_contract_bf (W = 100)
+    int64_t qsplitA_cs = 0;             // bytes per chain
+    unsigned char* qsplitB = nullptr;   // per chain: trunk outputs pre-split for k_contract_bf_b
+    int64_t qsplitB_cs = 0;
     float* partB = nullptr;
     int64_t partB_cs = 0;
     int qchunksB = 1, qperB = 32;
@@ -126,6 +130,12 @@ struct vihmc_plan {
     // fp32-level accuracy, vihmc_fused.hip); VIHMC_FWD_BF16=0 or vihmc_plan_option turns it off
     int fwd_bf16x6 = [] {
         const char* e = std::getenv("VIHMC_FWD_BF16");
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+    }();
+    // layer backward in the same form (k_bwd_bf, layers with n_out = 100, n_in <= 112); VIHMC_BWD_BF16=0
+    // turns it off. Read at plan creation: it also sizes the backward row chunks (1 workgroup per CU)
+    int bwd_bf16x6 = [] {
+        const char* e = std::getenv("VIHMC_BWD_BF16");
         return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
     }();
     // side-A contraction in the same bf16x6 form (k_contract_bf); VIHMC_CONTRACT_BF16=0 turns it off
@@ -315,6 +325,12 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     if (int rc = p->upload(&p->y, y, NP)) return rc;
     p->gT_cs = r64(NP);
     if (int rc = p->alloc(&p->gT, p->gT_cs * C)) return rc;
+    if (p->W == 100) {
+        p->qsplitA_cs = (int64_t)cdiv(p->N, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
+        if (int rc = p->alloc(&p->qsplitA, p->qsplitA_cs * C)) return rc;
+        p->qsplitB_cs = (int64_t)cdiv(p->P, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
+        if (int rc = p->alloc(&p->qsplitB, p->qsplitB_cs * C)) return rc;
+    }
 
     // ---- per-chain work buffers ---------------------------------------------------------------------
     for (int net = 0; net < 2; ++net) {
@@ -333,12 +349,13 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             if (int rc = p->alloc(&n.delta[b], n.delta_cs * C)) return rc;
         // weight-gradient partial slabs: one per row chunk
         // fused-backward row chunk: one workgroup per chunk, sized so a max_chains launch over both
-        // nets is ~one resident round (2 workgroups/CU x 256 CUs; the kernel needs ~68 KB of LDS)
+        // nets is ~one resident round (k_bwd_ws: 2 workgroups/CU x 256 CUs, ~68 KB of LDS; k_bwd_bf:
+        // 1 workgroup/CU, 87 KB of LDS and 256-VGPR waves)
         {
             const int64_t rows_all = (int64_t)p->nets[0].rows + p->nets[1].rows;
             // two 512-thread workgroups per CU, 32-row sub-tiles; the chunk R (a multiple of the sub-tile)
             // is the smallest for which both nets' workgroups of all max_chains chains fit one resident round
-            const int slots = 512, sub = BWD_SUB;
+            const int slots = p->bwd_bf16x6 ? 256 : 512, sub = BWD_SUB;
             const int64_t r_b = p->nets[0].rows, r_t = p->nets[1].rows;
             int64_t R = std::max<int64_t>(sub, (cdiv((int64_t)C * rows_all, slots) + sub - 1) / sub * sub);
             while ((int64_t)C * (cdiv(r_b, R) + cdiv(r_t, R)) > slots && R < rows_all) R += sub;
@@ -361,7 +378,8 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         const int og_a = cdiv(p->P, CONTRACT_OWN_PER_WG), og_b = cdiv(p->N, CONTRACT_OWN_PER_WG);
         int qa = std::max(1, std::min(8, (int)std::lround(1024.0 / ((double)C * og_a))));
         if (const char* e = std::getenv("VIHMC_QSPLIT_A")) qa = std::max(1, std::min(64, std::atoi(e)));
-        p->qperA = (int)(((int64_t)cdiv(p->N, qa) + CONTRACT_QC - 1) / CONTRACT_QC * CONTRACT_QC);
+        // multiple of 32 rows: whole blocks of the pre-split image for k_contract_bf (and 16-row chunks)
+        p->qperA = (int)(((int64_t)cdiv(p->N, qa) + CONTRACT_SPLIT_ROWS - 1) / CONTRACT_SPLIT_ROWS * CONTRACT_SPLIT_ROWS);
         p->qchunksA = cdiv(p->N, p->qperA);
         if (p->qchunksA > 1) {
             p->partA_cs = r64((int64_t)p->qchunksA * p->P * p->ldz);
@@ -369,8 +387,13 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         }
         // side B: workgroups own 128 branch rows, the trunk sweep is split to match side A's grid
         int qc = std::max(1, (int)std::lround((double)og_a * p->qchunksA / og_b));
+        if (p->W == 100) {
+            // bf16x6 side B (k_contract_bf_b, 256 owner rows, 1 workgroup per CU): ~256 workgroups
+            qc = std::max(1, (int)std::lround(256.0 / ((double)C * cdiv(p->N, CONTRACT_BF_B_OWN))));
+            qc = std::min(qc, cdiv(p->P, CONTRACT_SPLIT_ROWS));
+        }
         if (const char* e = std::getenv("VIHMC_QSPLIT_B")) qc = std::max(1, std::min(256, std::atoi(e)));
-        p->qperB = (int)(((int64_t)cdiv(p->P, qc) + CONTRACT_QC - 1) / CONTRACT_QC * CONTRACT_QC);
+        p->qperB = (int)(((int64_t)cdiv(p->P, qc) + CONTRACT_SPLIT_ROWS - 1) / CONTRACT_SPLIT_ROWS * CONTRACT_SPLIT_ROWS);
         p->qchunksB = cdiv(p->P, p->qperB);
         p->partB_cs = r64((int64_t)p->qchunksB * p->N * p->ldz);
         if (int rc = p->alloc(&p->partB, p->partB_cs * C)) return rc;
@@ -584,6 +607,8 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
     q.q_per_chunk = p->qperA;
     q.with_stats = 1;
     q.bf16x6 = grad && p->W == 100 ? p->contract_bf16x6 : 0;
+    q.qimg = p->qsplitA;
+    q.qimg_cs = p->qsplitA_cs;
     const float v = std::max(p->lik.tau_out, 1e-6f);
     q.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
     (void)C;
@@ -597,6 +622,8 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
     const bool want_grad = grad != nullptr && out == nullptr;
     {
         ContractProb a = side_a(p, C, want_grad, out);
+        if (a.bf16x6)
+            HIPCHK(launch_split_blocks(a.Q, a.q_cs, a.ldq, p->N, p->qsplitA, p->qsplitA_cs, C, s));
         hipEvent_t stop = nullptr;
         if (int rc = p->timing_begin(0, s, &stop)) return rc;
         HIPCHK(launch_contract(a, C, want_grad, s));
@@ -618,6 +645,9 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         q.ldy = p->N;
         q.y_cs = p->gT_cs;
         q.load_g = 1;
+        q.bf16x6 = p->W == 100 ? p->contract_bf16x6 : 0;
+        q.qimg = p->qsplitB;
+        q.qimg_cs = p->qsplitB_cs;
         q.xcd_group = ((int64_t)C * p->qchunksB) % 8 == 0 ? 1 : 0;
         if (const char* e = std::getenv("VIHMC_XCD_GROUP")) q.xcd_group = q.xcd_group && std::atoi(e) != 0;
         q.b0 = p->packed;
@@ -630,12 +660,14 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         q.Mo = p->N;
         q.Mq = p->P;
         q.W = p->W;
-        q.o_tiles = cdiv(p->N, CONTRACT_OWN_PER_WG);
+        q.o_tiles = cdiv(p->N, q.bf16x6 ? CONTRACT_BF_B_OWN : CONTRACT_OWN_PER_WG);
         q.q_chunks = p->qchunksB;
         q.q_per_chunk = p->qperB;
         q.with_stats = 0;
         const float v = std::max(p->lik.tau_out, 1e-6f);
         q.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
+        if (q.bf16x6)
+            HIPCHK(launch_split_blocks(q.Q, q.q_cs, q.ldq, p->P, p->qsplitB, p->qsplitB_cs, C, s));
         hipEvent_t stop = nullptr;
         if (int rc = p->timing_begin(1, s, &stop)) return rc;
         HIPCHK(launch_contract(q, C, true, s));
@@ -681,7 +713,8 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
                 nti = std::max(nti, nt_of(L.n_in));
             }
             if (ba.nprob == 1) ba.p[1] = ba.p[0];
-            HIPCHK(launch_bwd(ba, nti, s));
+            if (p->bwd_bf16x6 && bwd_bf_ok(ba)) HIPCHK(launch_bwd_bf(ba, s));
+            else HIPCHK(launch_bwd(ba, nti, s));
             for (int net = 0; net < 2; ++net) {
                 const int j = (int)p->nets[net].L.size() - 1 - i;
                 if (j >= 1) cur[net] ^= 1;
@@ -929,8 +962,9 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     const std::string k(key);
     if (k == "fwd_bf16x6") p->fwd_bf16x6 = value ? 1 : 0;
     else if (k == "contract_bf16x6") p->contract_bf16x6 = value ? 1 : 0;
+    else if (k == "bwd_bf16x6") p->bwd_bf16x6 = value ? 1 : 0;
     else if (k == "graph") p->graph_on = value ? 1 : 0;
-    else return fail("unknown plan option '" + k + "' (fwd_bf16x6, contract_bf16x6, graph)");
+    else return fail("unknown plan option '" + k + "' (fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph)");
     // captured graphs embed the kernel choice
     for (auto& g : p->graphs) (void)hipGraphExecDestroy(g.second);
     p->graphs.clear();
