@@ -12,8 +12,8 @@
 // MFMAs (32 cycles each) per 32-long k-block: 2.7x fewer matrix-core cycles. The 4-long k tail
 // (features 96..99) is one exact 16x16x4 f32 MFMA.
 //
-// Workgroup = 4 S waves + 4 D waves (one of each per SIMD, 1 workgroup per CU, 256 VGPRs a wave) for
-// 128 owner (trunk) rows; the branch rows stream through LDS in 32-row chunks:
+// Workgroup = 8 S waves + 8 D waves (4 waves per SIMD, 1 workgroup per CU, <= 128 VGPRs a wave) for
+// 128 owner (trunk) rows, 16 per wave pair; the branch rows stream through LDS in 32-row chunks:
 //   Q image  (3 rotating buffers): the chunk's three bf16 planes, row-major [32 q][112 j], 224-B rows,
 //            plus the fp32 tail [32 q][4]. S waves read it by rows (ds_read_b128, the A operand of
 //            S = Q Own^T); D waves read it by columns (ds_read_b64_tr_b16, the B operand of G^T Q).
@@ -23,20 +23,16 @@
 //            linear. The D role's k order is chosen so that its A operand IS that register layout:
 //            lane (lr, lg) element jj <-> branch row 4lg + jj (jj < 4) or 16 + 4lg + jj - 4 (jj >= 4),
 //            and the two transposed reads fetch exactly those rows.
-//   S wave w: 32 owner rows, their three planes in registers (72 VGPRs) as the B operand; per chunk two
+//   S wave w: 16 owner rows, their three planes in registers (36 VGPRs) as the B operand; per chunk two
 //             16-row S tiles, G = gscale (S + b0 - y), likelihood sums, G^T stores for side B.
-//   D wave w: one chunk behind: splits G, dOwn[32 rows][112] += G^T Q over the chunk's 32 rows.
+//   D wave w: one chunk behind: splits G, dOwn[16 rows][112] += G^T Q over the chunk's 32 rows.
+// Likelihood sums: 2 doubles per S wave at stats[(qc * o_tiles + og) * 8 + w].
 #include "vihmc_internal.h"
 #include "vihmc_bf16x6.h"
 
 #ifndef CB_ABL
-#define CB_ABL 0        // timing-only ablations: 1 no G^T stores, 2 no D MFMAs, 3 no S MFMAs (wrong results)
-#endif
-#ifndef CB_YBUF
-#define CB_YBUF 1
-#endif
-#ifndef CB_GBUF
-#define CB_GBUF 1
+#define CB_ABL 0        // timing-only ablations: 1 no G^T stores, 2 no D MFMAs, 3 no S MFMAs, 4 G^T stores to
+                        // contiguous addresses (wrong results)
 #endif
 
 namespace vihmc {
@@ -62,13 +58,13 @@ constexpr int CB_TAIL = 3 * CB_PLANE;              // fp32 [32][4] tail image of
 constexpr int CB_BLOCK = CONTRACT_SPLIT_BLOCK;     // 22528: 3 planes + tail, padded to 22 KB
 static_assert(CB_TAIL + CB_QC * 16 <= CB_BLOCK && CB_BLOCK % 1024 == 0, "split block layout");
 constexpr int CB_QIMG = CB_BLOCK;                  // bytes per Q buffer (one pre-split block)
-constexpr int CB_GIMG = 4 * 4 * 64 * 16;           // 4 S waves x 4 f32x4 x 64 lanes = 16384
+constexpr int CB_GIMG = 8 * 2 * 64 * 16;           // 8 S waves x 2 f32x4 x 64 lanes = 16384
 constexpr int CB_LDS = 3 * CB_QIMG + 2 * CB_GIMG;  // 98816
 constexpr int CB_GLDS = CB_BLOCK / 1024;           // 22 wave-wide 16-B-per-lane DMA copies per block
 
 }  // namespace
 
-__global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
+__global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smc[];
     int b = blockIdx.x;
     const int per_chain = P.o_tiles * P.q_chunks;
@@ -77,9 +73,8 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
     const int qc = b / P.o_tiles;
     const int og = b - qc * P.o_tiles;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-    const int w = wave & 3;
-    const float* Q = P.Q + c * P.q_cs;
-    const int o0 = og * CONTRACT_OWN_PER_WG + w * 32;
+    const int w = wave & 7;                            // S wave w and D wave w share owner rows o0 .. o0+15
+    const int o0 = og * CONTRACT_OWN_PER_WG + w * 16;
     const int q_lo = qc * P.q_per_chunk;
     const int q_hi = min(q_lo + P.q_per_chunk, P.Mq);
     const int nchunks = q_hi > q_lo ? (q_hi - q_lo + CB_QC - 1) / CB_QC : 0;
@@ -88,24 +83,23 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
     // with wave-wide DMA (global_load_lds_dwordx4: 1 KB per instruction, no VGPRs, no VALU)
     const unsigned char* qblk = P.qimg + c * P.qimg_cs + (int64_t)(q_lo / CB_QC) * CB_BLOCK;
 #define VIHMC_CB_GLDS(CI, BUF)                                                                              \
-    for (int k = wave - 4; k < CB_GLDS; k += 4)                                                             \
+    for (int k = wave - 8; k < CB_GLDS; k += 8)                                                             \
         __builtin_amdgcn_global_load_lds(                                                                   \
             reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
             (__attribute__((address_space(3))) void*)(smc + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
-    if (wave >= 4 && nchunks > 0) {
+    if (wave >= 8 && nchunks > 0) {
         VIHMC_CB_GLDS(0, 0)
     }
 
-    if (wave < 4) {
+    if (wave < 8) {
         // ---------------- S role ----------------
         const float* Own = P.Own + c * P.own_cs;
         const float* Yc = P.Y + c * P.y_cs;
         const float b0 = P.b0[c * P.b0_cs];
-        bf16x8 ob[2][3][3];     // [s][kb][plane]: Own[o0 + 16s + lr][32kb + 8lg + j]
-        float otl[2];           // Own[o0 + 16s + lr][96 + lg]
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const float* orow = Own + (int64_t)min(o0 + 16 * s + lr, P.Mo - 1) * P.ldown;
+        bf16x8 ob[3][3];        // [kb][plane]: Own[o0 + lr][32kb + 8lg + j]
+        float otl;              // Own[o0 + lr][96 + lg]
+        {
+            const float* orow = Own + (int64_t)min(o0 + lr, P.Mo - 1) * P.ldown;
 #pragma unroll
             for (int kb = 0; kb < 3; ++kb) {
                 const f32x4 x0 = *reinterpret_cast<const f32x4*>(orow + 32 * kb + 8 * lg);
@@ -113,41 +107,36 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
                 bf16x4 a0, a1, a2, c0, c1, c2;
                 split4(x0, a0, a1, a2);
                 split4(x1, c0, c1, c2);
-                ob[s][kb][0] = cat8(a0, c0);
-                ob[s][kb][1] = cat8(a1, c1);
-                ob[s][kb][2] = cat8(a2, c2);
+                ob[kb][0] = cat8(a0, c0);
+                ob[kb][1] = cat8(a1, c1);
+                ob[kb][2] = cat8(a2, c2);
             }
-            otl[s] = orow[96 + lg];
+            otl = orow[96 + lg];
         }
         double ssq = 0.0, gsum = 0.0;
         // targets and G^T through buffer resources: 32-bit offsets, rows past the end read 0 and owner
         // rows past Mo are dropped by the hardware range check (no exec-mask branches per element)
         const __amdgpu_buffer_rsrc_t yrs = make_rsrc_c(Yc, (uint32_t)((int64_t)P.Mq * P.ldy * 4));
-        const __amdgpu_buffer_rsrc_t grs =
-            make_rsrc_c(P.gout ? P.gout + c * P.gout_cs : P.Y, P.gout ? (uint32_t)((int64_t)P.Mo * P.ldg * 4) : 0u);
-        bool ovalid[2];
-        uint32_t yoff[2], goff[2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int oo = o0 + 16 * s + lr;
-            ovalid[s] = oo < P.Mo;
-            yoff[s] = (uint32_t)((4 * lg) * P.ldy + min(oo, P.Mo - 1)) * 4u;
-            goff[s] = ovalid[s] ? (uint32_t)(oo * P.ldg + q_lo + 4 * lg) * 4u : OOB_C;
-        }
+        // G^T exchange buffer, chunk-blocked: element (o, q) at ((q / 32) * ldg + o) * 32 + q % 32 (ldg = Mo
+        // rows per block) -- one chunk of one workgroup is 128 rows x 128 B, contiguous
+        const __amdgpu_buffer_rsrc_t grs = make_rsrc_c(
+            P.gout ? P.gout + c * P.gout_cs : P.Y,
+            P.gout ? (uint32_t)((int64_t)((P.Mq + CB_QC - 1) / CB_QC) * P.ldg * CB_QC * 4) : 0u);
+        const int oo = o0 + lr;
+        const bool ovalid = oo < P.Mo;
+        const uint32_t yoff = (uint32_t)((4 * lg) * P.ldy + min(oo, P.Mo - 1)) * 4u;
+        const uint32_t goff = ovalid ? (uint32_t)(((q_lo / CB_QC) * P.ldg + oo) * CB_QC + 4 * lg) * 4u : OOB_C;
         const uint32_t ystep = (uint32_t)P.ldy * 4u;
-        // targets [sub][s][r] one chunk ahead in two register sets used alternately (the loop is unrolled
-        // by two), so no register copy forces a wait on the newest loads and the G^T stores
-        float ya[2][2][4], yb[2][2][4];
+        // targets [sub][r] one chunk ahead in two register sets used alternately (the loop is unrolled by
+        // two), so no register copy forces a wait on the newest loads and the G^T stores
+        float ya[2][4], yb[2][4];
 #define VIHMC_CB_YLOAD(YN, CI)                                                                           \
         _Pragma("unroll") for (int sub = 0; sub < 2; ++sub)                                              \
-            _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                \
-                _Pragma("unroll") for (int r = 0; r < 4; ++r)                                            \
-                    YN[sub][s][r] = CB_YBUF ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32( \
-                        yrs, yoff[s], (uint32_t)(q_lo + (CI) * CB_QC + 16 * sub + r) * ystep, 0))             \
-                        : Yc[(int64_t)min(q_lo + (CI) * CB_QC + 16 * sub + 4 * lg + r, P.Mq - 1) * P.ldy +    \
-                             min(o0 + 16 * s + lr, P.Mo - 1)];
+            _Pragma("unroll") for (int r = 0; r < 4; ++r)                                                \
+                YN[sub][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(              \
+                    yrs, yoff, (uint32_t)(q_lo + (CI) * CB_QC + 16 * sub + r) * ystep, 0));
         VIHMC_CB_YLOAD(ya, 0)
-        auto s_chunk = [&](int i, float (&yv)[2][2][4], float (&yn)[2][2][4]) __attribute__((always_inline)) {
+        auto s_chunk = [&](int i, float (&yv)[2][4], float (&yn)[2][4]) __attribute__((always_inline)) {
             if (i > nchunks) return;                // same barrier count as the D role
             __syncthreads();
             if (i < nchunks) {
@@ -155,83 +144,57 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
                 const bool full = q0 + CB_QC <= q_hi;
                 const unsigned char* img = smc + (i % 3) * CB_QIMG;
                 VIHMC_CB_YLOAD(yn, min(i + 1, nchunks - 1))
-                f32x4* gdst = reinterpret_cast<f32x4*>(smc + 3 * CB_QIMG + (i & 1) * CB_GIMG) + w * 256;
+                f32x4* gdst = reinterpret_cast<f32x4*>(smc + 3 * CB_QIMG + (i & 1) * CB_GIMG) + w * 128;
                 float ps = 0.f;
 #pragma unroll
                 for (int sub = 0; sub < 2; ++sub) {
                     const unsigned char* row = img + (16 * sub + lr) * CB_PITCH + 16 * lg;
-                    f32x4 sacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+                    const float qt = reinterpret_cast<const float*>(img + CB_TAIL)[(16 * sub + lr) * 4 + lg];
+                    // the exact f32 tail (features 96..99) seeds the accumulator
+                    f32x4 sacc = CB_ABL != 3 ? __builtin_amdgcn_mfma_f32_16x16x4f32(qt, otl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0)
+                                             : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int kb = 0; kb < 3; ++kb) {
                         bf16x8 qa[3];
 #pragma unroll
                         for (int p = 0; p < 3; ++p)
                             qa[p] = *reinterpret_cast<const bf16x8*>(row + p * CB_PLANE + 64 * kb);
-                        if (CB_ABL != 3) {
-                            sacc[0] = six(qa, ob[0][kb], sacc[0]);
-                            sacc[1] = six(qa, ob[1][kb], sacc[1]);
-                        }
+                        if (CB_ABL != 3) sacc = six(qa, ob[kb], sacc);
                     }
-                    const float qt = reinterpret_cast<const float*>(img + CB_TAIL)[(16 * sub + lr) * 4 + lg];
-                    f32x4 tacc[2];
+                    f32x4 g;
 #pragma unroll
-                    for (int s = 0; s < 2; ++s)
-                        tacc[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(qt, otl[s], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                    f32x4 g[2];
-#pragma unroll
-                    for (int s = 0; s < 2; ++s)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int qq = q0 + 16 * sub + 4 * lg + r;
-                            const bool ok = ovalid[s] && (full || qq < q_hi);
-                            float rv = (sacc[s][r] + tacc[s][r]) + b0 - yv[sub][s][r];
-                            rv = ok ? rv : 0.f;
-                            g[s][r] = P.gscale * rv;
-                            ps = fmaf(rv, rv, ps);
-                            gsum += (double)g[s][r];  // G terms cancel: exact-order fp64, not fp32 partials
-                        }
-                    gdst[(2 * sub + 0) * 64 + lane] = g[0];
-                    gdst[(2 * sub + 1) * 64 + lane] = g[1];
-                    if (P.gout && !CB_GBUF) {
-                        float* gw = P.gout + c * P.gout_cs;
-                        const int qq = q0 + 16 * sub + 4 * lg;
-#pragma unroll
-                        for (int s = 0; s < 2; ++s) {
-                            const int oo = o0 + 16 * s + lr;
-                            if (oo >= P.Mo) continue;
-                            float* dst = gw + (int64_t)oo * P.ldg + qq;
-                            if (qq + 3 < q_hi) {
-                                *reinterpret_cast<f32x4*>(dst) = g[s];
-                            } else {
-#pragma unroll
-                                for (int r = 0; r < 4; ++r)
-                                    if (qq + r < q_hi) dst[r] = g[s][r];
-                            }
-                        }
+                    for (int r = 0; r < 4; ++r) {
+                        const int qq = q0 + 16 * sub + 4 * lg + r;
+                        const bool ok = ovalid && (full || qq < q_hi);
+                        float rv = sacc[r] + b0 - yv[sub][r];
+                        rv = ok ? rv : 0.f;
+                        g[r] = P.gscale * rv;
+                        ps = fmaf(rv, rv, ps);
+                        gsum += (double)g[r];  // G terms cancel: exact-order fp64, not fp32 partials
                     }
-                    if (P.gout && CB_GBUF && CB_ABL != 1) {
-                        const uint32_t qofs = (uint32_t)(q0 - q_lo + 16 * sub) * 4u;
-                        if (full) {
-#pragma unroll
-                            for (int s = 0; s < 2; ++s)
-                                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, g[s]), grs,
-                                                                       goff[s] + qofs, 0, 0);
+                    gdst[sub * 64 + lane] = g;
+                    if (P.gout && CB_ABL != 1) {
+                        const uint32_t qofs = (uint32_t)i * (uint32_t)P.ldg * (CB_QC * 4u) + 64u * sub;
+                        if (CB_ABL == 4) {
+                            // timing only: the same bytes to contiguous 1 KB pieces (wrong layout)
+                            const uint32_t cofs = (uint32_t)(((og * 8 + w) * (nchunks + 1) + i) * 2 + sub) * 1024u;
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, g), grs, cofs + lane * 16, 0, 0);
+                        } else if (full) {
+                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, g), grs, goff + qofs, 0, 0);
                         } else {
                             const int qq = q0 + 16 * sub + 4 * lg;
 #pragma unroll
-                            for (int s = 0; s < 2; ++s)
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) {
-                                    // copy the element out first: __builtin_bit_cast of an ext-vector
-                                    // element subscript compiled to element 0 for every r (hipcc, ROCm 7.2)
-                                    const float gv = g[s][r];
-                                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs,
-                                        qq + r < q_hi ? goff[s] + qofs + 4u * r : OOB_C, 0, 0);
-                                }
+                            for (int r = 0; r < 4; ++r) {
+                                // copy the element out first: __builtin_bit_cast of an ext-vector element
+                                // subscript compiled to element 0 for every r (hipcc, ROCm 7.2)
+                                const float gv = g[r];
+                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs,
+                                    qq + r < q_hi ? goff + qofs + 4u * r : OOB_C, 0, 0);
+                            }
                         }
                     }
                 }
-                // sum r^2 (no cancellation): per-chunk fp32 partial of 16 terms per lane, then fp64
+                // sum r^2 (no cancellation): per-chunk fp32 partial of 8 terms per lane, then fp64
                 ssq += (double)ps;
             }
         };
@@ -246,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
                 gsum += __shfl_xor(gsum, o, 64);
             }
             if (lane == 0) {
-                double* st = P.stats + c * P.stats_cs + 2 * (int64_t)((qc * P.o_tiles + og) * 4 + w);
+                double* st = P.stats + c * P.stats_cs + 2 * (int64_t)((qc * P.o_tiles + og) * 8 + w);
                 st[0] = ssq;
                 st[1] = gsum;
             }
@@ -255,14 +218,10 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
     }
 
     // ---------------- D role ----------------
-    f32x4 dacc[2][7];
+    f32x4 dacc[7];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int t = 0; t < 7; ++t) dacc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // transposed-read lane address: group lg reads rows 4lg .. 4lg+3 (and 16 + those), lane 4qq+pp
-    // supplies row 4lg + qq, features 16t + 4pp .. +3
-    const int tr_off = (4 * lg + (lr >> 2)) * CB_PITCH + 8 * (lr & 3);
+    for (int t = 0; t < 7; ++t) dacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int tro = bf6::tr_lane_off(lr, lg);
     for (int i = 0; i <= nchunks; ++i) {
         __syncthreads();
         // chunk i+1 -> buffer (i+1)%3 (last read by this role in iteration i-1, by S in i-2); the copies
@@ -272,47 +231,36 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf(ContractProb P) {
         }
         if (i >= 1) {
             const unsigned char* img = smc + ((i - 1) % 3) * CB_QIMG;
-            const f32x4* gsrc = reinterpret_cast<const f32x4*>(smc + 3 * CB_QIMG + ((i - 1) & 1) * CB_GIMG) + w * 256;
-            bf16x8 ga[2][3];
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
+            const f32x4* gsrc = reinterpret_cast<const f32x4*>(smc + 3 * CB_QIMG + ((i - 1) & 1) * CB_GIMG) + w * 128;
+            bf16x8 ga[3];
+            {
                 bf16x4 l0, l1, l2, h0, h1, h2;
-                split4(gsrc[s * 64 + lane], l0, l1, l2);          // sub 0
-                split4(gsrc[(2 + s) * 64 + lane], h0, h1, h2);    // sub 1
-                ga[s][0] = cat8(l0, h0);
-                ga[s][1] = cat8(l1, h1);
-                ga[s][2] = cat8(l2, h2);
+                split4(gsrc[lane], l0, l1, l2);          // sub 0
+                split4(gsrc[64 + lane], h0, h1, h2);     // sub 1
+                ga[0] = cat8(l0, h0);
+                ga[1] = cat8(l1, h1);
+                ga[2] = cat8(l2, h2);
             }
 #pragma unroll
             for (int t = 0; t < 7; ++t) {
                 bf16x8 qb[3];
 #pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    const unsigned char* a = img + p * CB_PLANE + tr_off + 32 * t;
-                    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));
-                    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 16 * CB_PITCH));
-                    qb[p] = cat8(lo, hi);
-                }
-                if (CB_ABL != 2) {
-                    dacc[0][t] = six(ga[0], qb, dacc[0][t]);
-                    dacc[1][t] = six(ga[1], qb, dacc[1][t]);
-                }
+                for (int p = 0; p < 3; ++p) qb[p] = bf6::tr_frag(img + p * CB_PLANE, tro, 16 * t);
+                if (CB_ABL != 2) dacc[t] = six(ga, qb, dacc[t]);
             }
         }
     }
     float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int t = 0; t < 7; ++t) {
+        const int j = 16 * t + lr;
+        if (j >= P.ldout) continue;
 #pragma unroll
-        for (int t = 0; t < 7; ++t) {
-            const int j = 16 * t + lr;
-            if (j >= P.ldout) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int oo = o0 + 16 * s + 4 * lg + r;
-                if (oo < P.Mo) out[(int64_t)oo * P.ldout + j] = (j < 100) ? dacc[s][t][r] : 0.f;
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int oo = o0 + 4 * lg + r;
+            if (oo < P.Mo) out[(int64_t)oo * P.ldout + j] = (j < 100) ? dacc[t][r] : 0.f;
         }
+    }
 #undef VIHMC_CB_GLDS
 #undef VIHMC_CB_YLOAD
 }
@@ -348,8 +296,8 @@ hipError_t launch_split_blocks(const float* src, int64_t src_cs, int ld, int row
 
 
 // =============================================================================================
-// Side B (load-G), bf16x6: dOwn[o][j] += sum_q G[q][o] Q[q][j] with G read from side A's G^T (P.Y,
-// [q][o] with ldy) and Q = the trunk outputs pre-split into blocks. No S role: all 8 waves are alike,
+// Side B (load-G), bf16x6: dOwn[o][j] += sum_q G[q][o] Q[q][j] with G read from side A's chunk-blocked
+// G^T (P.Y) and Q = the trunk outputs pre-split into blocks. No S role: all 8 waves are alike,
 // 32 owner (branch) rows each (256 per workgroup); per 32-row chunk each wave loads its G (one chunk
 // ahead, two register sets), splits it into the A operand (same k order as the side-A D role) and runs
 // 7 column tiles x 2 row tiles x 6 products against transposed reads of the shared chunk image.
@@ -385,11 +333,14 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
     // buffer loads with the whole offset in the range-checked VGPR: rows past Mq read 0, rows past q_hi
     // (another workgroup's range, only in a partial last chunk) are sent out of range
     const float* Gc = P.Y + c * P.y_cs;
-    const __amdgpu_buffer_rsrc_t grs = make_rsrc_c(Gc, (uint32_t)((int64_t)P.Mq * P.ldy * 4));
+    // chunk-blocked G^T (see k_contract_bf): element (q, o) at ((o / 32) * ldy + q) * 32 + o % 32 with
+    // ldy = Mq rows per block; this wave's 32 owner rows are one block
+    const __amdgpu_buffer_rsrc_t grs =
+        make_rsrc_c(Gc, (uint32_t)((int64_t)((P.Mo + CB_QC - 1) / CB_QC) * P.ldy * CB_QC * 4));
     uint32_t gcol[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) gcol[s] = (uint32_t)min(o0 + 16 * s + lr, P.Mo - 1) * 4u;
-    const uint32_t ystep = (uint32_t)P.ldy * 4u;
+    for (int s = 0; s < 2; ++s) gcol[s] = (uint32_t)(((o0 / CB_QC) * P.ldy) * CB_QC + 16 * s + lr) * 4u;
+    const uint32_t ystep = CB_QC * 4u;
     float ga_[2][8], gb_[2][8];
 #define VIHMC_CBB_GLOAD(GN, CI)                                                                             \
     {                                                                                                       \
@@ -474,7 +425,7 @@ hipError_t launch_contract_bf_b(const ContractProb& p, int C, hipStream_t s) {
 
 hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s) {
     if (p.W != 100 || p.load_g || !p.qimg || p.q_per_chunk % CB_QC) return hipErrorInvalidValue;
-    dim3 g(C * p.o_tiles * p.q_chunks), blk(512);
+    dim3 g(C * p.o_tiles * p.q_chunks), blk(1024);
     hipLaunchKernelGGL(k_contract_bf, g, blk, CB_LDS, s, p);
     return hipGetLastError();
 }

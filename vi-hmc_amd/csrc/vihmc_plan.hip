@@ -89,8 +89,10 @@ struct vihmc_plan {
     float* gp = nullptr;
     int64_t dp = 0;
     float* y = nullptr;
-    float* gT = nullptr;        // per chain G^T [P][N] (side A -> side B); gT_cs floats per chain
+    float* gT = nullptr;        // per chain G^T [P][ldgT] (side A -> side B); gT_cs floats per chain
     int64_t gT_cs = 0;
+    int ldgT = 0;               // N rounded up to 32 floats: every row starts on a 128-B line; the bf16x6
+                                // kernels use the same bytes chunk-blocked ([N/32][P][32])
     unsigned char* qsplitA = nullptr;   // per chain: branch outputs pre-split for k_contract_bf (W = 100)
     int64_t qsplitA_cs = 0;             // bytes per chain
     unsigned char* qsplitB = nullptr;   // per chain: trunk outputs pre-split for k_contract_bf_b
@@ -323,7 +325,8 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     }
     const int64_t NP = (int64_t)p->N * p->P;
     if (int rc = p->upload(&p->y, y, NP)) return rc;
-    p->gT_cs = r64(NP);
+    p->ldgT = (int)((p->N + 31) / 32 * 32);
+    p->gT_cs = r64((int64_t)p->P * p->ldgT);
     if (int rc = p->alloc(&p->gT, p->gT_cs * C)) return rc;
     if (p->W == 100) {
         p->qsplitA_cs = (int64_t)cdiv(p->N, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
@@ -397,7 +400,8 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         p->qchunksB = cdiv(p->P, p->qperB);
         p->partB_cs = r64((int64_t)p->qchunksB * p->N * p->ldz);
         if (int rc = p->alloc(&p->partB, p->partB_cs * C)) return rc;
-        p->nwavesA = p->qchunksA * og_a * 4;
+        p->nwavesA = p->qchunksA * og_a * 8;   // stats slots: 8 S waves per workgroup (k_contract_bf;
+                                               // the fp32 kernels fill 4 of them)
         p->stats_cs = 2 * (int64_t)p->nwavesA;
         if (int rc = p->alloc(&p->stats, p->stats_cs * C)) return rc;
         if (int rc = p->alloc(&p->lik_buf, C)) return rc;
@@ -590,7 +594,7 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
         q.out_chunk_stride = p->qchunksA > 1 ? (int64_t)p->P * p->ldz : 0;
         q.gout = p->gT;
         q.gout_cs = p->gT_cs;
-        q.ldg = p->N;
+        q.ldg = p->contract_bf16x6 && p->W == 100 ? p->P : p->ldgT;   // bf16x6: chunk-blocked rows
     } else {
         q.out = out ? out : p->lik_buf;   // dummy when not writing S
         q.out_cs = out ? (int64_t)p->N * p->P : 0;
@@ -620,8 +624,10 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
     HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s));
     if (int rc = deeponet_forward_layers(p, C, s)) return rc;
     const bool want_grad = grad != nullptr && out == nullptr;
+    int stats_waves = 0;
     {
         ContractProb a = side_a(p, C, want_grad, out);
+        stats_waves = p->qchunksA * cdiv(p->P, CONTRACT_OWN_PER_WG) * (a.bf16x6 ? 8 : 4);
         if (a.bf16x6)
             HIPCHK(launch_split_blocks(a.Q, a.q_cs, a.ldq, p->N, p->qsplitA, p->qsplitA_cs, C, s));
         hipEvent_t stop = nullptr;
@@ -629,7 +635,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         HIPCHK(launch_contract(a, C, want_grad, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
     }
-    HIPCHK(launch_contract_stats(p->stats, p->stats_cs, p->nwavesA, C, p->lik_buf, p->gp, p->dp,
+    HIPCHK(launch_contract_stats(p->stats, p->stats_cs, stats_waves, C, p->lik_buf, p->gp, p->dp,
                                  (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out, s));
     if (want_grad) {
         Net& b = p->nets[0];
@@ -642,7 +648,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         q.q_cs = t.act_cs;
         q.ldq = p->ldz;
         q.Y = p->gT;           // G^T written by side A: no S recompute on this side
-        q.ldy = p->N;
+        q.ldy = p->contract_bf16x6 && p->W == 100 ? p->P : p->ldgT;
         q.y_cs = p->gT_cs;
         q.load_g = 1;
         q.bf16x6 = p->W == 100 ? p->contract_bf16x6 : 0;
