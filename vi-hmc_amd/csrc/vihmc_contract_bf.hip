@@ -31,8 +31,7 @@
 #include "vihmc_bf16x6.h"
 
 #ifndef CB_ABL
-#define CB_ABL 0        // timing-only ablations: 1 no G^T stores, 2 no D MFMAs, 3 no S MFMAs, 4 G^T stores to
-                        // contiguous addresses (wrong results)
+#define CB_ABL 0        // timing-only ablations: 1 no G^T stores, 2 no D MFMAs, 3 no S MFMAs (wrong results)
 #endif
 
 namespace vihmc {
@@ -125,7 +124,11 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
         const int oo = o0 + lr;
         const bool ovalid = oo < P.Mo;
         const uint32_t yoff = (uint32_t)((4 * lg) * P.ldy + min(oo, P.Mo - 1)) * 4u;
-        const uint32_t goff = ovalid ? (uint32_t)(((q_lo / CB_QC) * P.ldg + oo) * CB_QC + 4 * lg) * 4u : OOB_C;
+        // G^T store offsets (see the stores): rows o0 + (lr & 7) and o0 + 8 + (lr & 7), q half by lr >= 8
+        const int gxr = o0 + (lr & 7), gyr = gxr + 8;
+        const int gq = (lr < 8 ? 0 : 16) + 4 * lg;
+        const uint32_t gx_off = gxr < P.Mo ? (uint32_t)(((q_lo / CB_QC) * P.ldg + gxr) * CB_QC + gq) * 4u : OOB_C;
+        const uint32_t gy_off = gyr < P.Mo ? (uint32_t)(((q_lo / CB_QC) * P.ldg + gyr) * CB_QC + gq) * 4u : OOB_C;
         const uint32_t ystep = (uint32_t)P.ldy * 4u;
         // targets [sub][r] one chunk ahead in two register sets used alternately (the loop is unrolled by
         // two), so no register copy forces a wait on the newest loads and the G^T stores
@@ -146,6 +149,7 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
                 VIHMC_CB_YLOAD(yn, min(i + 1, nchunks - 1))
                 f32x4* gdst = reinterpret_cast<f32x4*>(smc + 3 * CB_QIMG + (i & 1) * CB_GIMG) + w * 128;
                 float ps = 0.f;
+                f32x4 gs[2];
 #pragma unroll
                 for (int sub = 0; sub < 2; ++sub) {
                     const unsigned char* row = img + (16 * sub + lr) * CB_PITCH + 16 * lg;
@@ -173,24 +177,36 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
                         gsum += (double)g[r];  // G terms cancel: exact-order fp64, not fp32 partials
                     }
                     gdst[sub * 64 + lane] = g;
-                    if (P.gout && CB_ABL != 1) {
-                        const uint32_t qofs = (uint32_t)i * (uint32_t)P.ldg * (CB_QC * 4u) + 64u * sub;
-                        if (CB_ABL == 4) {
-                            // timing only: the same bytes to contiguous 1 KB pieces (wrong layout)
-                            const uint32_t cofs = (uint32_t)(((og * 8 + w) * (nchunks + 1) + i) * 2 + sub) * 1024u;
-                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, g), grs, cofs + lane * 16, 0, 0);
-                        } else if (full) {
-                            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, g), grs, goff + qofs, 0, 0);
-                        } else {
-                            const int qq = q0 + 16 * sub + 4 * lg;
+                    gs[sub] = g;
+                }
+                if (P.gout && CB_ABL != 1) {
+                    // Whole 128-B lines per store: lanes lr and lr ^ 8 swap halves (DPP row_ror:8), so
+                    // store X covers rows o0 + (lr & 7) and store Y rows o0 + 8 + (lr & 7), each row's 32
+                    // q values from 8 lanes (sub 0 from lr < 8, sub 1 from lr >= 8): 1 KB contiguous.
+                    const bool lo = lr < 8;
+                    f32x4 recv;
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                // copy the element out first: __builtin_bit_cast of an ext-vector element
-                                // subscript compiled to element 0 for every r (hipcc, ROCm 7.2)
-                                const float gv = g[r];
-                                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), grs,
-                                    qq + r < q_hi ? goff + qofs + 4u * r : OOB_C, 0, 0);
-                            }
+                    for (int r = 0; r < 4; ++r) {
+                        const float sv = lo ? gs[1][r] : gs[0][r];
+                        recv[r] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(sv), 0x128, 0xF, 0xF, false));
+                    }
+                    const f32x4 X = lo ? gs[0] : recv;
+                    const f32x4 Y = lo ? recv : gs[1];
+                    const uint32_t cofs = (uint32_t)i * (uint32_t)P.ldg * (CB_QC * 4u);
+                    if (full) {
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, X), grs, gx_off + cofs, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, Y), grs, gy_off + cofs, 0, 0);
+                    } else {
+                        const int qq = q0 + (lo ? 0 : 16) + 4 * lg;
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            // copy the element out first: __builtin_bit_cast of an ext-vector element
+                            // subscript compiled to element 0 for every r (hipcc, ROCm 7.2)
+                            const float xv = X[r], yv2 = Y[r];
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xv), grs,
+                                qq + r < q_hi ? gx_off + cofs + 4u * r : OOB_C, 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yv2), grs,
+                                qq + r < q_hi ? gy_off + cofs + 4u * r : OOB_C, 0, 0);
                         }
                     }
                 }
