@@ -27,6 +27,8 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "leapfrog-steps/sec/GPU (grad evals/sec) + ESS/sec, DeepONet VI-HMC"
 FP32_PEAK_TFLOPS = 157.3        # MI355X_MICROARCH.md: dense fp32 (vector = MFMA rate)
+BF16_PEAK_TFLOPS = 2516.6       # MI355X_MICROARCH.md "~2.5 PF dense": 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz
+BF16X6_PRODUCTS = 6             # fp32 operand = 3 exact bf16 planes; the 6 products of order <= 2 are kept
 HBM_PEAK_GBS = 8000.0
 
 
@@ -194,12 +196,18 @@ def main():
     avg_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = flops_contract / avg_s / 1e12 if k_n else None
     evals_per_s = world * grad_evals / T
+    bf = eng.get_option("contract_bf16x6")
+    # bf16x6: each fp32 product costs 6 bf16 MFMA products, so the fp32-equivalent ceiling of the kernel is
+    # the bf16 dense peak / 6 (= 419.4 TFLOP/s); the fp32 MFMA path is priced against the fp32 peak
+    peak = BF16_PEAK_TFLOPS / BF16X6_PRODUCTS if bf else FP32_PEAK_TFLOPS
+    kname = ("k_contract_bf: side-A contraction on the bf16 MFMA, bf16x6 fp32 emulation" if bf else
+             "k_contract_ws: side-A contraction on the fp32 MFMA")
     traffic = None
     tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic_contract.json")
     if os.path.exists(tpath):
         with open(tpath) as f:
             tj = json.load(f)
-        if tj.get("chains_per_gpu") == C:
+        if tj.get("chains_per_gpu") == C and tj.get("contract_bf16x6", 0) == bf:
             traffic = tj["hbm_bytes_per_launch"]     # PMC-measured bytes per side-A launch (same config)
     line = {
         "metric": METRIC,
@@ -213,6 +221,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
+        "mfma_form": {k: eng.get_option(k) for k in ("fwd_bf16x6", "contract_bf16x6", "bwd_bf16x6")},
         "data": "synthetic (Burgers shapes, seeded teacher DeepONet; the .mat is not shipped)",
         "config": {"workload": "DeepONet VI-HMC Burgers, config 5 per-GPU share", "N": prob.N, "P": prob.P,
                    "D": spec.n_params, "K": prob.K, "chains_per_gpu": C, "global_chains": world * C, "L": args.L,
@@ -221,9 +230,12 @@ def main():
         "hamiltorch_equiv_grad_evals_per_s": world * C * (args.L + 1) * args.steps / T,
         "eval_tflops_algorithmic": evals_per_s * spec.flops_per_grad_eval(prob.N, prob.P) / 1e12,
         "accept_rate": acc_rate,
-        "roofline": {"kernel": "k_contract_ws: side-A contraction (branch x trunk S, Gaussian NLL, G, dZ_trunk)",
-                     "bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None, "traffic": traffic,
+        "roofline": {"kernel": kname + " (branch x trunk S, Gaussian NLL, G, dZ_trunk)",
+                     "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "frac": (achieved / peak) if achieved else None, "traffic": traffic,
+                     "peak_basis": ("fp32-equivalent: bf16 dense MFMA peak 2516.6 / 6 bf16 products per fp32 product"
+                                    if bf else "fp32 MFMA dense peak"),
+                     "achieved_vs_fp32_mfma_peak": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
                      "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE; profiles/traffic_contract.json)",
                      "avg_launch_ms": avg_s * 1e3, "launches": k_n,
                      "flops_per_launch": flops_contract},

@@ -145,6 +145,9 @@ int vihmc_graph_enable(vihmc_plan* p, int on);
  * row chunks at plan creation. "graph" = vihmc_graph_enable. Changing an option drops captured graphs.
  * Returns nonzero for an unknown key. */
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value);
+/* Current value of an option (contract_bf16x6 reads 1 only where the bf16x6 contraction applies,
+ * i.e. width 100; graph reads -1 while it follows VIHMC_GRAPH). */
+int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value);
 
 void        vihmc_plan_destroy(vihmc_plan* p);
 const char* vihmc_last_error(void);

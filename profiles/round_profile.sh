@@ -14,3 +14,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T
 B="$B --ess-steps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/${TAG}_fetch -o p -- $B > $O/${TAG}_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $O/${TAG}_write -o p -- $B > $O/${TAG}_write.log 2>&1
+python3 $ROOT/profiles/traffic_from_pmc.py $O/${TAG}_fetch $O/${TAG}_write $O/${TAG}_traffic.json 16 > $O/${TAG}_traffic.log 2>&1
+cd $ROOT && python3 profiles/kstats.py $(ls $O/${TAG}_stats/*kernel_stats.csv | head -1) 30 > $O/${TAG}_kstats.txt 2>&1 || true

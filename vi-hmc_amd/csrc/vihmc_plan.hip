@@ -977,6 +977,17 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     return 0;
 }
 
+int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
+    if (!p || !key || !value) return fail("null argument");
+    const std::string k(key);
+    if (k == "fwd_bf16x6") *value = p->fwd_bf16x6;
+    else if (k == "contract_bf16x6") *value = p->contract_bf16x6 && p->W == 100;
+    else if (k == "bwd_bf16x6") *value = p->bwd_bf16x6;
+    else if (k == "graph") *value = p->graph_on;
+    else return fail("unknown plan option '" + k + "' (fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph)");
+    return 0;
+}
+
 int vihmc_graph_enable(vihmc_plan* p, int on) {
     if (!p) return fail("null plan");
     p->graph_on = on ? 1 : 0;

@@ -60,6 +60,7 @@ SIGNATURES = {
     "vihmc_timing_enable": (c_int, [c_void_p, c_int, c_int]),
     "vihmc_graph_enable": (c_int, [c_void_p, c_int]),
     "vihmc_plan_option": (c_int, [c_void_p, c_char_p, c_int]),
+    "vihmc_plan_get_option": (c_int, [c_void_p, c_char_p, ctypes.POINTER(c_int)]),
     "vihmc_timing_read": (c_int, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int64)]),
     "vihmc_plan_destroy": (None, [c_void_p]),
     "vihmc_last_error": (c_char_p, []),

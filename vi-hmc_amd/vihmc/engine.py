@@ -129,6 +129,13 @@ class _Engine:
         "graph"."""
         _lib.check(self.L.vihmc_plan_option(self._plan, key.encode(), int(value)), f"vihmc_plan_option({key})")
 
+    def get_option(self, key: str) -> int:
+        """vihmc_plan_get_option: the option's current value."""
+        v = ctypes.c_int()
+        _lib.check(self.L.vihmc_plan_get_option(self._plan, key.encode(), ctypes.byref(v)),
+                   f"vihmc_plan_get_option({key})")
+        return v.value
+
     def timing_read(self):
         ms, n = ctypes.c_double(), ctypes.c_int64()
         _lib.check(self.L.vihmc_timing_read(self._plan, ctypes.byref(ms), ctypes.byref(n)), "vihmc_timing_read")
