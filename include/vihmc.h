@@ -118,6 +118,18 @@ int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float
 int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* out, void* stream);
 
 /* Plan introspection: 0 = DeepONet, 1 = MLP; D; K; max_chains; device bytes owned. */
+/* Sensitivity scores of every parameter at theta (chain 0 of the plan, [K] device):
+ *   out[d] = sigma[d]^2 * mean over outputs of (d f / d theta_d)^2,  d < D, flat (named_parameters) order.
+ * DeepONet: the outputs are f[n][pts[n][k]], n < N, k < npts; pts is HOST memory [N][npts] int32 (the
+ *   trunk points each validation function samples, BurgersDataSet.__getitem__ at
+ *   Operator_network/VI/utils.py:39-41). BNN: every data row and output; pts ignored.
+ * sigma [D] device or NULL (then out = the mean squared gradient). out [D] device.
+ * Replaces eval_std_dydw + eval_jac (Operator_network/VI/sensitivity.py:62-126,
+ * Neural_network/VI/sensitivity.py:71-126; torch.func.jacrev over all D parameters). Synchronises
+ * `stream` before returning (temporaries are freed). */
+int vihmc_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, int npts, const float* sigma,
+                      float* out, void* stream);
+
 int     vihmc_plan_kind(const vihmc_plan* p);
 int64_t vihmc_plan_n_params(const vihmc_plan* p);
 int     vihmc_plan_K(const vihmc_plan* p);

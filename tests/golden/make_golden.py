@@ -265,9 +265,80 @@ def init_cases(out):
     np.savez(os.path.join(out, "init_fixtures.npz"), deeponet_16_12_3=don, bnn_10_10=bnn)
 
 
+# ------------------------------------------------------------------------------------------------
+# Sensitivity scores (Operator_network/VI/sensitivity.py, Neural_network/VI/sensitivity.py)
+# ------------------------------------------------------------------------------------------------
+def import_ref_mods(subdir: str, main: str, clash=("util", "utils", "config", "config_sens", "model",
+                                                     "my_make_func", "sensitivity")):
+    for m in clash:
+        sys.modules.pop(m, None)
+    d = os.path.join(REF, subdir)
+    sys.path.insert(0, d)
+    try:
+        mod = __import__(main)
+    finally:
+        sys.path.remove(d)
+    return mod
+
+
+def sensitivity_cases(out):
+    """eval_std_dydw of the reference (torch.func.jacrev over all D parameters, squared, mean over the
+    sampled outputs, times sigma^2) on seeded inputs. DeepONet: batch_size 1 batches (x_branch [1,1,in],
+    x_trunk [1,p,2]) as BurgersDataSet / DataLoader(batch_size=1) yield them (Operator_network/VI/utils.py:
+    27-50, config_sens.py:11); the trunk points of function n are grid rows pts[n] (stored). BNN: the
+    synthetic validation inputs of Neural_network/VI/sensitivity.py:56-57 (load_data = False)."""
+    S = import_ref_mods("Operator_network/VI", "sensitivity")
+    cases = {
+        "sens_deeponet_small": dict(width=12, in_b=7, depth=3, act="tanh", n=6, nt=5, nx=6, p=8, seed=31),
+        "sens_deeponet_relu": dict(width=10, in_b=5, depth=4, act="relu", n=5, nt=4, nx=5, p=6, seed=32),
+        "sens_deeponet_w100": dict(width=100, in_b=101, depth=4, act="tanh", n=4, nt=4, nx=5, p=10, seed=33),
+    }
+    for name, c in cases.items():
+        cfg = S.cfg
+        cfg.layer_width, cfg.in_branch, cfg.branch_depth, cfg.trunk_depth = c["width"], c["in_b"], c["depth"], c["depth"]
+        cfg.output_neurons, cfg.activation, cfg.dataset = c["width"], c["act"], "Burgers"
+        torch.manual_seed(c["seed"])
+        model = S.DeepONet(c["width"], c["in_b"], 5, c["depth"], c["depth"], c["width"], c["act"], impose_bc=True)
+        flat = torch.cat([p.detach().flatten() for p in model.parameters()]).numpy()
+        rng = np.random.default_rng(c["seed"])
+        D = flat.size
+        mu = (flat + 0.05 * rng.standard_normal(D)).astype(np.float32)
+        sd = (0.1 * np.abs(mu) + 0.01).astype(np.float32)
+        branch = rng.standard_normal((c["n"], c["in_b"])).astype(np.float32)
+        t = np.linspace(0.0, 1.0, c["nt"], dtype=np.float32)
+        x = np.linspace(0.0, 1.0, c["nx"], dtype=np.float32)
+        grid = np.stack(np.meshgrid(t, x, indexing="ij"), -1).reshape(-1, 2).astype(np.float32)
+        pts = np.stack([rng.choice(grid.shape[0], c["p"], replace=False) for _ in range(c["n"])]).astype(np.int32)
+        data = [(torch.from_numpy(branch[i]).view(1, 1, -1), torch.from_numpy(grid[pts[i]]).view(1, c["p"], 2))
+                for i in range(c["n"])]
+        scores = S.eval_std_dydw(data, model, torch.from_numpy(mu.copy()), torch.from_numpy(sd))
+        np.savez(os.path.join(out, f"{name}.npz"), spec=np.array([c["width"], c["width"], c["in_b"], 5, c["depth"],
+                                                                   c["depth"], c["width"]]),
+                 activation=c["act"], mu=mu, sd=sd, branch_in=branch, trunk_in=grid, pts=pts,
+                 scores=np.asarray(scores, np.float32))
+        print(name, "D", D, "scores sum", float(np.sum(scores)))
+    B = import_ref_mods("Neural_network/VI", "sensitivity")
+    for name, width, act, seed in (("sens_bnn_tanh", [10, 10], "tanh", 41), ("sens_bnn_sine", [8, 6], "sine", 42)):
+        torch.manual_seed(seed)
+        model = B.get_model(width, act, True)
+        flat = torch.cat([p.detach().flatten() for p in model.parameters()]).numpy()
+        rng = np.random.default_rng(seed)
+        mu = (flat + 0.05 * rng.standard_normal(flat.size)).astype(np.float32)
+        sd = (0.1 * np.abs(mu) + 0.01).astype(np.float32)
+        x_val = torch.linspace(-1.2, 1.2, 300).view(-1, 1)
+        y_val = 4 * torch.sin(4 * x_val) + 5 * torch.cos(12 * x_val)
+        scores = B.eval_std_dydw((x_val, y_val), model, torch.from_numpy(mu.copy()), torch.from_numpy(sd))
+        np.savez(os.path.join(out, f"{name}.npz"), width=np.array(width), activation=act, mu=mu, sd=sd,
+                 x_val=x_val.numpy(), scores=np.asarray(scores, np.float32))
+        print(name, "D", flat.size, "scores sum", float(np.sum(scores)))
+
+
 if __name__ == "__main__":
     stub_hamiltorch()
     torch.set_num_threads(8)
+    if "--sens-only" in sys.argv:
+        sensitivity_cases(HERE)
+        sys.exit(0)
     if "--init-only" in sys.argv:
         init_cases(HERE)
         sys.exit(0)
@@ -275,3 +346,4 @@ if __name__ == "__main__":
     bnn_cases(HERE)
     deeponet_cases(HERE, full_size="--no-full" not in sys.argv)
     deeponet_split_cases(HERE)
+    sensitivity_cases(HERE)

@@ -168,4 +168,45 @@ struct MlpArgs {
 hipError_t launch_mlp(const MlpArgs& a, int C, int maxw, hipStream_t s);
 size_t mlp_lds_bytes(int D, int n_layers, int maxw);
 
+// ---------------------------------------------------------------------------------------------
+// Sensitivity scores (vihmc_sens.hip): mean over the selected outputs f[n][p] of (df/dtheta)^2 for every
+// parameter of both DeepONet MLPs, by pair backprop. A pair (n, p) seeds the branch at row n with the
+// trunk output row Z_t[p] and the trunk at row p with Z_b[n]; within one row ("group") the pairs share
+// every activation, so sum_pairs (delta_l[i] h_{l-1}[j])^2 = q_l[i] h_{l-1}[j]^2 with
+// q_l = sum_pairs delta_l^2. k_sens_seeds propagates 16 seeds of one group per wave and writes q_l per
+// layer; k_sens_outer forms sum_tasks q_l[i] h^2[j] per task chunk; k_sens_reduce sums the chunks in a
+// fixed order into the packed layout; k_sens_flat maps to flat order and applies sigma^2 / count.
+// ---------------------------------------------------------------------------------------------
+constexpr int SENS_MAXL = 16;
+constexpr int SENS_WAVES = 8;          // tasks (waves) per k_sens_seeds workgroup, sharing the W_l image
+constexpr int SENS_SEEDS = 16;         // seeds per task
+constexpr int SENS_QLD = 128;          // q row stride (floats)
+constexpr int SENS_PART = 128 * 128 + 128;
+constexpr int SENS_TCH = 64;           // tasks staged per k_sens_outer LDS round
+struct SensLayer {
+    const float* W;          // packed Wp [n_out][ldi] of layer l
+    const float* Hprev;      // input rows of layer l: h_{l-1} [rows][ldh] (l > 0) or the net input (l = 0)
+    int64_t wp, bias;        // packed offsets of W_l and b_l (output image)
+    int32_t ldi, n_out, n_in, ldh, act_prev;   // act_prev: activation of layer l-1 (unused for l = 0)
+};
+struct SensNet {
+    SensLayer L[SENS_MAXL];
+    int32_t nl, n_tasks, n_wg, chunks, tasks_per_chunk;
+    const float* seeds; int32_t ld_seed;   // the other net's output rows
+    const int32_t* tasks;                  // [n_tasks][3]: group row, first seed, seed count (<= 16)
+    const int32_t* seed_idx;
+    float* Q;                              // [n_tasks][nl][SENS_QLD]
+    float* part;                           // [nl][chunks][SENS_PART]
+};
+struct SensArgs {
+    SensNet net[2];
+    int32_t ldd, ldw;        // LDS strides of the delta and W images (floats)
+    float* S;                // packed-layout output (one chain), slot 0 = the output bias b
+    float count;             // pairs = outputs averaged over
+};
+hipError_t launch_sens(const SensArgs& a, const SensArgs* dev_a, const int32_t* fmap, int64_t D, const float* sigma,
+                       float* out, hipStream_t s);    // dev_a: a copy of `a` in device memory
+size_t sens_seeds_lds_bytes(int ldd, int ldw);
+hipError_t launch_sens_mlp(const MlpArgs& a, float* slab, const float* sigma, float* out, int maxw, hipStream_t s);
+
 }  // namespace vihmc

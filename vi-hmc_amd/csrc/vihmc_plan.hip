@@ -112,6 +112,8 @@ struct vihmc_plan {
     ReduceJob* jobsW = nullptr;
     int n_jobsW = 0, max_lenW = 0, lenB = 0;
 
+    std::vector<int32_t> fmap_host;    // flat parameter index -> packed offset (sensitivity output map)
+
     // MLP
     MlpArgs mlp{};
     int maxw = 0;
@@ -276,6 +278,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     }
     for (int64_t i = 0; i < p->D; ++i)
         if (map_w[i] < 0) return fail("layer table does not cover parameter " + std::to_string(i));
+    p->fmap_host = map_w;
     if (p->nets[0].L.back().n_out != p->nets[1].L.back().n_out)
         return fail("branch and trunk output widths differ");
     p->W = p->nets[0].L.back().n_out;
@@ -931,6 +934,141 @@ int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         hipStream_t s = static_cast<hipStream_t>(stream);
         return p->kind == 0 ? deeponet_eval(p, theta, C, logp, nullptr, out, s)
                             : mlp_eval(p, theta, C, logp, nullptr, out, s);
+    });
+}
+
+namespace {
+int ld_residue(int n, int res) {       // smallest v >= n with v % 16 == res
+    int v = n;
+    while (v % 16 != res) ++v;
+    return v;
+}
+
+// DeepONet sensitivity (vihmc_sens.hip): pair tasks built on the host from the point lists, one forward
+// of chain 0, then seeds -> outer -> reduce -> flat. Temporaries are freed after a stream sync.
+int deeponet_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, int npts, const float* sigma,
+                         float* out, hipStream_t s) {
+    if (!pts || npts < 1) return fail("DeepONet sensitivity needs point lists (pts, npts >= 1)");
+    const int N = p->N, P = p->P;
+    for (int64_t e = 0; e < (int64_t)N * npts; ++e)
+        if (pts[e] < 0 || pts[e] >= P) return fail("point index out of range [0, P)");
+    for (int net = 0; net < 2; ++net)
+        if ((int)p->nets[net].L.size() > SENS_MAXL) return fail("sensitivity: too many layers");
+    // branch: group n, seeds = trunk rows pts[n][*]; trunk: group p, seeds = branch rows n with p in pts[n]
+    std::vector<int32_t> tasks[2], seeds[2];
+    seeds[0].assign(pts, pts + (int64_t)N * npts);
+    for (int n = 0; n < N; ++n)
+        for (int k = 0; k < npts; k += SENS_SEEDS)
+            tasks[0].insert(tasks[0].end(), {n, n * npts + k, std::min(SENS_SEEDS, npts - k)});
+    {
+        std::vector<int32_t> cnt(P + 1, 0);
+        for (int64_t e = 0; e < (int64_t)N * npts; ++e) ++cnt[pts[e] + 1];
+        for (int q = 0; q < P; ++q) cnt[q + 1] += cnt[q];
+        std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+        seeds[1].resize((size_t)N * npts);
+        for (int n = 0; n < N; ++n)
+            for (int k = 0; k < npts; ++k) seeds[1][fill[pts[(int64_t)n * npts + k]]++] = n;
+        for (int q = 0; q < P; ++q)
+            for (int k = cnt[q]; k < cnt[q + 1]; k += SENS_SEEDS)
+                tasks[1].insert(tasks[1].end(), {q, k, std::min(SENS_SEEDS, cnt[q + 1] - k)});
+    }
+    std::vector<void*> tmp;
+    auto talloc = [&](void** d, size_t bytes) -> hipError_t {
+        hipError_t e = hipMalloc(d, std::max<size_t>(bytes, 4));
+        if (e == hipSuccess) tmp.push_back(*d);
+        return e;
+    };
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(s);
+        for (void* v : tmp) (void)hipFree(v);
+    };
+    SensArgs a{};
+    int kmax = 16, jmax = 16;
+    hipError_t e = hipSuccess;
+    for (int net = 0; net < 2 && e == hipSuccess; ++net) {
+        Net& n = p->nets[net];
+        Net& o = p->nets[1 - net];
+        SensNet& sn = a.net[net];
+        sn.nl = (int)n.L.size();
+        sn.n_tasks = (int)(tasks[net].size() / 3);
+        sn.n_wg = cdiv(sn.n_tasks, SENS_WAVES);
+        sn.chunks = std::max(1, std::min(128, cdiv(sn.n_tasks, 256)));
+        sn.tasks_per_chunk = cdiv(sn.n_tasks, sn.chunks);
+        sn.seeds = o.act + o.h_off.back();
+        sn.ld_seed = p->ldz;
+        for (int l = 0; l < sn.nl; ++l) {
+            const LayerPk& L = n.L[l];
+            SensLayer& q = sn.L[l];
+            q.W = p->packed + L.wp;
+            q.wp = L.wp;
+            q.bias = L.bias;
+            q.ldi = L.ldi;
+            q.n_out = L.n_out;
+            q.n_in = L.n_in;
+            q.Hprev = l == 0 ? n.input : n.act + n.h_off[l - 1];
+            q.ldh = l == 0 ? n.ld_in : n.L[l - 1].ldo;
+            q.act_prev = l == 0 ? ACT_ID : n.L[l - 1].act;
+            kmax = std::max(kmax, (L.n_out + 15) & ~15);
+            jmax = std::max(jmax, (L.n_in + 15) & ~15);
+        }
+        int32_t *dt = nullptr, *ds = nullptr;
+        e = talloc((void**)&dt, tasks[net].size() * 4);
+        if (e == hipSuccess) e = talloc((void**)&ds, seeds[net].size() * 4);
+        if (e == hipSuccess) e = hipMemcpyAsync(dt, tasks[net].data(), tasks[net].size() * 4, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(ds, seeds[net].data(), seeds[net].size() * 4, hipMemcpyHostToDevice, s);
+        sn.tasks = dt;
+        sn.seed_idx = ds;
+        if (e == hipSuccess) e = talloc((void**)&sn.Q, (size_t)std::max(sn.n_tasks, 1) * sn.nl * SENS_QLD * 4);
+        if (e == hipSuccess) e = hipMemsetAsync(sn.Q, 0, (size_t)std::max(sn.n_tasks, 1) * sn.nl * SENS_QLD * 4, s);
+        if (e == hipSuccess) e = talloc((void**)&sn.part, (size_t)sn.nl * sn.chunks * SENS_PART * 4);
+    }
+    int32_t* dmap = nullptr;
+    if (e == hipSuccess) e = talloc((void**)&a.S, (size_t)p->dp * 4);
+    if (e == hipSuccess) e = hipMemsetAsync(a.S, 0, (size_t)p->dp * 4, s);
+    if (e == hipSuccess) e = talloc((void**)&dmap, (size_t)p->D * 4);
+    if (e == hipSuccess) e = hipMemcpyAsync(dmap, p->fmap_host.data(), (size_t)p->D * 4, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+        cleanup();
+        return fail(std::string("sensitivity setup: ") + hipGetErrorString(e), (int)e);
+    }
+    (void)kmax;
+    (void)jmax;
+    a.ldd = ld_residue(128, 8);       // deltas [16][136]: float4 row reads of 16 rows are conflict free
+    a.ldw = ld_residue(128, 4);       // W image [128][132]: b32 reads of rows 4 apart hit distinct bank groups
+    a.count = (float)((double)N * npts);
+    e = launch_scatter(p->packed, p->dp, 1, theta, p->K, p->smap_w, p->smap_wt, s);
+    int rc = e == hipSuccess ? deeponet_forward_layers(p, 1, s) : 0;
+    SensArgs* dev_a = nullptr;
+    if (e == hipSuccess && rc == 0) e = talloc((void**)&dev_a, sizeof(SensArgs));
+    if (e == hipSuccess && rc == 0) e = hipMemcpyAsync(dev_a, &a, sizeof(SensArgs), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && rc == 0) e = launch_sens(a, dev_a, dmap, p->D, sigma, out, s);
+    cleanup();
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(std::string("sensitivity: ") + hipGetErrorString(e), (int)e);
+    return 0;
+}
+
+int mlp_sensitivity(vihmc_plan* p, const float* theta, const float* sigma, float* out, hipStream_t s) {
+    MlpArgs a = p->mlp;
+    a.theta = theta;
+    float* slab = nullptr;
+    const int nblk = cdiv(p->mlp.N, 64);
+    HIPCHK(hipMalloc((void**)&slab, (size_t)nblk * p->D * 4));
+    hipError_t e = launch_sens_mlp(a, slab, sigma, out, p->maxw, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(slab);
+    if (e != hipSuccess) return fail(std::string("sensitivity (MLP): ") + hipGetErrorString(e), (int)e);
+    return 0;
+}
+}  // namespace
+
+int vihmc_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, int npts, const float* sigma,
+                      float* out, void* stream) {
+    return guarded([&]() -> int {
+        if (!p || !theta || !out) return fail("null argument");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        return p->kind == 0 ? deeponet_sensitivity(p, theta, pts, npts, sigma, out, s)
+                            : mlp_sensitivity(p, theta, sigma, out, s);
     });
 }
 

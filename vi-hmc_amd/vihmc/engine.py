@@ -116,6 +116,32 @@ class _Engine:
         _lib.check(rc, "vihmc_forward")
         return logp, out
 
+    def sensitivity(self, theta: torch.Tensor, pts=None, sigma=None) -> torch.Tensor:
+        """vihmc_sensitivity: sigma^2 * mean over outputs of (d f / d theta)^2 for all D parameters, flat
+        order, at theta ([K], the plan's chain 0). DeepONet: ``pts`` [N, npts] int, the trunk points each
+        branch row is evaluated at (required); BNN: every data row. ``sigma=None`` returns the mean
+        squared gradient."""
+        th = self._theta(torch.as_tensor(theta).reshape(1, -1))
+        out = torch.empty(self.D, device=self.device, dtype=torch.float32)
+        sg = None
+        if sigma is not None:
+            sg = torch.as_tensor(sigma).to(device=self.device, dtype=torch.float32).reshape(-1).contiguous()
+            if sg.numel() != self.D:
+                raise ValueError(f"sigma must have D={self.D} entries")
+        pp, npts = None, 0
+        if self.kind == "deeponet":
+            if pts is None:
+                raise ValueError("DeepONet sensitivity needs pts [N, npts] (trunk points per branch row)")
+            pp = np.ascontiguousarray(np.asarray(pts, dtype=np.int32))
+            if pp.ndim != 2 or pp.shape[0] != self.N:
+                raise ValueError(f"pts must be [N={self.N}, npts]")
+            npts = pp.shape[1]
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_sensitivity(self._plan, th.data_ptr(), None if pp is None else pp.ctypes.data, npts,
+                                          None if sg is None else sg.data_ptr(), out.data_ptr(), self._stream())
+        _lib.check(rc, "vihmc_sensitivity")
+        return out
+
     # ---- kernel timing hook (roofline) -----------------------------------------------------------
     def timing(self, which: int = 0, on: bool = True):
         _lib.check(self.L.vihmc_timing_enable(self._plan, which, int(on)), "vihmc_timing_enable")
