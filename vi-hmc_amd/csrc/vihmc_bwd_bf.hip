@@ -23,7 +23,12 @@
 
 #ifndef BB_ABL
 #define BB_ABL 0    // timing-only ablations (wrong results): 1 no loads after the first sub-tile, 2 no dX
-                    // MFMAs, 3 no dW MFMAs
+                    // MFMAs, 3 no dW MFMAs, 4 no three-way split (one cvt), 5 dX W operands not re-read
+                    // from LDS per sub-tile, 6 no LDS plane stores after the first sub-tile
+#endif
+
+#ifndef BB_WPITCH_B
+#define BB_WPITCH_B 224   // W^T plane row pitch (bytes)
 #endif
 
 namespace vihmc {
@@ -44,11 +49,14 @@ constexpr int BB_DP = 0;                               // D planes
 constexpr int BB_HP = 3 * BB_PLANE;                    // H planes
 constexpr int BB_DT = 6 * BB_PLANE;                    // D fp32 tail [32][4]
 constexpr int BB_BUF = BB_DT + BB_SUB * 16;            // 43520 bytes per buffer
-constexpr int BB_WPITCH = 208;                         // W^T plane rows: 13 x 16 B (odd) -> row reads conflict free
+// W^T plane rows: read like the D planes (lane l: row l & 15, 16-B column l >> 4), so the same pitch
+// residue (8 mod 16 dwords) keeps the b128 reads conflict free; 208 B (4 mod 16) measured 2-way
+constexpr int BB_WPITCH = BB_WPITCH_B;
 constexpr int BB_WPLANE = 100 * BB_WPITCH;             // 20800 (rows 0..99; tile-6 reads clamp to row 99)
 constexpr int BB_W = 2 * BB_BUF;                       // W^T planes after the two sub-tile buffers
 constexpr int BB_WT = BB_W + 3 * BB_WPLANE;            // W^T fp32 tail [100][4]
-constexpr int BB_LDS = BB_WT + 100 * 16;               // 150080
+constexpr int BB_LDS = BB_WT + 100 * 16;               // 154880 (pitch 224)
+static_assert(BB_LDS <= 160 * 1024, "LDS");
 constexpr int BB_THREADS = 1024;                       // 8 dX + 8 dW waves, 4 per SIMD
 constexpr int BB_SLOTS = 2;                            // staged float4 per thread (<= 800 D + 896 H)
 
@@ -125,10 +133,18 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
             const bool isd = (st_d >> v) & 1;                                                           \
             unsigned char* base = smw + (BUF) * BB_BUF + (isd ? BB_DP : BB_HP) + r * BB_PITCH + 8 * c4; \
             bf16x4 p0, p1, p2;                                                                          \
-            split4(x, p0, p1, p2);                                                                      \
-            *reinterpret_cast<bf16x4*>(base) = p0;                                                      \
-            *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;                                           \
-            *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;                                       \
+            if (BB_ABL == 4) {                                                                          \
+                for (int j_ = 0; j_ < 4; ++j_) p0[j_] = (__bf16)x[j_];                                  \
+                p1 = p0;                                                                                \
+                p2 = p0;                                                                                \
+            } else {                                                                                    \
+                split4(x, p0, p1, p2);                                                                  \
+            }                                                                                           \
+            if (BB_ABL != 6 || (SUB) == r0) {                                                           \
+                *reinterpret_cast<bf16x4*>(base) = p0;                                                  \
+                *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;                                       \
+                *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;                                   \
+            }                                                                                           \
             if (isd) {                                                                                  \
                 if (v == 0) dcol += x;                                                                  \
                 if (c4 == 24) *reinterpret_cast<f32x4*>(smw + (BUF) * BB_BUF + BB_DT + r * 16) = x;     \
@@ -178,8 +194,13 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     db[p] = *reinterpret_cast<const bf16x8*>(drow + p * BB_PLANE + 64 * kb);
-                    wa[p] = *reinterpret_cast<const bf16x8*>(wrow0 + p * BB_WPLANE + 64 * kb);
-                    wb[p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
+                    if (BB_ABL == 5) {
+                        wa[p] = db[p];
+                        wb[p] = db[(p + 1) % 3];
+                    } else {
+                        wa[p] = *reinterpret_cast<const bf16x8*>(wrow0 + p * BB_WPLANE + 64 * kb);
+                        wb[p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
+                    }
                 }
                 if (BB_ABL != 2) {
                     acc[0] = six(wa, db, acc[0]);
