@@ -130,6 +130,11 @@ int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* 
 int vihmc_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, int npts, const float* sigma,
                       float* out, void* stream);
 
+/* Replace the data of a DeepONet plan (same N and P): x_branch [N, in_branch] and y [N, P], device
+ * pointers, copied into the plan on `stream` (ordered before later evaluations on it). For minibatch loops
+ * (Operator_network/VI/main_VI_deeponet.py:58-79) without re-creating the plan. */
+int vihmc_plan_set_data(vihmc_plan* p, const float* x_branch, const float* y, void* stream);
+
 int     vihmc_plan_kind(const vihmc_plan* p);
 int64_t vihmc_plan_n_params(const vihmc_plan* p);
 int     vihmc_plan_K(const vihmc_plan* p);

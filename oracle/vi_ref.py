@@ -1,0 +1,64 @@
+"""ORACLE (test infrastructure only) -- one BBB training step of the Bayesian DeepONet restated on the CPU.
+
+Restates the ELBO of Operator_network/VI/main_VI_deeponet.py:58-79 (train_model's inner loop) with
+bayesian_model.py:76-114 / layers/BBB/BBBLinear.py:54-78 / metrics.py:13-31,58-60 in float64 torch with
+autograd: for each weight draw j, W_j = mu + eps_j * softplus(rho), pred = DeepONet(W_j) (F.linear + act,
+einsum, + b), loss_j = gaussian_nll(mean) * train_size + beta * KL(prior || posterior); the step's loss is
+the mean over draws. Pinned by tests/golden/vi_deeponet_*.npz (the reference's own train_model).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .deeponet_ref import trunk_feats_np
+
+
+def _mlp(W, layers, x, act):
+    h = x
+    for i, l in enumerate(layers):
+        w = W[l.w_off:l.w_off + l.n_out * l.n_in].reshape(l.n_out, l.n_in)
+        h = F.linear(h, w, W[l.b_off:l.b_off + l.n_out])
+        if i < len(layers) - 1:
+            h = torch.tanh(h) if act == "tanh" else torch.relu(h)
+    return h
+
+
+def elbo_step(layout, mu, rho, eps_list, branch_in, trunk_grid, y_grid, beta, train_size, noise_var=1.0,
+              prior_mu=0.0, prior_sigma=0.1, act="tanh"):
+    """(loss, d loss / d mu, d loss / d rho) in float64; y_grid [B, P] in trunk_grid order."""
+    br, tr, D = layout
+    mu_t = torch.tensor(np.asarray(mu, np.float64), requires_grad=True)
+    rho_t = torch.tensor(np.asarray(rho, np.float64), requires_grad=True)
+    xb = torch.tensor(np.asarray(branch_in, np.float64))
+    ft = torch.tensor(trunk_feats_np(trunk_grid))
+    y = torch.tensor(np.asarray(y_grid, np.float64))
+    sig = torch.log1p(torch.exp(rho_t))
+    sp = torch.tensor(float(prior_sigma), dtype=torch.float64)
+    kl = 0.5 * (2 * torch.log(sig / sp) - 1 + (sp / sig) ** 2 + ((mu_t - prior_mu) / sig) ** 2).sum()
+    total = 0.0
+    for eps in eps_list:
+        W = mu_t + torch.tensor(np.asarray(eps, np.float64)) * sig
+        pred = _mlp(W, br, xb, act) @ _mlp(W, tr, ft, act).T + W[0]
+        nll = F.gaussian_nll_loss(pred, y, torch.full_like(y, noise_var), reduction="mean")
+        total = total + nll * train_size + beta * kl
+    loss = total / len(eps_list)
+    gm, gr = torch.autograd.grad(loss, (mu_t, rho_t))
+    return float(loss.detach()), gm.numpy(), gr.numpy()
+
+
+def eval_loss(layout, mu, rho, branch_in, trunk_grid, y_grid, beta, size, noise_var=1.0, prior_mu=0.0,
+              prior_sigma=0.1, act="tanh"):
+    """validate_model's loss (eval mode: W = mu) and metrics.mse, float64."""
+    br, tr, D = layout
+    W = torch.tensor(np.asarray(mu, np.float64))
+    sig = torch.log1p(torch.exp(torch.tensor(np.asarray(rho, np.float64))))
+    sp = torch.tensor(float(prior_sigma), dtype=torch.float64)
+    kl = 0.5 * (2 * torch.log(sig / sp) - 1 + (sp / sig) ** 2 + ((W - prior_mu) / sig) ** 2).sum()
+    xb = torch.tensor(np.asarray(branch_in, np.float64))
+    ft = torch.tensor(trunk_feats_np(trunk_grid))
+    y = torch.tensor(np.asarray(y_grid, np.float64))
+    pred = _mlp(W, br, xb, act) @ _mlp(W, tr, ft, act).T + W[0]
+    nll = F.gaussian_nll_loss(pred, y, torch.full_like(y, noise_var), reduction="mean")
+    return float(nll * size + beta * kl), float(torch.mean((pred - y) ** 2))

@@ -333,9 +333,93 @@ def sensitivity_cases(out):
         print(name, "D", flat.size, "scores sum", float(np.sum(scores)))
 
 
+# ------------------------------------------------------------------------------------------------
+# BBB VI training of the Bayesian DeepONet (Operator_network/VI/main_VI_deeponet.py, bayesian_model.py)
+# ------------------------------------------------------------------------------------------------
+class _GradRecorder:
+    """Optimizer stand-in for the reference's train_model: records the gradients at step()."""
+
+    def __init__(self, model):
+        self.model, self.grads = model, None
+
+    def zero_grad(self):
+        self.model.zero_grad()
+
+    def step(self):
+        self.grads = {n: p.grad.detach().clone() for n, p in self.model.named_parameters()}
+
+
+def _flat(named, kind):
+    """[b_kind] + [W_kind, bias_kind per BBB layer] in module order (the deterministic DeepONet order)."""
+    parts = [named[f"b_{kind}"].reshape(-1)]
+    layer_names = sorted({n.rsplit(".", 1)[0] for n in named if n.endswith("W_mu")},
+                         key=lambda s: (s.split(".")[0], int(s.split(".")[1])))
+    for ln in layer_names:
+        parts += [named[f"{ln}.W_{kind}"].reshape(-1), named[f"{ln}.bias_{kind}"].reshape(-1)]
+    return torch.cat(parts).numpy()
+
+
+def vi_cases(out):
+    """The reference's own train_model / validate_model / metrics.mse on a small Bayesian DeepONet: init
+    (after torch.manual_seed), one training step's loss and mu / rho gradients with num_ens weight draws,
+    the eval-mode validation loss and MSE. Batches: B functions, each with a permutation of the whole trunk
+    grid (BurgersDataSet with p = P, utils.py:39-41)."""
+    clash = ("util", "utils", "config", "config_sens", "model", "my_make_func", "sensitivity", "metrics",
+             "bayesian_model", "main_VI_deeponet", "layers", "layers.BBB", "layers.BBB.BBBLinear", "layers.BBB.BBBConv",
+             "layers.BBB_LRT", "layers.BBB_LRT.BBBLinear", "layers.BBB_LRT.BBBConv", "layers.misc")
+    M = import_ref_mods("Operator_network/VI", "main_VI_deeponet", clash)
+    import metrics as MET
+    import bayesian_model as BM
+    cases = {
+        "vi_deeponet_tanh": dict(width=12, in_b=7, depth=3, act="tanh", B=4, nt=5, nx=6, num_ens=2, beta=1.0,
+                                 seed=51, rho0=(-5, 0.1)),
+        "vi_deeponet_relu": dict(width=10, in_b=5, depth=4, act="relu", B=3, nt=4, nx=5, num_ens=3, beta="Standard",
+                                 seed=52, rho0=(-3, 0.1)),
+    }
+    for name, c in cases.items():
+        priors = {"prior_mu": 0, "prior_sigma": 0.1, "posterior_mu_initial": (0, 0.1), "posterior_rho_initial": c["rho0"]}
+        torch.manual_seed(c["seed"])
+        model = BM.Bayesian_DeepONet(priors, c["width"], c["width"], c["in_b"], 5, c["depth"], c["depth"], c["width"],
+                                     c["act"], 0, 0, impose_bc=True)
+        named = {n: p.detach().clone() for n, p in model.named_parameters()}
+        mu0, rho0 = _flat(named, "mu"), _flat(named, "rho")
+        rng = np.random.default_rng(c["seed"])
+        P = c["nt"] * c["nx"]
+        t = np.linspace(0.0, 1.0, c["nt"], dtype=np.float32)
+        x = np.linspace(0.0, 1.0, c["nx"], dtype=np.float32)
+        grid = np.stack(np.meshgrid(t, x, indexing="ij"), -1).reshape(-1, 2).astype(np.float32)
+        branch = rng.standard_normal((c["B"], c["in_b"])).astype(np.float32)
+        y_grid = (0.5 * rng.standard_normal((c["B"], P))).astype(np.float32)
+        perms = np.stack([rng.permutation(P) for _ in range(c["B"])]).astype(np.int64)
+        batch = (torch.from_numpy(branch).view(c["B"], 1, -1),
+                 torch.from_numpy(np.stack([grid[perms[b]] for b in range(c["B"])])),
+                 torch.from_numpy(np.stack([y_grid[b, perms[b]] for b in range(c["B"])])))
+        train_size = c["B"] * P * 10
+        loss = MET.ELBO(False, 0)
+        rec = _GradRecorder(model)
+        torch.manual_seed(c["seed"] + 1000)
+        l_train = M.train_model([batch], model, loss, rec, train_size, 1, c["num_ens"], c["beta"],
+                                noise_param=torch.tensor(1.0))
+        g_mu, g_rho = _flat(rec.grads, "mu"), _flat(rec.grads, "rho")
+        l_val = M.validate_model([batch], model, loss, train_size, c["beta"], 1, noise_param=torch.tensor(1.0))
+        m_val = MET.mse([batch], model, 0, "Burgers")
+        with torch.no_grad():
+            _, kl0 = model(batch[0], batch[1])      # eval mode after validate_model: W = mu
+        np.savez(os.path.join(out, f"{name}.npz"), spec=np.array([c["width"], c["width"], c["in_b"], 5, c["depth"],
+                                                                   c["depth"], c["width"]]),
+                 activation=c["act"], prior_rho0=np.array(c["rho0"], np.float64), seed=c["seed"], mu0=mu0, rho0=rho0,
+                 branch_in=branch, trunk_grid=grid, perms=perms, y_grid=y_grid, train_size=train_size,
+                 num_ens=c["num_ens"], beta=str(c["beta"]), loss_train=np.float64(l_train), grad_mu=g_mu,
+                 grad_rho=g_rho, loss_val=np.float64(l_val), mse_val=np.float64(m_val), kl0=np.float64(float(kl0)))
+        print(name, "D", mu0.size, "train loss", l_train, "val loss", l_val, "mse", m_val)
+
+
 if __name__ == "__main__":
     stub_hamiltorch()
     torch.set_num_threads(8)
+    if "--vi-only" in sys.argv:
+        vi_cases(HERE)
+        sys.exit(0)
     if "--sens-only" in sys.argv:
         sensitivity_cases(HERE)
         sys.exit(0)
@@ -347,3 +431,4 @@ if __name__ == "__main__":
     deeponet_cases(HERE, full_size="--no-full" not in sys.argv)
     deeponet_split_cases(HERE)
     sensitivity_cases(HERE)
+    vi_cases(HERE)

@@ -1,0 +1,99 @@
+"""Bayesian DeepONet VI training on the GPU (vihmc/vi.py: the NLL part of every ELBO through the HIP engine)
+against the reference's own train_model / validate_model / metrics.mse (tests/golden/vi_deeponet_*.npz), and
+at the Burgers shapes (width 100, depth 9, 101 x 101 grid) against the float64 oracle (oracle/vi_ref.py)."""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.vi_ref import elbo_step
+from vi_cases import VI_CASES, GradRecorder, make_model, rel_norm, vi_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", VI_CASES)
+def test_train_validate_mse_match_reference(name, cuda_device):
+    from vihmc.vi import ELBO, BatchEngines, mse, train_model, validate_model
+    c = vi_case(name)
+    m = make_model(c).to(cuda_device)
+    eng = BatchEngines(m.spec, c.g["trunk_grid"], 1.0, c.num_ens, cuda_device)
+    try:
+        rec = GradRecorder(m)
+        torch.manual_seed(c.seed + 1000)
+        lt = train_model([c.batch], m, ELBO(), rec, c.train_size, 1, c.num_ens, c.beta, engines=eng)
+        assert lt == pytest.approx(float(c.g["loss_train"]), rel=2e-5)
+        assert rel_norm(rec.grads[0].cpu().numpy(), c.g["grad_mu"]) < 2e-4
+        assert rel_norm(rec.grads[1].cpu().numpy(), c.g["grad_rho"]) < 2e-4
+        lv = validate_model([c.batch], m, ELBO(), c.train_size, c.beta, 1, engines=eng)
+        assert lv == pytest.approx(float(c.g["loss_val"]), rel=2e-5)
+        assert mse([c.batch], m, engines=eng) == pytest.approx(float(c.g["mse_val"]), rel=1e-4)
+    finally:
+        eng.close()
+
+
+def test_burgers_shape_step_matches_oracle(cuda_device):
+    """Width 100, depth 9, the 101 x 101 grid, 6 functions with permuted points, 2 weight draws: one training
+    step's loss and gradients against the float64 oracle; plus the data swap between two batches."""
+    from oracle.deeponet_ref import deeponet_layout
+    from vihmc.data import deeponet_problem
+    from vihmc.vi import ELBO, BatchEngines, Bayesian_DeepONet, train_model
+    prob = deeponet_problem(seed=3, n=12)
+    grid = prob.trunk_in[0]
+    P = grid.shape[0]
+    priors = {"prior_mu": 0, "prior_sigma": 0.1, "posterior_mu_initial": (0, 0.1), "posterior_rho_initial": (-5, 0.1)}
+    torch.manual_seed(7)
+    m = Bayesian_DeepONet(priors, 100, 100, 101, 5, 9, 9, 100, "tanh", 0, 0, impose_bc=True)
+    mu0, rho0 = m.mu_flat().detach().numpy().copy(), m.rho_flat().detach().numpy().copy()
+    m = m.to(cuda_device)
+    rng = np.random.default_rng(5)
+    batches = []
+    for b0 in (0, 6):
+        perms = np.stack([rng.permutation(P) for _ in range(6)])
+        batches.append((torch.from_numpy(prob.branch_in[b0:b0 + 6]),
+                        torch.from_numpy(np.stack([grid[p] for p in perms])),
+                        torch.from_numpy(np.stack([prob.y[b0 + i, perms[i]] for i in range(6)]))))
+    eng = BatchEngines(m.spec, grid, 1.0, 2, cuda_device)
+    lay = deeponet_layout()
+    try:
+        for bi, batch in enumerate(batches):
+            rec = GradRecorder(m)
+            torch.manual_seed(100 + bi)
+            eps = [m.draw_eps().numpy() for _ in range(2)]
+            torch.manual_seed(100 + bi)
+            lt = train_model([batch], m, ELBO(), rec, 1000 * P, 1, 2, 1.0, engines=eng)
+            b0 = 6 * bi
+            loss, gm, gr = elbo_step(lay, mu0, rho0, eps, prob.branch_in[b0:b0 + 6, 0], grid, prob.y[b0:b0 + 6], 1.0,
+                                     1000 * P)
+            assert lt == pytest.approx(loss, rel=2e-5)
+            assert rel_norm(rec.grads[0].cpu().numpy(), gm) < 2e-4
+            assert rel_norm(rec.grads[1].cpu().numpy(), gr) < 2e-4
+    finally:
+        eng.close()
+
+
+def test_burgers_training_step_timing(cuda_device):
+    """main_VI_deeponet's configuration: batch 128 functions x 10,201 points, num_ens 5, Adam."""
+    from vihmc.data import deeponet_problem
+    from vihmc.vi import ELBO, BatchEngines, Bayesian_DeepONet, train_model
+    prob = deeponet_problem(seed=3, n=256)
+    grid = prob.trunk_in[0]
+    priors = {"prior_mu": 0, "prior_sigma": 0.1, "posterior_mu_initial": (0, 0.1), "posterior_rho_initial": (-5, 0.1)}
+    torch.manual_seed(7)
+    m = Bayesian_DeepONet(priors, 100, 100, 101, 5, 9, 9, 100, "tanh", 0, 0, impose_bc=True).to(cuda_device)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    loader = [(torch.from_numpy(prob.branch_in[b:b + 128]), torch.from_numpy(np.broadcast_to(grid, (128,) + grid.shape)),
+               torch.from_numpy(prob.y[b:b + 128])) for b in (0, 128)]
+    eng = BatchEngines(m.spec, grid, 1.0, 5, cuda_device)
+    try:
+        train_model(loader[:1], m, ELBO(), opt, 1000 * grid.shape[0], 2, 5, 1.0, engines=eng)   # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        l = train_model(loader, m, ELBO(), opt, 1000 * grid.shape[0], 2, 5, 1.0, engines=eng)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / 2
+        print(f"VI training step (B=128, P=10201, num_ens=5, D=172401): {dt * 1e3:.1f} ms, loss {l:.1f}")
+        assert np.isfinite(l)
+    finally:
+        eng.close()

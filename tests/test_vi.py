@@ -1,0 +1,72 @@
+"""CPU checks of the Bayesian DeepONet VI training surface (vihmc/vi.py) against the reference's own
+train_model / validate_model / metrics.mse outputs (tests/golden/vi_deeponet_*.npz): initialisation draws,
+weight-noise draw order (through the float64 oracle oracle/vi_ref.py), KL, ELBO / MSE values, and the host
+logic that maps each item's permuted trunk points back to the grid order."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.vi_ref import elbo_step, eval_loss
+from vi_cases import VI_CASES, make_model, rel_norm, vi_case
+
+
+@pytest.mark.parametrize("name", VI_CASES)
+def test_init_matches_reference(name):
+    c = vi_case(name)
+    m = make_model(c)
+    assert np.array_equal(m.mu_flat().detach().numpy(), c.g["mu0"])
+    assert np.array_equal(m.rho_flat().detach().numpy(), c.g["rho0"])
+
+
+@pytest.mark.parametrize("name", VI_CASES)
+def test_oracle_step_with_our_draws_matches_reference(name):
+    """Our draw order + the float64 oracle ELBO reproduce the reference's loss and mu / rho gradients."""
+    c = vi_case(name)
+    m = make_model(c)
+    torch.manual_seed(c.seed + 1000)
+    eps = [m.draw_eps().numpy() for _ in range(c.num_ens)]
+    from vihmc.vi import get_beta
+    beta = get_beta(0, 1, c.beta, None, None)
+    loss, gm, gr = elbo_step(c.layout, c.g["mu0"], c.g["rho0"], eps, c.g["branch_in"], c.g["trunk_grid"],
+                             c.g["y_grid"], beta, c.train_size, act=c.act)
+    assert loss == pytest.approx(float(c.g["loss_train"]), rel=2e-6)
+    assert rel_norm(gm, c.g["grad_mu"]) < 1e-5
+    assert rel_norm(gr, c.g["grad_rho"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", VI_CASES)
+def test_eval_loss_mse_and_kl(name):
+    """After the recorded step the reference validated with the unchanged parameters (the recorder did
+    not update them): eval-mode loss, MSE and KL."""
+    c = vi_case(name)
+    m = make_model(c)
+    from vihmc.vi import get_beta
+    beta = get_beta(0, 1, c.beta, None, None)
+    lv, mv = eval_loss(c.layout, c.g["mu0"], c.g["rho0"], c.g["branch_in"], c.g["trunk_grid"], c.g["y_grid"], beta,
+                       c.train_size, act=c.act)
+    assert lv == pytest.approx(float(c.g["loss_val"]), rel=2e-6)
+    assert mv == pytest.approx(float(c.g["mse_val"]), rel=1e-5)
+    assert float(m.kl()) == pytest.approx(float(c.g["kl0"]), rel=1e-6)
+
+
+def test_canonical_undoes_item_permutations():
+    from vihmc.layout import DeepONetSpec
+    from vihmc.vi import BatchEngines
+    c = vi_case("vi_deeponet_tanh")
+    be = BatchEngines(DeepONetSpec(12, 12, 7, 5, 3, 3, "tanh", 12), c.g["trunk_grid"], 1.0, 2, "cuda")
+    y = be.canonical(c.batch[1], c.batch[2])
+    assert torch.equal(y, torch.from_numpy(c.g["y_grid"]))
+    bad = c.batch[1].clone()
+    bad[0, 0] = bad[0, 1]                      # a repeated point: not a permutation of the grid
+    with pytest.raises(NotImplementedError):
+        be.canonical(bad, c.batch[2])
+
+
+def test_elbo_module_matches_formula():
+    from vihmc.vi import ELBO, calculate_kl
+    torch.manual_seed(0)
+    pred, y = torch.randn(3, 7), torch.randn(3, 7)
+    kl = calculate_kl(0, 0.1, torch.randn(5), torch.rand(5) + 0.05)
+    v = ELBO()(pred, y, kl, 0.5, 100, torch.tensor(2.0))
+    ref = 100 * torch.mean(0.5 * (np.log(2.0) + (pred - y) ** 2 / 2.0)) + 0.5 * kl
+    assert float(v) == pytest.approx(float(ref), rel=1e-6)

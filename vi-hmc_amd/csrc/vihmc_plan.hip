@@ -1072,6 +1072,21 @@ int vihmc_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, int
     });
 }
 
+int vihmc_plan_set_data(vihmc_plan* p, const float* x_branch, const float* y, void* stream) {
+    return guarded([&]() -> int {
+        if (!p || !x_branch || !y) return fail("null argument");
+        if (p->kind != 0) return fail("vihmc_plan_set_data: DeepONet plans only");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        Net& b = p->nets[0];
+        const size_t in_b = (size_t)b.L[0].n_in * sizeof(float);
+        // branch rows into the padded [N][ld_in] input (pad columns stay zero), y as is
+        HIPCHK(hipMemcpy2DAsync(b.input, (size_t)b.ld_in * sizeof(float), x_branch, in_b, in_b, (size_t)b.rows,
+                                hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(p->y, y, (size_t)p->N * p->P * sizeof(float), hipMemcpyDeviceToDevice, s));
+        return 0;
+    });
+}
+
 int vihmc_plan_kind(const vihmc_plan* p) { return p ? p->kind : -1; }
 int64_t vihmc_plan_n_params(const vihmc_plan* p) { return p ? p->D : -1; }
 int vihmc_plan_K(const vihmc_plan* p) { return p ? p->K : -1; }

@@ -53,6 +53,7 @@ SIGNATURES = {
     "vihmc_logp_grad": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_sensitivity": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "vihmc_plan_set_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "vihmc_plan_kind": (c_int, [c_void_p]),
     "vihmc_plan_n_params": (c_int64, [c_void_p]),
     "vihmc_plan_K": (c_int, [c_void_p]),

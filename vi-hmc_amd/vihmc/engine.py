@@ -116,6 +116,17 @@ class _Engine:
         _lib.check(rc, "vihmc_forward")
         return logp, out
 
+    def set_data(self, x_branch: torch.Tensor, y: torch.Tensor):
+        """vihmc_plan_set_data (DeepONet): new branch rows [N, in_branch] and targets [N, P], same N / P."""
+        xb = torch.as_tensor(x_branch).to(device=self.device, dtype=torch.float32).contiguous()
+        yy = torch.as_tensor(y).to(device=self.device, dtype=torch.float32).contiguous()
+        if xb.numel() != self.N * self.spec.in_branch or yy.numel() != self.N * self.P:
+            raise ValueError(f"set_data needs x_branch [{self.N}, {self.spec.in_branch}] and y [{self.N}, {self.P}]")
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_plan_set_data(self._plan, xb.data_ptr(), yy.data_ptr(), self._stream())
+        _lib.check(rc, "vihmc_plan_set_data")
+        self._keep_data = (xb, yy)          # the copy is asynchronous on the stream
+
     def sensitivity(self, theta: torch.Tensor, pts=None, sigma=None) -> torch.Tensor:
         """vihmc_sensitivity: sigma^2 * mean over outputs of (d f / d theta)^2 for all D parameters, flat
         order, at theta ([K], the plan's chain 0). DeepONet: ``pts`` [N, npts] int, the trunk points each
