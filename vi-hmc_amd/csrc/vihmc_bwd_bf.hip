@@ -24,7 +24,7 @@
 #ifndef BB_ABL
 #define BB_ABL 0    // timing-only ablations (wrong results): 1 no loads after the first sub-tile, 2 no dX
                     // MFMAs, 3 no dW MFMAs, 4 no three-way split (one cvt), 5 dX W operands not re-read
-                    // from LDS per sub-tile, 6 no LDS plane stores after the first sub-tile
+                    // from LDS per sub-tile, 6 no LDS plane stores after the first sub-tile, 7 no dX (Dout) stores
 #endif
 
 #ifndef BB_WPITCH_B
@@ -224,7 +224,8 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
                         const float hv = ((float)h2[r] + (float)h1[r]) + (float)h0[r];
                         o[r] = (col + r < P.n_in) ? acc[u][r] * act_grad_bf(P.act, hv) : 0.f;
                     }
-                    *reinterpret_cast<f32x4*>(orow + col) = o;
+                    if (BB_ABL == 7) asm volatile("" :: "v"(o));
+                    else *reinterpret_cast<f32x4*>(orow + col) = o;
                 }
             }
         }

@@ -33,6 +33,9 @@ __device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+#ifndef FWD_ABL
+#define FWD_ABL 0     // timing-only ablation (wrong results): 1 = no h stores in the bf16x6 forward
+#endif
 #ifndef FWD_TANH_CHEAP
 #define FWD_TANH_CHEAP 1   // 0: odd Taylor series below 0.25, exp-rcp above (<= 4 ulp, ~17 VALU)
 #endif
@@ -305,7 +308,13 @@ __device__ __forceinline__ float4 bf_epi(const float* bias, int t, int lg, const
     h.z = n + 2 < FW ? act_t<ACT>(acc[2] + bv.z) : 0.f;
     h.w = n + 3 < FW ? act_t<ACT>(acc[3] + bv.w) : 0.f;
     const uint32_t off = (t < 6 || lg == 0) ? ooff + 4u * n : OOB;
+#if FWD_ABL == 1
+    asm volatile("" :: "v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w));
+    (void)off;
+    (void)orsrc;
+#else
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), orsrc, off, 0, 0);
+#endif
     return h;
 }
 
