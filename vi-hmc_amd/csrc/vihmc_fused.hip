@@ -373,12 +373,15 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
     const float* Wc = args.packed + c * args.dp;
 
     // zero the never-written tail columns 100..111 of every plane row and the bias pad, both buffers
-    for (int i = tid; i < 2 * 3 * FW; i += FTHREADS) {
-        __bf16* r = reinterpret_cast<__bf16*>(fsmb + (i / (3 * FW)) * BBUF) + (i % (3 * FW)) * BROW + 100;
+    // (register staging only: the pre-split images carry their zeros)
+    if (!N.wimg) {
+        for (int i = tid; i < 2 * 3 * FW; i += FTHREADS) {
+            __bf16* r = reinterpret_cast<__bf16*>(fsmb + (i / (3 * FW)) * BBUF) + (i % (3 * FW)) * BROW + 100;
 #pragma unroll
-        for (int z = 0; z < 12; ++z) r[z] = (__bf16)0.f;
+            for (int z = 0; z < 12; ++z) r[z] = (__bf16)0.f;
+        }
+        if (tid < 24) reinterpret_cast<float*>(fsmb + (tid / 12) * BBUF + 3 * BPLANE * 2)[100 + tid % 12] = 0.f;
     }
-    if (tid < 24) reinterpret_cast<float*>(fsmb + (tid / 12) * BBUF + 3 * BPLANE * 2)[100 + tid % 12] = 0.f;
 
     // staging slot v: float4 i of [W | bias] -> (plane row position) or bias position
     int sdst[FSLOTS];
@@ -419,7 +422,20 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         }                                                                                             \
     }
 
-    VIHMC_FB_LOAD(0)
+    // pre-split weight images (k_split_wimg): layer j's image is DMA-copied into buffer j&1 one layer ahead
+    // (global_load_lds, 1 KB per wave-instruction, no VGPRs / VALU); the barrier drains it (vmcnt(0))
+    const bool dma = N.wimg != nullptr;
+    const unsigned char* wimgc = dma ? N.wimg + c * N.wimg_cs : nullptr;
+#define VIHMC_FB_DMA(J, BUF)                                                                          \
+    for (int k = wave; k < FWD_WIMG / 1024; k += NW)                                                  \
+        __builtin_amdgcn_global_load_lds(                                                             \
+            reinterpret_cast<const void*>(wimgc + (int64_t)(J) * FWD_WIMG + k * 1024 + lane * 16),   \
+            (__attribute__((address_space(3))) void*)(fsmb + (BUF) * FWD_WIMG + k * 1024), 16, 0, 0);
+    if (dma) {
+        VIHMC_FB_DMA(0, 0)
+    } else {
+        VIHMC_FB_LOAD(0)
+    }
     float4 h[7];
     {
         const float* ar = N.in + c * N.in_cs + (int64_t)rowc * N.ldin;
@@ -428,15 +444,23 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         h[6] = lg == 0 ? *reinterpret_cast<const float4*>(ar + 96) : float4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();                            // zero fill done before the staging writes
-    VIHMC_FB_STORE(0)
+    if (!dma) {
+        VIHMC_FB_STORE(0)
+    }
     __builtin_amdgcn_s_waitcnt(0x0F70);         // see k_fwd_fused: no vmcnt waits inside the layer loop
     const float* outc = N.out + c * N.out_cs;
     const uint32_t ooff = rok ? (uint32_t)row * (uint32_t)N.ldo * 4u : OOB;
     const uint32_t obytes = (uint32_t)N.rows * (uint32_t)N.ldo * 4u;
     for (int j = 0; j < N.nl; ++j) {
         __syncthreads();
-        VIHMC_FB_LOAD(min(j + 1, N.nl - 1))
-        const unsigned char* bbuf = fsmb + (j & 1) * BBUF;
+        if (dma) {
+            if (j + 1 < N.nl) {
+                VIHMC_FB_DMA(j + 1, (j + 1) & 1)
+            }
+        } else {
+            VIHMC_FB_LOAD(min(j + 1, N.nl - 1))
+        }
+        const unsigned char* bbuf = fsmb + (j & 1) * (dma ? FWD_WIMG : BBUF);
         const __bf16* wb = reinterpret_cast<const __bf16*>(bbuf);
         const float* bias = reinterpret_cast<const float*>(bbuf + 3 * BPLANE * 2);
         const __amdgpu_buffer_rsrc_t orsrc = make_rsrc(outc + N.h_off[j], obytes);
@@ -447,13 +471,67 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         if (act == ACT_TANH) bf_layer<ACT_TANH>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
         else if (act == ACT_RELU) bf_layer<ACT_RELU>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
         else bf_layer<ACT_ID>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
-        VIHMC_FB_STORE((j + 1) & 1)
+        if (!dma) {
+            VIHMC_FB_STORE((j + 1) & 1)
+        }
     }
 #undef VIHMC_FB_LOAD
 #undef VIHMC_FB_STORE
+#undef VIHMC_FB_DMA
 }
 
-size_t fwd_fused_bf_lds_bytes() { return 2 * (size_t)BBUF; }
+// [W_j | bias_j] of every fused layer of every chain -> the LDS image k_fwd_fused_bf stages (same permuted
+// column order as VIHMC_FB_STORE, zero padding, bias fp32 [112]); one block per (chain, net, layer)
+__global__ __launch_bounds__(256) void k_split_wimg(FusedArgs args) {
+    const int C = args.C;
+    int b = blockIdx.x;
+    const int c = b % C;
+    b /= C;
+    const int net = b < args.net[0].nl ? 0 : 1;
+    const int j = net ? b - args.net[0].nl : b;
+    const FusedNet& N = args.net[net];
+    const float* src = args.packed + c * args.dp + N.w_off[j];
+    unsigned char* img = const_cast<unsigned char*>(N.wimg) + c * N.wimg_cs + (int64_t)j * FWD_WIMG;
+    __bf16* pl = reinterpret_cast<__bf16*>(img);
+    for (int i = threadIdx.x; i < FW * 112 / 4; i += 256) {          // plane positions, 4 at a time
+        const int n = i / 28, q = i % 28;                            // row n, positions 4q..4q+3
+        const int pos = 4 * q;
+        // inverse of VIHMC_FB_STORE's map: position -> source column
+        int col;
+        if (pos < 96) {
+            const int kb = pos >> 5, g = (pos & 31) >> 3, hi = (pos >> 2) & 1;
+            col = 16 * (2 * kb + hi) + 4 * g;
+        } else {
+            col = pos;                                               // 96..99 real, 100..111 zero
+        }
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        if (col < FW) x = *reinterpret_cast<const f32x4*>(src + n * FW + col);
+        bf16x4 a, bb, cc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            __bf16 x0, x1, x2;
+            split3(x[e], x0, x1, x2);
+            a[e] = x0;
+            bb[e] = x1;
+            cc[e] = x2;
+        }
+        *reinterpret_cast<bf16x4*>(pl + n * BROW + pos) = a;
+        *reinterpret_cast<bf16x4*>(pl + BPLANE + n * BROW + pos) = bb;
+        *reinterpret_cast<bf16x4*>(pl + 2 * BPLANE + n * BROW + pos) = cc;
+    }
+    float* bias = reinterpret_cast<float*>(img + 3 * BPLANE * 2);
+    for (int i = threadIdx.x; i < 112; i += 256) bias[i] = i < FW ? src[FW * FW + i] : 0.f;
+    for (int i = 3 * BPLANE * 2 + 112 * 4 + threadIdx.x * 4; i < FWD_WIMG; i += 256 * 4)
+        *reinterpret_cast<float*>(img + i) = 0.f;
+}
+
+hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_split_wimg, dim3(a.C * (a.net[0].nl + a.net[1].nl)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+size_t fwd_fused_bf_lds_bytes() { return 2 * (size_t)FWD_WIMG; }
+static_assert(BBUF <= FWD_WIMG && FWD_WIMG % 1024 == 0 && 2 * FWD_WIMG <= 160 * 1024, "weight image");
 
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s) {
     dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk));

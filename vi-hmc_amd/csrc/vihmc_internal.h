@@ -145,12 +145,17 @@ struct FusedNet {
     int64_t w_off[FUSED_MAXL];                      // packed offset of W_j [100][100] (+ bias right after)
     int32_t act[FUSED_MAXL];
     int32_t nl, rows, nblk;                         // nblk = ceil(rows / (16 * waves per workgroup))
+    const unsigned char* wimg; int64_t wimg_cs;     // bf16x6: pre-split [W_j | bias] LDS images of layers
+                                                    // 1..nl, FWD_WIMG bytes each (k_split_wimg), or null
 };
 struct FusedArgs {
     FusedNet net[2];
     const float* packed; int64_t dp;
     int32_t C;
 };
+constexpr int FWD_WIMG = 69632;                     // one pre-split weight image: 3 x [100][112] bf16 + fp32
+                                                    // bias [112], zero padded to 68 KB (whole 1-KB DMA pieces)
+hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s);
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s);             // bf16x6, 12 waves
 size_t fwd_fused_lds_bytes();

@@ -128,6 +128,14 @@ struct vihmc_plan {
     // evaluation is 4 stream operations instead of ~20 kernel launches
     std::vector<std::pair<int, hipGraphExec_t>> graphs;
     hipStream_t cap_stream = nullptr;
+    // bf16x6 forward: weights pre-split once per evaluation (k_split_wimg) and DMA-staged; VIHMC_FWD_WIMG=0
+    // restores per-workgroup register staging + split
+    unsigned char* wimg = nullptr;
+    int64_t wimg_cs = 0;
+    int fwd_wimg = [] {
+        const char* e = std::getenv("VIHMC_FWD_WIMG");
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
+    }();
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
     int graph_on = -1;          // -1: follow VIHMC_GRAPH
     // hidden-layer forward products as exact 3-way bf16 splits (6 bf16 MFMA products, fp32 accumulate;
@@ -332,6 +340,9 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     p->gT_cs = r64((int64_t)p->P * p->ldgT);
     if (int rc = p->alloc(&p->gT, p->gT_cs * C)) return rc;
     if (p->W == 100) {
+        // pre-split weight images of the bf16x6 fused forward (layers 1.. of both nets)
+        p->wimg_cs = (int64_t)(p->nets[0].L.size() - 1 + p->nets[1].L.size() - 1) * FWD_WIMG;
+        if (int rc = p->alloc(&p->wimg, p->wimg_cs * C)) return rc;
         p->qsplitA_cs = (int64_t)cdiv(p->N, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
         if (int rc = p->alloc(&p->qsplitA, p->qsplitA_cs * C)) return rc;
         p->qsplitB_cs = (int64_t)cdiv(p->P, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
@@ -517,6 +528,13 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s) {
     }
     if (p->fwd_bf16x6 && nw == 12) {
         for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * 12);
+        if (p->fwd_wimg && p->wimg) {
+            // pre-split weight images, DMA-staged by the forward (FWD_WIMG bytes per fused layer)
+            a.net[0].wimg = p->wimg;
+            a.net[1].wimg = p->wimg + (int64_t)a.net[0].nl * FWD_WIMG;
+            a.net[0].wimg_cs = a.net[1].wimg_cs = p->wimg_cs;
+            HIPCHK(launch_split_wimg(a, s));
+        }
         HIPCHK(launch_fwd_fused_bf(a, s));
         return 0;
     }
