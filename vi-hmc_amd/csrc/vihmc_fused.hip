@@ -482,7 +482,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
 
 // [W_j | bias_j] of every fused layer of every chain -> the LDS image k_fwd_fused_bf stages (same permuted
 // column order as VIHMC_FB_STORE, zero padding, bias fp32 [112]); one block per (chain, net, layer)
-__global__ __launch_bounds__(256) void k_split_wimg(FusedArgs args) {
+__global__ __launch_bounds__(1024) void k_split_wimg(FusedArgs args) {
     const int C = args.C;
     int b = blockIdx.x;
     const int c = b % C;
@@ -493,7 +493,7 @@ __global__ __launch_bounds__(256) void k_split_wimg(FusedArgs args) {
     const float* src = args.packed + c * args.dp + N.w_off[j];
     unsigned char* img = const_cast<unsigned char*>(N.wimg) + c * N.wimg_cs + (int64_t)j * FWD_WIMG;
     __bf16* pl = reinterpret_cast<__bf16*>(img);
-    for (int i = threadIdx.x; i < FW * 112 / 4; i += 256) {          // plane positions, 4 at a time
+    for (int i = threadIdx.x; i < FW * 112 / 4; i += 1024) {          // plane positions, 4 at a time
         const int n = i / 28, q = i % 28;                            // row n, positions 4q..4q+3
         const int pos = 4 * q;
         // inverse of VIHMC_FB_STORE's map: position -> source column
@@ -520,13 +520,13 @@ __global__ __launch_bounds__(256) void k_split_wimg(FusedArgs args) {
         *reinterpret_cast<bf16x4*>(pl + 2 * BPLANE + n * BROW + pos) = cc;
     }
     float* bias = reinterpret_cast<float*>(img + 3 * BPLANE * 2);
-    for (int i = threadIdx.x; i < 112; i += 256) bias[i] = i < FW ? src[FW * FW + i] : 0.f;
-    for (int i = 3 * BPLANE * 2 + 112 * 4 + threadIdx.x * 4; i < FWD_WIMG; i += 256 * 4)
+    for (int i = threadIdx.x; i < 112; i += 1024) bias[i] = i < FW ? src[FW * FW + i] : 0.f;
+    for (int i = 3 * BPLANE * 2 + 112 * 4 + threadIdx.x * 4; i < FWD_WIMG; i += 1024 * 4)
         *reinterpret_cast<float*>(img + i) = 0.f;
 }
 
 hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_split_wimg, dim3(a.C * (a.net[0].nl + a.net[1].nl)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_split_wimg, dim3(a.C * (a.net[0].nl + a.net[1].nl)), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 
