@@ -71,6 +71,26 @@ __device__ __forceinline__ bf16x8 tr_frag(const unsigned char* plane, int tr_off
 // per-lane byte offset for tr_frag: lane 4qq + pp of group lg supplies row 4lg + qq, columns +4pp
 __device__ __forceinline__ int tr_lane_off(int lr, int lg) { return (4 * lg + (lr >> 2)) * PITCH + 8 * (lr & 3); }
 
+// LDS-DMA of 16 B per lane (global_load_lds_dwordx4: lane l's bytes land at lds_dst + 16 l) issued from inline
+// asm, so hipcc does not put it in its vmcnt bookkeeping: with the builtin form, hipcc waits vmcnt(0) before
+// the next LDS read of ANY buffer (it cannot prove the DMA target disjoint) -- which serialised the DMA
+// latency into every chunk. The issuing wave must wait for completion itself (s_waitcnt vmcnt(0)) before the
+// barrier that publishes the buffer. M0 is written and restored in the same statement.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, const void* lds_generic) {
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds_generic);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+// vmcnt(0) twice: through the builtin, so hipcc's waitcnt bookkeeping sees every earlier load retired (its
+// counted waits after this point do not wait on loads issued before it), and as asm volatile, which hipcc
+// cannot drop or merge -- the asm DMA it guards is invisible to its bookkeeping
+__device__ __forceinline__ void wait_vmcnt0() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);                 // vmcnt(0) expcnt(7) lgkmcnt(15)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // buffer resource over [p, p + bytes) from wave-uniform inputs (out-of-range loads read 0, stores drop)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
     const uint64_t a = reinterpret_cast<uint64_t>(p);

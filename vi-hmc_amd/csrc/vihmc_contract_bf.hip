@@ -81,13 +81,26 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
     // Q chunks: blocks of the pre-split image (vihmc_split_blocks), copied global -> LDS by the D waves
     // with wave-wide DMA (global_load_lds_dwordx4: 1 KB per instruction, no VGPRs, no VALU)
     const unsigned char* qblk = P.qimg + c * P.qimg_cs + (int64_t)(q_lo / CB_QC) * CB_BLOCK;
+#ifndef CB_ASM_DMA
+#define CB_ASM_DMA 1      // side B: asm LDS-DMA + G two chunks ahead (266 -> 237 us at C = 16)
+#endif
+#ifndef CBA_ASM_DMA
+#define CBA_ASM_DMA 0     // side A: the asm form measured 2 % slower (411 -> 419 us): builtin DMA kept
+#endif
+#if CBA_ASM_DMA
+#define VIHMC_CB_GLDS(CI, BUF)                                                                              \
+    for (int k = wave - 8; k < CB_GLDS; k += 8)                                                             \
+        bf6::glds16_asm(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16, smc + (BUF) * CB_QIMG + k * 1024);
+#else
 #define VIHMC_CB_GLDS(CI, BUF)                                                                              \
     for (int k = wave - 8; k < CB_GLDS; k += 8)                                                             \
         __builtin_amdgcn_global_load_lds(                                                                   \
             reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
             (__attribute__((address_space(3))) void*)(smc + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
+#endif
     if (wave >= 8 && nchunks > 0) {
         VIHMC_CB_GLDS(0, 0)
+        if (CBA_ASM_DMA) bf6::wait_vmcnt0();         // chunk 0 published by the first barrier
     }
 
     if (wave < 8) {
@@ -265,6 +278,8 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
                 if (CB_ABL != 2) dacc[t] = six(ga, qb, dacc[t]);
             }
         }
+        // chunk i+1 (asm DMA, issued at the top of this iteration) lands before the next barrier publishes it
+        if (CBA_ASM_DMA) bf6::wait_vmcnt0();
     }
     float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
 #pragma unroll
@@ -339,11 +354,17 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
     const int q_hi = min(q_lo + P.q_per_chunk, P.Mq);
     const int nchunks = q_hi > q_lo ? (q_hi - q_lo + CB_QC - 1) / CB_QC : 0;
     const unsigned char* qblk = P.qimg + c * P.qimg_cs + (int64_t)(q_lo / CB_QC) * CB_BLOCK;
+#if CB_ASM_DMA
+#define VIHMC_CBB_GLDS(CI, BUF)                                                                             \
+    for (int k = wave; k < CB_GLDS; k += 8)                                                                 \
+        bf6::glds16_asm(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16, smb + (BUF) * CB_QIMG + k * 1024);
+#else
 #define VIHMC_CBB_GLDS(CI, BUF)                                                                             \
     for (int k = wave; k < CB_GLDS; k += 8)                                                                 \
         __builtin_amdgcn_global_load_lds(                                                                   \
             reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
             (__attribute__((address_space(3))) void*)(smb + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
+#endif
 
     // G[q][o] for this lane: rows 4lg + jj (jj < 4) and 16 + 4lg + jj - 4 of the chunk, column o0+16s+lr;
     // buffer loads with the whole offset in the range-checked VGPR: rows past Mq read 0, rows past q_hi
@@ -369,9 +390,15 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
         }                                                                                                   \
     }
 
+    // G two chunks ahead in three register sets (named, rotated by a 3x unrolled loop), the image one chunk
+    // ahead by asm DMA, and every wave drains its own loads (vmcnt(0)) at the end of each chunk: the counted
+    // wait hipcc puts before the split of G(i) (its 32 newer loads) then never waits on this chunk's loads
+    float gc_[2][8];
     if (nchunks > 0) {
         VIHMC_CBB_GLDS(0, 0)
         VIHMC_CBB_GLOAD(ga_, 0)
+        if (nchunks > 1) VIHMC_CBB_GLOAD(gb_, 1)
+        if (CBA_ASM_DMA) bf6::wait_vmcnt0();
     }
     f32x4 dacc[2][7];
 #pragma unroll
@@ -381,10 +408,10 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
     const int tr_off = (4 * lg + (lr >> 2)) * CB_PITCH + 8 * (lr & 3);
     auto chunk = [&](int i, float (&gv)[2][8], float (&gn)[2][8]) __attribute__((always_inline)) {
         if (i >= nchunks) return;
-        __syncthreads();                      // chunk i landed (vmcnt(0)); buffer (i+1)%3 free
+        __syncthreads();                      // chunk i landed; buffer (i+1)%3 free
+        if (i + 2 < nchunks) VIHMC_CBB_GLOAD(gn, i + 2)
         if (i + 1 < nchunks) {
             VIHMC_CBB_GLDS(i + 1, (i + 1) % 3)
-            VIHMC_CBB_GLOAD(gn, i + 1)
         }
         const unsigned char* img = smb + (i % 3) * CB_QIMG;
         bf16x8 ga[2][3];
@@ -410,10 +437,12 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
             dacc[0][t] = six(ga[0], qb, dacc[0][t]);
             dacc[1][t] = six(ga[1], qb, dacc[1][t]);
         }
+        if (CB_ASM_DMA) bf6::wait_vmcnt0();   // this chunk's DMA (i+1) and G loads (i+2) done
     };
-    for (int i = 0; i < nchunks; i += 2) {
-        chunk(i, ga_, gb_);
+    for (int i = 0; i < nchunks; i += 3) {
+        chunk(i, ga_, gc_);
         chunk(i + 1, gb_, ga_);
+        chunk(i + 2, gc_, gb_);
     }
     float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
 #pragma unroll
