@@ -398,7 +398,7 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
         VIHMC_CBB_GLDS(0, 0)
         VIHMC_CBB_GLOAD(ga_, 0)
         if (nchunks > 1) VIHMC_CBB_GLOAD(gb_, 1)
-        if (CBA_ASM_DMA) bf6::wait_vmcnt0();
+        if (CB_ASM_DMA) bf6::wait_vmcnt0();          // chunk 0 published by the first barrier
     }
     f32x4 dacc[2][7];
 #pragma unroll
