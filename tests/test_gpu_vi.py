@@ -97,3 +97,39 @@ def test_burgers_training_step_timing(cuda_device):
         assert np.isfinite(l)
     finally:
         eng.close()
+
+
+def test_run_end_to_end_writes_artefacts(tmp_path, cuda_device):
+    """vi.run (main_VI_deeponet.run) for two epochs on a small synthetic Burgers problem, then the
+    sensitivity step on the exported posterior: the artefact files VI-HMC loads, in their formats."""
+    from types import SimpleNamespace
+    from vihmc import configs, sensitivity as S, vi
+    from vihmc.data import deeponet_problem, load_vi_artefacts
+    cfg = configs.load("burgers_vi", epochs=2, N_train=16, N_valid=8, batch_size=8, num_ens=2,
+                       save_loc=str(tmp_path), uid="t", width_branch=20, width_trunk=20, output_neurons=20,
+                       branch_depth=3, trunk_depth=3, in_branch=11)
+    spec_like = SimpleNamespace(width_branch=20, width_trunk=20, in_branch=11, in_trunk=5, depth_branch=3,
+                                depth_trunk=3, activation="tanh", output_neurons=20, impose_bc=True)
+    from vihmc.layout import DeepONetSpec
+    spec = DeepONetSpec(**vars(spec_like))
+    prob = deeponet_problem(seed=1, n=24, nt=6, nx=7, spec=spec)
+    grid = prob.trunk_in[0]
+    P = grid.shape[0]
+    cfg.p = P
+    tr = vi.BurgersDataSet(prob.branch_in[:16], grid, prob.y[:16], P, seed=0)
+    va = vi.BurgersDataSet(prob.branch_in[16:], grid, prob.y[16:], P, seed=1)
+    tl = torch.utils.data.DataLoader(tr, batch_size=8, shuffle=True)
+    vl = torch.utils.data.DataLoader(va, batch_size=8)
+    torch.manual_seed(0)
+    model, metrics = vi.run(cfg, tl, vl, 16 * P, 8 * P, grid, device=cuda_device, log=lambda s: None)
+    assert len(metrics) == 2 and all(np.isfinite(m).all() for m in np.asarray(metrics))
+    mu = torch.load(f"{tmp_path}/means_flattened_t", weights_only=True)
+    sd = torch.load(f"{tmp_path}/stds_flattened_t", weights_only=True)
+    assert mu.shape == (spec.n_params,) and sd.shape == mu.shape and bool((sd > 0).all())
+    pts = S.sample_points(8, P, 10, seed=2)
+    scores = S.sensitivity_scores(spec, prob.branch_in[16:], grid, pts, mu, sd, device=cuda_device)
+    ind = S.select_indices(scores, 0.9)
+    from vihmc.data import save_vi_artefacts
+    save_vi_artefacts(str(tmp_path), "t2", mu.numpy(), sd.numpy(), ind)
+    m2, s2, i2 = load_vi_artefacts(str(tmp_path), "t2")
+    assert np.array_equal(i2, ind) and np.all(np.diff(i2) > 0) and i2.size > 0
