@@ -161,6 +161,11 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
         }
     }
 
+#ifndef BB_PRIO
+#define BB_PRIO 2       // static wave priority: 1 dW waves (dispatched second) at 1: 69 -> 76 us; 2 dX waves at 1: 68.5 -> 67 us
+#endif
+    if (BB_PRIO == 1 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 512) __builtin_amdgcn_s_setprio(1);
+    if (BB_PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) < 512) __builtin_amdgcn_s_setprio(1);
     if (wave < 8) {
         // ---------------- dX role: i-tiles {2p, 2p+1} x row half h ----------------
         const int h = wave & 1, p2 = wave >> 1;

@@ -57,15 +57,48 @@ constexpr int CB_TAIL = 3 * CB_PLANE;              // fp32 [32][4] tail image of
 constexpr int CB_BLOCK = CONTRACT_SPLIT_BLOCK;     // 22528: 3 planes + tail, padded to 22 KB
 static_assert(CB_TAIL + CB_QC * 16 <= CB_BLOCK && CB_BLOCK % 1024 == 0, "split block layout");
 constexpr int CB_QIMG = CB_BLOCK;                  // bytes per Q buffer (one pre-split block)
-constexpr int CB_GIMG = 8 * 2 * 64 * 16;           // 8 S waves x 2 f32x4 x 64 lanes = 16384
-constexpr int CB_LDS = 3 * CB_QIMG + 2 * CB_GIMG;  // 98816
+#ifndef CBA_PRIO
+#define CBA_PRIO 0      // static wave priority: 1 D waves (the critical role, dispatched second) at 1: 418 -> 438 us;
+                        // 2 S waves at 1: no change
+#endif
+constexpr int CBA_DW = 8;                         // D waves (DMA stride)
+constexpr int CBA_THREADS = 1024;
+#ifndef CBA_GSPLIT
+#define CBA_GSPLIT 0      // 1: the S waves hand G over already split (3 bf16 planes): measured no change (412 vs 411 us)
+#endif
+// G image per buffer: 8 S waves x 64 lanes x (3 bf16x8 planes = 48 B, or 2 f32x4 = 32 B)
+constexpr int CB_GIMG = CBA_GSPLIT ? 8 * 3 * 64 * 16 : 8 * 2 * 64 * 16;
+constexpr int CB_LDS = 3 * CB_QIMG + 2 * CB_GIMG;  // 116736 (98816 unsplit)
 constexpr int CB_GLDS = CB_BLOCK / 1024;           // 22 wave-wide 16-B-per-lane DMA copies per block
 
 }  // namespace
 
-__global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
+#ifndef CB_STAMP
+#define CB_STAMP 0      // timing-only instrumentation (variant builds): in-kernel phase stamps, see below
+#endif
+#if CB_STAMP
+// every 64th workgroup: per wave and chunk, s_memtime at the barrier exit [0] and when the chunk's results
+// exist [1]; per workgroup s_memtime / s_memrealtime (100 MHz) at start and end (scripts/diag/stamps_side_a.py)
+constexpr int CBS_WG = 24, CBS_CH = 40;
+__device__ unsigned long long cb_stamps[CBS_WG][16][CBS_CH][2];
+__device__ unsigned long long cb_real[CBS_WG][2][2];
+#define VIHMC_CB_STAMP(I, K)                                                                                  \
+    if (samp && lane == 0 && (I) < CBS_CH) cb_stamps[sidx][wave][(I)][(K)] = __builtin_amdgcn_s_memtime();
+#else
+#define VIHMC_CB_STAMP(I, K)
+#endif
+
+__global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smc[];
     int b = blockIdx.x;
+#if CB_STAMP
+    const bool samp = (blockIdx.x % 64) == 0 && blockIdx.x / 64 < CBS_WG;
+    const int sidx = blockIdx.x / 64;
+    if (samp && threadIdx.x == 0) {
+        cb_real[sidx][0][0] = __builtin_amdgcn_s_memtime();
+        cb_real[sidx][0][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     const int per_chain = P.o_tiles * P.q_chunks;
     const int c = b / per_chain;
     b -= c * per_chain;
@@ -89,11 +122,11 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
 #endif
 #if CBA_ASM_DMA
 #define VIHMC_CB_GLDS(CI, BUF)                                                                              \
-    for (int k = wave - 8; k < CB_GLDS; k += 8)                                                             \
+    for (int k = wave - 8; k < CB_GLDS; k += CBA_DW)                                                        \
         bf6::glds16_asm(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16, smc + (BUF) * CB_QIMG + k * 1024);
 #else
 #define VIHMC_CB_GLDS(CI, BUF)                                                                              \
-    for (int k = wave - 8; k < CB_GLDS; k += 8)                                                             \
+    for (int k = wave - 8; k < CB_GLDS; k += CBA_DW)                                                        \
         __builtin_amdgcn_global_load_lds(                                                                   \
             reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
             (__attribute__((address_space(3))) void*)(smc + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
@@ -105,6 +138,7 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
 
     if (wave < 8) {
         // ---------------- S role ----------------
+        if (CBA_PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) < 512) __builtin_amdgcn_s_setprio(1);
         const float* Own = P.Own + c * P.own_cs;
         const float* Yc = P.Y + c * P.y_cs;
         const float b0 = P.b0[c * P.b0_cs];
@@ -155,12 +189,13 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
         auto s_chunk = [&](int i, float (&yv)[2][4], float (&yn)[2][4]) __attribute__((always_inline)) {
             if (i > nchunks) return;                // same barrier count as the D role
             __syncthreads();
+            VIHMC_CB_STAMP(i, 0)
             if (i < nchunks) {
                 const int q0 = q_lo + i * CB_QC;
                 const bool full = q0 + CB_QC <= q_hi;
                 const unsigned char* img = smc + (i % 3) * CB_QIMG;
                 VIHMC_CB_YLOAD(yn, min(i + 1, nchunks - 1))
-                f32x4* gdst = reinterpret_cast<f32x4*>(smc + 3 * CB_QIMG + (i & 1) * CB_GIMG) + w * 128;
+                unsigned char* gimg = smc + 3 * CB_QIMG + (i & 1) * CB_GIMG + w * (CB_GIMG / 8);
                 float ps = 0.f;
                 f32x4 gs[2];
 #pragma unroll
@@ -189,8 +224,18 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
                         ps = fmaf(rv, rv, ps);
                         gsum += (double)g[r];  // G terms cancel: exact-order fp64, not fp32 partials
                     }
-                    gdst[sub * 64 + lane] = g;
+                    if (!CBA_GSPLIT) reinterpret_cast<f32x4*>(gimg)[sub * 64 + lane] = g;
                     gs[sub] = g;
+                }
+                if (CBA_GSPLIT) {
+                    // the D partner's A operand, planes [3][64 lanes] of bf16x8 (sub 0 -> slots 0..3)
+                    bf16x4 l0, l1, l2, h0, h1, h2;
+                    split4(gs[0], l0, l1, l2);
+                    split4(gs[1], h0, h1, h2);
+                    bf16x8* gp = reinterpret_cast<bf16x8*>(gimg) + lane;
+                    gp[0] = cat8(l0, h0);
+                    gp[64] = cat8(l1, h1);
+                    gp[128] = cat8(l2, h2);
                 }
                 if (P.gout && CB_ABL != 1) {
                     // Whole 128-B lines per store: lanes lr and lr ^ 8 swap halves (DPP row_ror:8), so
@@ -225,6 +270,10 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
                 }
                 // sum r^2 (no cancellation): per-chunk fp32 partial of 8 terms per lane, then fp64
                 ssq += (double)ps;
+#if CB_STAMP
+                asm volatile("" :: "v"(ps));
+                VIHMC_CB_STAMP(i, 1)
+#endif
             }
         };
         for (int i = 0; i <= nchunks; i += 2) {
@@ -247,12 +296,14 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
     }
 
     // ---------------- D role ----------------
+    if (CBA_PRIO == 1 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 512) __builtin_amdgcn_s_setprio(1);
     f32x4 dacc[7];
 #pragma unroll
     for (int t = 0; t < 7; ++t) dacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int tro = bf6::tr_lane_off(lr, lg);
     for (int i = 0; i <= nchunks; ++i) {
         __syncthreads();
+        VIHMC_CB_STAMP(i, 0)
         // chunk i+1 -> buffer (i+1)%3 (last read by this role in iteration i-1, by S in i-2); the copies
         // land while this iteration computes and are drained by the next barrier (vmcnt(0))
         if (i + 1 < nchunks) {
@@ -260,9 +311,15 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
         }
         if (i >= 1) {
             const unsigned char* img = smc + ((i - 1) % 3) * CB_QIMG;
-            const f32x4* gsrc = reinterpret_cast<const f32x4*>(smc + 3 * CB_QIMG + ((i - 1) & 1) * CB_GIMG) + w * 128;
+            const unsigned char* gimg = smc + 3 * CB_QIMG + ((i - 1) & 1) * CB_GIMG + w * (CB_GIMG / 8);
             bf16x8 ga[3];
-            {
+            if (CBA_GSPLIT) {
+                const bf16x8* gp = reinterpret_cast<const bf16x8*>(gimg) + lane;
+                ga[0] = gp[0];
+                ga[1] = gp[64];
+                ga[2] = gp[128];
+            } else {
+                const f32x4* gsrc = reinterpret_cast<const f32x4*>(gimg);
                 bf16x4 l0, l1, l2, h0, h1, h2;
                 split4(gsrc[lane], l0, l1, l2);          // sub 0
                 split4(gsrc[64 + lane], h0, h1, h2);     // sub 1
@@ -277,6 +334,10 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
                 for (int p = 0; p < 3; ++p) qb[p] = bf6::tr_frag(img + p * CB_PLANE, tro, 16 * t);
                 if (CB_ABL != 2) dacc[t] = six(ga, qb, dacc[t]);
             }
+#if CB_STAMP
+            asm volatile("" :: "v"(dacc[0]), "v"(dacc[6]));
+            VIHMC_CB_STAMP(i, 1)
+#endif
         }
         // chunk i+1 (asm DMA, issued at the top of this iteration) lands before the next barrier publishes it
         if (CBA_ASM_DMA) bf6::wait_vmcnt0();
@@ -292,6 +353,12 @@ __global__ __launch_bounds__(1024, 1) void k_contract_bf(ContractProb P) {
             if (oo < P.Mo) out[(int64_t)oo * P.ldout + j] = (j < 100) ? dacc[t][r] : 0.f;
         }
     }
+#if CB_STAMP
+    if (samp && wave == 8 && lane == 0) {
+        cb_real[sidx][1][0] = __builtin_amdgcn_s_memtime();
+        cb_real[sidx][1][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 #undef VIHMC_CB_GLDS
 #undef VIHMC_CB_YLOAD
 }
@@ -461,6 +528,15 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
 #undef VIHMC_CBB_GLOAD
 }
 
+#if CB_STAMP
+extern "C" int vihmc_debug_cb_stamps(void* stamps, size_t stamp_bytes, void* real, size_t real_bytes) {
+    if (stamp_bytes != sizeof(cb_stamps) || real_bytes != sizeof(cb_real)) return -1;
+    hipError_t e = hipMemcpyFromSymbol(stamps, HIP_SYMBOL(cb_stamps), stamp_bytes, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(real, HIP_SYMBOL(cb_real), real_bytes, 0, hipMemcpyDeviceToHost);
+    return (int)e;
+}
+#endif
+
 hipError_t launch_contract_bf_b(const ContractProb& p, int C, hipStream_t s) {
     if (p.W != 100 || !p.load_g || !p.qimg || p.q_per_chunk % CB_QC) return hipErrorInvalidValue;
     dim3 g(C * p.o_tiles * p.q_chunks), blk(512);
@@ -470,7 +546,7 @@ hipError_t launch_contract_bf_b(const ContractProb& p, int C, hipStream_t s) {
 
 hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s) {
     if (p.W != 100 || p.load_g || !p.qimg || p.q_per_chunk % CB_QC) return hipErrorInvalidValue;
-    dim3 g(C * p.o_tiles * p.q_chunks), blk(1024);
+    dim3 g(C * p.o_tiles * p.q_chunks), blk(CBA_THREADS);
     hipLaunchKernelGGL(k_contract_bf, g, blk, CB_LDS, s, p);
     return hipGetLastError();
 }
