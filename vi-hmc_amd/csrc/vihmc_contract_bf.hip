@@ -80,7 +80,7 @@ constexpr int CB_GLDS = CB_BLOCK / 1024;           // 22 wave-wide 16-B-per-lane
 // every 64th workgroup: per wave and chunk, s_memtime at the barrier exit [0] and when the chunk's results
 // exist [1]; per workgroup s_memtime / s_memrealtime (100 MHz) at start and end (scripts/diag/stamps_side_a.py)
 constexpr int CBS_WG = 24, CBS_CH = 40;
-__device__ unsigned long long cb_stamps[CBS_WG][16][CBS_CH][2];
+__device__ unsigned long long cb_stamps[CBS_WG][16][CBS_CH][3];
 __device__ unsigned long long cb_real[CBS_WG][2][2];
 #define VIHMC_CB_STAMP(I, K)                                                                                  \
     if (samp && lane == 0 && (I) < CBS_CH) cb_stamps[sidx][wave][(I)][(K)] = __builtin_amdgcn_s_memtime();
@@ -226,6 +226,12 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                     }
                     if (!CBA_GSPLIT) reinterpret_cast<f32x4*>(gimg)[sub * 64 + lane] = g;
                     gs[sub] = g;
+#if CB_STAMP
+                    if (sub == 0) {
+                        asm volatile("" :: "v"(g));
+                        VIHMC_CB_STAMP(i, 2)
+                    }
+#endif
                 }
                 if (CBA_GSPLIT) {
                     // the D partner's A operand, planes [3][64 lanes] of bf16x8 (sub 0 -> slots 0..3)
@@ -327,6 +333,10 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                 ga[1] = cat8(l1, h1);
                 ga[2] = cat8(l2, h2);
             }
+#if CB_STAMP
+            asm volatile("" :: "v"(ga[0]), "v"(ga[2]));
+            VIHMC_CB_STAMP(i, 2)
+#endif
 #pragma unroll
             for (int t = 0; t < 7; ++t) {
                 bf16x8 qb[3];

@@ -233,8 +233,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused(FusedArgs args) {
 //   k order: 16x16x32 k-block kb covers the column tiles t0 = 2kb, t1 = 2kb + 1; lane (l&15, g = l>>4)
 //   holds slots 8g..8g+7 = h[m][16 t0 + 4g + 0..3] and h[m][16 t1 + 4g + 0..3] -- exactly registers
 //   0..3 of accumulators t0 and t1 of the previous layer, so activations need no lane movement. The
-//   weights are stored in LDS in that permuted order (one b128 per plane per fragment). Tile 6 (columns
-//   96..111, 96..99 real) uses the 16x16x16 bf16 MFMA, whose k layout 4g + j is the accumulator's.
+//   weights are stored in LDS in that permuted order (one b128 per plane per fragment). The k tail
+//   (columns 96..99) is one exact 16x16x4 f32 MFMA per tile (FWD_TAILF32, below; the FWD_TAILF32 = 0 form
+//   runs six 16x16x16 bf16 MFMAs, whose k layout 4g + j is the accumulator's).
 // =============================================================================================
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -355,6 +356,73 @@ __device__ __forceinline__ void bf_split_operand(const float4 (&h)[7], bf16x8 (&
     }
 }
 
+// ---- f32 k tail (FWD_TAILF32): the 4-long k tail (features 96..99) as ONE exact 16x16x4 f32 MFMA that seeds
+// each tile's accumulator, instead of six 16x16x16 bf16 MFMAs -- which issue at 16 cycles each on gfx950, the
+// same as a 16x16x32 (scripts/diag/mfma_rate.hip): 6 x 16 = 96 -> 32 matrix cycles per tile. Its B operand
+// B[k = lg][m = lr] = h[m][96 + lg] must sit in lane (lr, lg): tile 6's A rows are W rows 96 + (lr >> 2)
+// (rows 4g .. 4g+3 all W row 96 + g), so accumulator register 0 of lane (lr, lg) is exactly h[lr][96 + lg] --
+// no cross-lane move. The image carries the fp32 tail W[n][96..99] ([100][4] after the bias).
+#ifndef FWD_TAILF32
+#define FWD_TAILF32 1
+#endif
+#ifndef FWD_DMA_ONLY
+#define FWD_DMA_ONLY 0     // timing builds: the register-staging path compiled out with FWD_TAILF32 = 0 too
+#endif
+#ifndef FWD_TF_SCHED
+#define FWD_TF_SCHED 0     // 1: sched_barrier between tile pairs (fewer spills, 257-262 vs 256 us: not kept)
+#endif
+constexpr int FWD_WTAIL = 3 * BPLANE * 2 + 112 * 4;   // byte offset of the fp32 W tail [100][4] in an image
+
+__device__ __forceinline__ int tf_row(int t, int lr) { return t < 6 ? 16 * t + lr : 96 + (lr >> 2); }
+
+__device__ __forceinline__ f32x4 tf_tile(const __bf16* wb, const float* wtail, int t, int lr, int lg,
+                                         const bf16x8 (&hp)[3][3], float h6) {
+    const int n = tf_row(t, lr);
+    const __bf16* row0 = wb + n * BROW;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 3; ++kb) {
+        const int o = kb * 32 + lg * 8;
+        const bf16x8 w0 = *reinterpret_cast<const bf16x8*>(row0 + o);
+        const bf16x8 w1 = *reinterpret_cast<const bf16x8*>(row0 + BPLANE + o);
+        const bf16x8 w2 = *reinterpret_cast<const bf16x8*>(row0 + 2 * BPLANE + o);
+        acc = mfma32(w2, hp[0][kb], acc);
+        acc = mfma32(w1, hp[1][kb], acc);
+        acc = mfma32(w0, hp[2][kb], acc);
+        acc = mfma32(w1, hp[0][kb], acc);
+        acc = mfma32(w0, hp[1][kb], acc);
+        acc = mfma32(w0, hp[0][kb], acc);
+    }
+    // the tail closes the chain (as the last MFMA it cannot be hoisted ahead of the tile: no extra live
+    // accumulators; seeding the chain with it spilled 67 VGPRs)
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(wtail[4 * n + lg], h6, acc, 0, 0, 0);
+}
+
+template <int ACT>
+__device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, const float* wtail,
+                                         const bf16x8 (&hp)[3][3], float h6, int lr, int lg,
+                                         __amdgpu_buffer_rsrc_t orsrc, uint32_t ooff, float4 (&hn)[7]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+        const f32x4 a0 = tf_tile(wb, wtail, 2 * p, lr, lg, hp, h6);
+        const f32x4 a1 = tf_tile(wb, wtail, 2 * p + 1, lr, lg, hp, h6);
+        hn[2 * p] = bf_epi<ACT>(bias, 2 * p, lg, a0, orsrc, ooff);
+        hn[2 * p + 1] = bf_epi<ACT>(bias, 2 * p + 1, lg, a1, orsrc, ooff);
+#if FWD_TF_SCHED
+        __builtin_amdgcn_sched_barrier(0);     // keep the scheduler from hoisting later tiles (VGPR pressure)
+#endif
+    }
+    // tile 6: register 0 of lane (lr, lg) = pre-activation of h[lr][96 + lg]
+    const f32x4 a6 = tf_tile(wb, wtail, 6, lr, lg, hp, h6);
+    const float v = act_t<ACT>(a6[0] + bias[96 + lg]);
+#if FWD_ABL == 1
+    asm volatile("" :: "v"(v));
+#else
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, ooff == OOB ? OOB : ooff + 4u * (96 + lg), 0, 0);
+#endif
+    hn[6].x = v;
+}
+
 template <int NW>
 __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
     constexpr int FTHREADS = NW * 64;
@@ -424,7 +492,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
 
     // pre-split weight images (k_split_wimg): layer j's image is DMA-copied into buffer j&1 one layer ahead
     // (global_load_lds, 1 KB per wave-instruction, no VGPRs / VALU); the barrier drains it (vmcnt(0))
-    const bool dma = N.wimg != nullptr;
+    const bool dma = FWD_TAILF32 || FWD_DMA_ONLY || N.wimg != nullptr;  // FWD_TAILF32: images only (host-checked)
     const unsigned char* wimgc = dma ? N.wimg + c * N.wimg_cs : nullptr;
 #define VIHMC_FB_DMA(J, BUF)                                                                          \
     for (int k = wave; k < FWD_WIMG / 1024; k += NW)                                                  \
@@ -441,7 +509,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         const float* ar = N.in + c * N.in_cs + (int64_t)rowc * N.ldin;
 #pragma unroll
         for (int t = 0; t < 6; ++t) h[t] = *reinterpret_cast<const float4*>(ar + 16 * t + 4 * lg);
-        h[6] = lg == 0 ? *reinterpret_cast<const float4*>(ar + 96) : float4{0.f, 0.f, 0.f, 0.f};
+        if (FWD_TAILF32) h[6] = float4{ar[96 + lg], 0.f, 0.f, 0.f};
+        else h[6] = lg == 0 ? *reinterpret_cast<const float4*>(ar + 96) : float4{0.f, 0.f, 0.f, 0.f};
     }
     __syncthreads();                            // zero fill done before the staging writes
     if (!dma) {
@@ -465,12 +534,22 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         const float* bias = reinterpret_cast<const float*>(bbuf + 3 * BPLANE * 2);
         const __amdgpu_buffer_rsrc_t orsrc = make_rsrc(outc + N.h_off[j], obytes);
         bf16x8 hp[3][3];
-        bf16x4 h6[3];
-        bf_split_operand(h, hp, h6);
         const int act = N.act[j];
-        if (act == ACT_TANH) bf_layer<ACT_TANH>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
-        else if (act == ACT_RELU) bf_layer<ACT_RELU>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
-        else bf_layer<ACT_ID>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
+        if (FWD_TAILF32) {
+            bf16x4 h6u[3];
+            bf_split_operand(h, hp, h6u);          // tile 6 planes unused (the f32 MFMA takes h[6].x)
+            const float* wtail = reinterpret_cast<const float*>(bbuf + FWD_WTAIL);
+            const float h6f = h[6].x;
+            if (act == ACT_TANH) tf_layer<ACT_TANH>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
+            else if (act == ACT_RELU) tf_layer<ACT_RELU>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
+            else tf_layer<ACT_ID>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
+        } else {
+            bf16x4 h6[3];
+            bf_split_operand(h, hp, h6);
+            if (act == ACT_TANH) bf_layer<ACT_TANH>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
+            else if (act == ACT_RELU) bf_layer<ACT_RELU>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
+            else bf_layer<ACT_ID>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
+        }
         if (!dma) {
             VIHMC_FB_STORE((j + 1) & 1)
         }
@@ -521,7 +600,10 @@ __global__ __launch_bounds__(1024) void k_split_wimg(FusedArgs args) {
     }
     float* bias = reinterpret_cast<float*>(img + 3 * BPLANE * 2);
     for (int i = threadIdx.x; i < 112; i += 1024) bias[i] = i < FW ? src[FW * FW + i] : 0.f;
-    for (int i = 3 * BPLANE * 2 + 112 * 4 + threadIdx.x * 4; i < FWD_WIMG; i += 1024 * 4)
+    // fp32 k tail W[n][96..99] (FWD_TAILF32), then zeros to the end of the image
+    float* wtail = reinterpret_cast<float*>(img + FWD_WTAIL);
+    for (int i = threadIdx.x; i < FW * 4; i += 1024) wtail[i] = src[(i >> 2) * FW + 96 + (i & 3)];
+    for (int i = FWD_WTAIL + FW * 16 + threadIdx.x * 4; i < FWD_WIMG; i += 1024 * 4)
         *reinterpret_cast<float*>(img + i) = 0.f;
 }
 
@@ -531,7 +613,9 @@ hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s) {
 }
 
 size_t fwd_fused_bf_lds_bytes() { return 2 * (size_t)FWD_WIMG; }
-static_assert(BBUF <= FWD_WIMG && FWD_WIMG % 1024 == 0 && 2 * FWD_WIMG <= 160 * 1024, "weight image");
+static_assert(BBUF <= FWD_WIMG && FWD_WTAIL + FW * 16 <= FWD_WIMG && FWD_WIMG % 1024 == 0 &&
+              2 * FWD_WIMG <= 160 * 1024, "weight image");
+bool fwd_fused_bf_needs_wimg() { return FWD_TAILF32 != 0; }
 
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s) {
     dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk));

@@ -156,6 +156,7 @@ struct FusedArgs {
 constexpr int FWD_WIMG = 69632;                     // one pre-split weight image: 3 x [100][112] bf16 + fp32
                                                     // bias [112], zero padded to 68 KB (whole 1-KB DMA pieces)
 hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s);
+bool fwd_fused_bf_needs_wimg();                     // the bf16x6 forward reads the fp32 k tail of the image
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s);             // bf16x6, 12 waves
 size_t fwd_fused_lds_bytes();

@@ -36,7 +36,7 @@ def main():
     for _ in range(5):
         eng.logp_grad(th)
     torch.cuda.synchronize()
-    st = np.zeros((WG, 16, CH, 2), np.uint64)
+    st = np.zeros((WG, 16, CH, 3), np.uint64)
     rl = np.zeros((WG, 2, 2), np.uint64)
     f = _lib.lib().vihmc_debug_cb_stamps
     f.restype = ctypes.c_int
@@ -51,10 +51,11 @@ def main():
     print(f"workgroups sampled: {ok.sum()}  duration {us.mean():.1f} us  shader clock {np.mean(cyc / us) / 1e3:.3f} GHz "
           f"(min {np.min(cyc / us) / 1e3:.3f}, max {np.max(cyc / us) / 1e3:.3f})")
     nch = 33   # 32 chunks + the D role's trailing iteration
-    per, s_work, d_work, skew, s_late, d_late = [], [], [], [], [], []
+    per, s_work, d_work, skew, s_late, d_late, s_mid, d_mid = [], [], [], [], [], [], [], []
     for g in np.nonzero(ok)[0]:
         bar = st[g, :, :nch, 0]
         end = st[g, :, :nch, 1]
+        mid = st[g, :, :nch, 2]
         for i in range(1, nch - 1):
             t0 = bar[:, i].min()
             per.append(bar[:, i + 1].min() - t0)
@@ -62,6 +63,8 @@ def main():
             s_work.append(np.mean(end[:8, i] - bar[:8, i]))
             d_work.append(np.mean(end[8:, i] - bar[8:, i]))
             s_late.append(np.max(end[:8, i]) - t0)
+            s_mid.append(np.mean(mid[:8, i] - bar[:8, i]))
+            d_mid.append(np.mean(mid[8:, i] - bar[8:, i]))
             d_late.append(np.max(end[8:, i]) - t0)
     f = lambda a: f"{np.mean(a):7.0f} (p10 {np.percentile(a, 10):6.0f}, p90 {np.percentile(a, 90):6.0f})"  # noqa: E731
     print("cycles per chunk (shader clock), steady-state chunks 1..31:")
@@ -69,13 +72,16 @@ def main():
     print(f"  barrier-exit skew            {f(skew)}")
     print(f"  S role work (mean wave)      {f(s_work)}")
     print(f"  D role work (mean wave)      {f(d_work)}")
+    print(f"  S role first sub-tile done   {f(s_mid)}")
+    print(f"  D role G split done          {f(d_mid)}")
     print(f"  S role last wave done        {f(s_late)}")
     print(f"  D role last wave done        {f(d_late)}")
     g0 = int(np.nonzero(ok)[0][0])
-    print("workgroup", g0, "chunk 5, per wave: barrier exit / done, relative to the first exit")
+    print("workgroup", g0, "chunk 5, per wave: barrier exit / mid (S: first sub-tile, D: G split) / done, from the first exit")
     t0 = st[g0, :, 5, 0].min()
     for w in range(16):
-        print(f"  wave {w:2d} {'S' if w < 8 else 'D'}  {st[g0, w, 5, 0] - t0:6.0f} {st[g0, w, 5, 1] - t0:6.0f}")
+        print(f"  wave {w:2d} {'S' if w < 8 else 'D'}  {st[g0, w, 5, 0] - t0:6.0f} {st[g0, w, 5, 2] - t0:6.0f} "
+              f"{st[g0, w, 5, 1] - t0:6.0f}")
     eng.close()
 
 
