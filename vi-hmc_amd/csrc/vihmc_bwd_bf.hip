@@ -27,6 +27,11 @@
                     // from LDS per sub-tile, 6 no LDS plane stores after the first sub-tile, 7 no dX (Dout) stores
 #endif
 
+#ifndef BB_WREG
+#define BB_WREG 2         // dX waves keep W^T fragments in registers (loaded once) instead of LDS re-reads:
+                          // 1 both i-tiles (spills at 128 VGPRs), 2 the first i-tile only
+#endif
+
 #ifndef BB_WPITCH_B
 #define BB_WPITCH_B 224   // W^T plane row pitch (bytes)
 #endif
@@ -175,9 +180,26 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
         const unsigned char* wrow1 = smw + BB_W + min(16 * (t0 + 1) + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
         const float* wtl = reinterpret_cast<const float*>(smw + BB_WT);
         const int wr0 = min(16 * t0 + lr, P.n_in - 1), wr1 = min(16 * (t0 + 1) + lr, P.n_in - 1);
+#if BB_WREG
+        bf16x8 wra[3][3], wrb[3][3];                   // [kb][plane] W^T fragments, loaded once (after barrier 0)
+        float wta = 0.f, wtb = 0.f;
+#endif
         for (int i = 0; i < nsub; ++i) {
             const int sub = r0 + i * BB_SUB;
             __syncthreads();                           // buffer i&1 holds sub-tile i
+#if BB_WREG
+            if (i == 0 && P.has_dx) {
+#pragma unroll
+                for (int kb = 0; kb < 3; ++kb)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        wra[kb][p] = *reinterpret_cast<const bf16x8*>(wrow0 + p * BB_WPLANE + 64 * kb);
+                        if (BB_WREG == 1) wrb[kb][p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
+                    }
+                wta = wtl[wr0 * 4 + lg];
+                wtb = wtl[wr1 * 4 + lg];
+            }
+#endif
             if (i + 1 < nsub) {
                 VIHMC_BB_STORE(sub + BB_SUB, (i + 1) & 1)
                 if (i + 2 < nsub && BB_ABL != 1) {
@@ -190,9 +212,29 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
             // the exact f32 tail (features 96..99) seeds each accumulator
             const float dtl = reinterpret_cast<const float*>(buf + BB_DT)[(16 * h + lr) * 4 + lg];
             f32x4 acc[2];
+#if BB_WREG
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wta, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            acc[1] = two ? __builtin_amdgcn_mfma_f32_16x16x4f32(wtb, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kb = 0; kb < 3; ++kb) {
+                bf16x8 db[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) db[p] = *reinterpret_cast<const bf16x8*>(drow + p * BB_PLANE + 64 * kb);
+                acc[0] = six(wra[kb], db, acc[0]);
+                if (BB_WREG == 2) {
+                    // only the first i-tile's W^T in registers (VGPR budget); the second re-read from LDS
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) wrb[kb][p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
+                }
+                if (two) acc[1] = six(wrb[kb], db, acc[1]);
+            }
+            if (false)
+#else
             acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wtl[wr0 * 4 + lg], dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             acc[1] = two ? __builtin_amdgcn_mfma_f32_16x16x4f32(wtl[wr1 * 4 + lg], dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0)
                          : f32x4{0.f, 0.f, 0.f, 0.f};
+#endif
 #pragma unroll
             for (int kb = 0; kb < 3; ++kb) {
                 bf16x8 db[3], wa[3], wb[3];
