@@ -27,6 +27,10 @@
                     // from LDS per sub-tile, 6 no LDS plane stores after the first sub-tile, 7 no dX (Dout) stores
 #endif
 
+#ifndef BB_ROW32
+#define BB_ROW32 1        // staging slots row-aligned (32 per row) instead of packed 25 per row
+#endif
+
 #ifndef BB_WREG
 #define BB_WREG 2         // dX waves keep W^T fragments in registers (loaded once) instead of LDS re-reads:
                           // 1 both i-tiles (spills at 128 VGPRs), 2 the first i-tile only
@@ -107,9 +111,20 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
     }
 
     // ---- staging geometry: slot v of this thread moves float4 (row, c4) of D (idx < 800) or H ----
-    const int ntot = BB_SUB * 25 + BB_SUB * hq4;
     int st[BB_SLOTS];                                  // (row << 8) | c4, -1 idle
     unsigned st_d = 0;
+#if BB_ROW32
+    // slot 0 = D, slot 1 = H, 32 slots per row (c4 = tid & 31; 25 / hq4 of them active): the 16-lane groups of
+    // the bf16x4 plane stores never straddle two rows (25 float4 per row did: 2-way bank conflicts)
+    static_assert(BB_SLOTS == 2 && BB_SUB * 32 == BB_THREADS, "row-aligned staging map");
+#pragma unroll
+    for (int v = 0; v < BB_SLOTS; ++v) {
+        const int r = tid >> 5, c4 = tid & 31;
+        st[v] = c4 < (v == 0 ? 25 : hq4) ? (r << 8) | c4 : -1;
+    }
+    st_d = 1u;
+#else
+    const int ntot = BB_SUB * 25 + BB_SUB * hq4;
 #pragma unroll
     for (int v = 0; v < BB_SLOTS; ++v) {
         const int idx = tid + BB_THREADS * v;
@@ -120,13 +135,14 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
         st[v] = idx < ntot ? (r << 8) | c4 : -1;
         st_d |= (isd ? 1u : 0u) << v;
     }
+#endif
     f32x4 pf[BB_SLOTS];
     f32x4 dcol = {0.f, 0.f, 0.f, 0.f};                 // db partial of this thread's D slot (slot 0 only:
                                                        // idx < 800 < 1024)
 #define VIHMC_BB_LOAD(SUB)                                                                              \
     _Pragma("unroll") for (int v = 0; v < BB_SLOTS; ++v) {                                              \
         const int row = min((SUB) + (max(st[v], 0) >> 8), P.M - 1);                                     \
-        const int c4 = st[v] & 255;                                                                     \
+        const int c4 = max(st[v], 0) & 255;            /* idle slots read column 0: in bounds */        \
         pf[v] = ((st_d >> v) & 1) ? reinterpret_cast<const f32x4*>(D + (int64_t)row * P.ldd)[c4]        \
                                   : reinterpret_cast<const f32x4*>(H + (int64_t)row * P.ldh)[c4];       \
     }

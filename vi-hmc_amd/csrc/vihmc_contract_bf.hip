@@ -68,7 +68,12 @@ constexpr int CBA_THREADS = 1024;
 #endif
 // G image per buffer: 8 S waves x 64 lanes x (3 bf16x8 planes = 48 B, or 2 f32x4 = 32 B)
 constexpr int CB_GIMG = CBA_GSPLIT ? 8 * 3 * 64 * 16 : 8 * 2 * 64 * 16;
-constexpr int CB_LDS = 3 * CB_QIMG + 2 * CB_GIMG;  // 116736 (98816 unsplit)
+#ifndef CBA_PIPE
+#define CBA_PIPE 0      // 1: 4 Q buffers, asm LDS-DMA two chunks ahead kept in flight across raw barriers
+                        // (counted vmcnt, no vmcnt(0) at every __syncthreads)
+#endif
+constexpr int CB_NQBUF = CBA_PIPE ? 4 : 3;
+constexpr int CB_LDS = CB_NQBUF * CB_QIMG + 2 * CB_GIMG;  // 98816 (3 buffers, unsplit G), 121344 (4)
 constexpr int CB_GLDS = CB_BLOCK / 1024;           // 22 wave-wide 16-B-per-lane DMA copies per block
 
 }  // namespace
@@ -120,7 +125,19 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
 #ifndef CBA_ASM_DMA
 #define CBA_ASM_DMA 0     // side A: the asm form measured 2 % slower (411 -> 419 us): builtin DMA kept
 #endif
-#if CBA_ASM_DMA
+#if CBA_PIPE
+    // raw barrier: LDS traffic of this wave retired (G image writes, reads of buffers about to be refilled),
+    // VMEM left in flight (the DMA two chunks ahead, the S waves' y loads and G^T stores)
+#define VIHMC_CB_BAR()                                                                                      \
+    {                                                                                                       \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                  \
+        __builtin_amdgcn_s_barrier();                                                                       \
+        asm volatile("" ::: "memory");                                                                      \
+    }
+#else
+#define VIHMC_CB_BAR() __syncthreads();
+#endif
+#if CBA_ASM_DMA || CBA_PIPE
 #define VIHMC_CB_GLDS(CI, BUF)                                                                              \
     for (int k = wave - 8; k < CB_GLDS; k += CBA_DW)                                                        \
         bf6::glds16_asm(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16, smc + (BUF) * CB_QIMG + k * 1024);
@@ -131,9 +148,21 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
             reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
             (__attribute__((address_space(3))) void*)(smc + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
 #endif
+    // DMA pieces per D wave and chunk: k = d, d + 8, d + 16 < 22 (scalar: the counted waits are immediates)
+    const int dpieces = __builtin_amdgcn_readfirstlane(wave - 8) < CB_GLDS - 16 ? 3 : 2;
     if (wave >= 8 && nchunks > 0) {
         VIHMC_CB_GLDS(0, 0)
-        if (CBA_ASM_DMA) bf6::wait_vmcnt0();         // chunk 0 published by the first barrier
+        if (CBA_PIPE) {
+            if (nchunks > 1) {
+                VIHMC_CB_GLDS(1, 1)
+                if (dpieces == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");   // chunk 0 landed
+                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                bf6::wait_vmcnt0();
+            }
+        } else if (CBA_ASM_DMA) {
+            bf6::wait_vmcnt0();                      // chunk 0 published by the first barrier
+        }
     }
 
     if (wave < 8) {
@@ -188,14 +217,14 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
         VIHMC_CB_YLOAD(ya, 0)
         auto s_chunk = [&](int i, float (&yv)[2][4], float (&yn)[2][4]) __attribute__((always_inline)) {
             if (i > nchunks) return;                // same barrier count as the D role
-            __syncthreads();
+            VIHMC_CB_BAR()
             VIHMC_CB_STAMP(i, 0)
             if (i < nchunks) {
                 const int q0 = q_lo + i * CB_QC;
                 const bool full = q0 + CB_QC <= q_hi;
-                const unsigned char* img = smc + (i % 3) * CB_QIMG;
+                const unsigned char* img = smc + (i % CB_NQBUF) * CB_QIMG;
                 VIHMC_CB_YLOAD(yn, min(i + 1, nchunks - 1))
-                unsigned char* gimg = smc + 3 * CB_QIMG + (i & 1) * CB_GIMG + w * (CB_GIMG / 8);
+                unsigned char* gimg = smc + CB_NQBUF * CB_QIMG + (i & 1) * CB_GIMG + w * (CB_GIMG / 8);
                 float ps = 0.f;
                 f32x4 gs[2];
 #pragma unroll
@@ -308,16 +337,22 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
     for (int t = 0; t < 7; ++t) dacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int tro = bf6::tr_lane_off(lr, lg);
     for (int i = 0; i <= nchunks; ++i) {
-        __syncthreads();
+        VIHMC_CB_BAR()
         VIHMC_CB_STAMP(i, 0)
         // chunk i+1 -> buffer (i+1)%3 (last read by this role in iteration i-1, by S in i-2); the copies
-        // land while this iteration computes and are drained by the next barrier (vmcnt(0))
-        if (i + 1 < nchunks) {
-            VIHMC_CB_GLDS(i + 1, (i + 1) % 3)
+        // land while this iteration computes and are drained by the next barrier (vmcnt(0)).
+        // CBA_PIPE: chunk i+2 -> buffer (i+2)%4 (last read by S in i-2, by this role in i-1), waited for at
+        // the end of iteration i+1
+        if (CBA_PIPE) {
+            if (i + 2 < nchunks) {
+                VIHMC_CB_GLDS(i + 2, (i + 2) % CB_NQBUF)
+            }
+        } else if (i + 1 < nchunks) {
+            VIHMC_CB_GLDS(i + 1, (i + 1) % CB_NQBUF)
         }
         if (i >= 1) {
-            const unsigned char* img = smc + ((i - 1) % 3) * CB_QIMG;
-            const unsigned char* gimg = smc + 3 * CB_QIMG + ((i - 1) & 1) * CB_GIMG + w * (CB_GIMG / 8);
+            const unsigned char* img = smc + ((i - 1) % CB_NQBUF) * CB_QIMG;
+            const unsigned char* gimg = smc + CB_NQBUF * CB_QIMG + ((i - 1) & 1) * CB_GIMG + w * (CB_GIMG / 8);
             bf16x8 ga[3];
             if (CBA_GSPLIT) {
                 const bf16x8* gp = reinterpret_cast<const bf16x8*>(gimg) + lane;
@@ -349,8 +384,17 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
             VIHMC_CB_STAMP(i, 1)
 #endif
         }
-        // chunk i+1 (asm DMA, issued at the top of this iteration) lands before the next barrier publishes it
-        if (CBA_ASM_DMA) bf6::wait_vmcnt0();
+        // chunk i+1 (asm DMA) lands before the next barrier publishes it
+        if (CBA_PIPE) {
+            if (i + 2 < nchunks) {
+                if (dpieces == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");   // chunk i+2 stays in flight
+                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                bf6::wait_vmcnt0();
+            }
+        } else if (CBA_ASM_DMA) {
+            bf6::wait_vmcnt0();
+        }
     }
     float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
 #pragma unroll
