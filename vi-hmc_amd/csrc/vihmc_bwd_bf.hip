@@ -77,6 +77,22 @@ __device__ __forceinline__ float act_grad_bf(int act, float h) {
 }
 }  // namespace
 
+#ifndef BB_STAMP
+#define BB_STAMP 0        // timing-only instrumentation (variant builds): in-kernel phase stamps
+#endif
+#if BB_STAMP
+// every 16th trunk workgroup of the launches with a dX part (the last one written wins: layer 1): per wave and
+// sub-tile s_memtime at the barrier exit [0], after the staging of the next sub-tile [1], when the MFMA results
+// exist [2]; per workgroup s_memtime / s_memrealtime at start and end (scripts/diag/stamps_bwd.py)
+constexpr int BBS_WG = 16, BBS_SUB = 32;
+__device__ unsigned long long bb_stamps[BBS_WG][16][BBS_SUB][3];
+__device__ unsigned long long bb_real[BBS_WG][2][2];
+#define VIHMC_BB_STAMP(I, K)                                                                                  \
+    if (samp && lane == 0 && (I) < BBS_SUB) bb_stamps[sidx][wave][(I)][(K)] = __builtin_amdgcn_s_memtime();
+#else
+#define VIHMC_BB_STAMP(I, K)
+#endif
+
 __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
     int b = blockIdx.x;
@@ -88,6 +104,14 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
     const int wg = b - c * P.n_wg;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int NI4 = (P.n_in + 3) & ~3;
+#if BB_STAMP
+    const bool samp = second && P.has_dx && (b % 16) == 0 && b / 16 < BBS_WG;
+    const int sidx = b / 16;
+    if (samp && tid == 0) {
+        bb_real[sidx][0][0] = __builtin_amdgcn_s_memtime();
+        bb_real[sidx][0][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     const int hq4 = NI4 >> 2;                          // H float4 per row (<= 28)
     const float* D = P.D + c * P.d_cs;
     const float* H = P.H + c * P.h_cs;
@@ -203,6 +227,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
         for (int i = 0; i < nsub; ++i) {
             const int sub = r0 + i * BB_SUB;
             __syncthreads();                           // buffer i&1 holds sub-tile i
+            VIHMC_BB_STAMP(i, 0)
 #if BB_WREG
             if (i == 0 && P.has_dx) {
 #pragma unroll
@@ -222,6 +247,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
                     VIHMC_BB_LOAD(sub + 2 * BB_SUB)
                 }
             }
+            VIHMC_BB_STAMP(i, 1)
             if (!P.has_dx) continue;
             const unsigned char* buf = smw + (i & 1) * BB_BUF;
             const unsigned char* drow = buf + BB_DP + (16 * h + lr) * BB_PITCH + 16 * lg;
@@ -270,6 +296,10 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
                     if (two) acc[1] = six(wb, db, acc[1]);
                 }
             }
+#if BB_STAMP
+            asm volatile("" :: "v"(acc[0]), "v"(acc[1]));
+            VIHMC_BB_STAMP(i, 2)
+#endif
             const int m = sub + 16 * h + lr;
             if (m < r1) {
                 const unsigned char* hrow = buf + BB_HP + (16 * h + lr) * BB_PITCH;
@@ -308,12 +338,14 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
         for (int i = 0; i < nsub; ++i) {
             const int sub = r0 + i * BB_SUB;
             __syncthreads();
+            VIHMC_BB_STAMP(i, 0)
             if (i + 1 < nsub) {
                 VIHMC_BB_STORE(sub + BB_SUB, (i + 1) & 1)
                 if (i + 2 < nsub && BB_ABL != 1) {
                     VIHMC_BB_LOAD(sub + 2 * BB_SUB)
                 }
             }
+            VIHMC_BB_STAMP(i, 1)
             const unsigned char* buf = smw + (i & 1) * BB_BUF;
             bf16x8 da[2][3];
 #pragma unroll
@@ -331,6 +363,10 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
                     if (two) acc[1][t] = six(da[1], hb, acc[1][t]);
                 }
             }
+#if BB_STAMP
+            asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][2]));
+            VIHMC_BB_STAMP(i, 2)
+#endif
         }
         float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride;
 #pragma unroll
@@ -365,6 +401,12 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
         for (int e = 0; e < 4; ++e)
             if (4 * tid + e < P.n_out) part[4 * tid + e] = sacc[e];
     }
+#if BB_STAMP
+    if (samp && tid == 0) {
+        bb_real[sidx][1][0] = __builtin_amdgcn_s_memtime();
+        bb_real[sidx][1][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 bool bwd_bf_ok(const BwdArgs& a) {
@@ -375,6 +417,15 @@ bool bwd_bf_ok(const BwdArgs& a) {
     }
     return true;
 }
+
+#if BB_STAMP
+extern "C" int vihmc_debug_bb_stamps(void* stamps, size_t stamp_bytes, void* real, size_t real_bytes) {
+    if (stamp_bytes != sizeof(bb_stamps) || real_bytes != sizeof(bb_real)) return -1;
+    hipError_t e = hipMemcpyFromSymbol(stamps, HIP_SYMBOL(bb_stamps), stamp_bytes, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(real, HIP_SYMBOL(bb_real), real_bytes, 0, hipMemcpyDeviceToHost);
+    return (int)e;
+}
+#endif
 
 hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s) {
     if (!bwd_bf_ok(a)) return hipErrorInvalidValue;
