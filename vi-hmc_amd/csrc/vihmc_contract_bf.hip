@@ -454,9 +454,15 @@ hipError_t launch_split_blocks(const float* src, int64_t src_cs, int ld, int row
 // ahead, two register sets), splits it into the A operand (same k order as the side-A D role) and runs
 // 7 column tiles x 2 row tiles x 6 products against transposed reads of the shared chunk image.
 // =============================================================================================
-constexpr int CBB_OWN = 256;        // owner rows per workgroup (8 waves x 32)
+constexpr int CBB_OWN = 256;        // owner rows per workgroup (8 waves x 32, or 16 x 16)
+#ifndef CBB_W16
+#define CBB_W16 1           // 16 waves of 16 owner rows (4 per SIMD, <= 128 VGPRs) instead of 8 of 32 (2 per SIMD)
+#endif
+constexpr int CBB_NS = CBB_W16 ? 1 : 2;                 // 16-row owner tiles per wave
+constexpr int CBB_WAVES = CBB_OWN / (16 * CBB_NS);
+constexpr int CBB_THREADS = 64 * CBB_WAVES;
 
-__global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
+__global__ __launch_bounds__(CBB_THREADS, 1) void k_contract_bf_b(ContractProb P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smb[];
     int b = blockIdx.x;
     if (P.xcd_group) {
@@ -470,18 +476,18 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
     const int qc = b / P.o_tiles;
     const int og = b - qc * P.o_tiles;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-    const int o0 = og * CBB_OWN + wave * 32;
+    const int o0 = og * CBB_OWN + wave * 16 * CBB_NS;
     const int q_lo = qc * P.q_per_chunk;
     const int q_hi = min(q_lo + P.q_per_chunk, P.Mq);
     const int nchunks = q_hi > q_lo ? (q_hi - q_lo + CB_QC - 1) / CB_QC : 0;
     const unsigned char* qblk = P.qimg + c * P.qimg_cs + (int64_t)(q_lo / CB_QC) * CB_BLOCK;
 #if CB_ASM_DMA
 #define VIHMC_CBB_GLDS(CI, BUF)                                                                             \
-    for (int k = wave; k < CB_GLDS; k += 8)                                                                 \
+    for (int k = wave; k < CB_GLDS; k += CBB_WAVES)                                                         \
         bf6::glds16_asm(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16, smb + (BUF) * CB_QIMG + k * 1024);
 #else
 #define VIHMC_CBB_GLDS(CI, BUF)                                                                             \
-    for (int k = wave; k < CB_GLDS; k += 8)                                                                 \
+    for (int k = wave; k < CB_GLDS; k += CBB_WAVES)                                                         \
         __builtin_amdgcn_global_load_lds(                                                                   \
             reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
             (__attribute__((address_space(3))) void*)(smb + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
@@ -495,18 +501,19 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
     // ldy = Mq rows per block; this wave's 32 owner rows are one block
     const __amdgpu_buffer_rsrc_t grs =
         make_rsrc_c(Gc, (uint32_t)((int64_t)((P.Mo + CB_QC - 1) / CB_QC) * P.ldy * CB_QC * 4));
-    uint32_t gcol[2];
+    uint32_t gcol[CBB_NS];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) gcol[s] = (uint32_t)(((o0 / CB_QC) * P.ldy) * CB_QC + 16 * s + lr) * 4u;
+    for (int s = 0; s < CBB_NS; ++s)
+        gcol[s] = (uint32_t)(((o0 / CB_QC) * P.ldy) * CB_QC + (o0 % CB_QC) + 16 * s + lr) * 4u;
     const uint32_t ystep = CB_QC * 4u;
-    float ga_[2][8], gb_[2][8];
+    float ga_[CBB_NS][8], gb_[CBB_NS][8];
 #define VIHMC_CBB_GLOAD(GN, CI)                                                                             \
     {                                                                                                       \
         const int qb0 = q_lo + (CI) * CB_QC;                                                                \
         _Pragma("unroll") for (int jj = 0; jj < 8; ++jj) {                                                  \
             const int qq = qb0 + (jj < 4 ? 4 * lg + jj : 12 + 4 * lg + jj);                                 \
             const uint32_t roff = qq < q_hi ? (uint32_t)qq * ystep : OOB_C;                                 \
-            _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                   \
+            _Pragma("unroll") for (int s = 0; s < CBB_NS; ++s)                                              \
                 GN[s][jj] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, roff + gcol[s], 0, 0)); \
         }                                                                                                   \
     }
@@ -514,20 +521,20 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
     // G two chunks ahead in three register sets (named, rotated by a 3x unrolled loop), the image one chunk
     // ahead by asm DMA, and every wave drains its own loads (vmcnt(0)) at the end of each chunk: the counted
     // wait hipcc puts before the split of G(i) (its 32 newer loads) then never waits on this chunk's loads
-    float gc_[2][8];
+    float gc_[CBB_NS][8];
     if (nchunks > 0) {
         VIHMC_CBB_GLDS(0, 0)
         VIHMC_CBB_GLOAD(ga_, 0)
         if (nchunks > 1) VIHMC_CBB_GLOAD(gb_, 1)
         if (CB_ASM_DMA) bf6::wait_vmcnt0();          // chunk 0 published by the first barrier
     }
-    f32x4 dacc[2][7];
+    f32x4 dacc[CBB_NS][7];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < CBB_NS; ++s)
 #pragma unroll
         for (int t = 0; t < 7; ++t) dacc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int tr_off = (4 * lg + (lr >> 2)) * CB_PITCH + 8 * (lr & 3);
-    auto chunk = [&](int i, float (&gv)[2][8], float (&gn)[2][8]) __attribute__((always_inline)) {
+    auto chunk = [&](int i, float (&gv)[CBB_NS][8], float (&gn)[CBB_NS][8]) __attribute__((always_inline)) {
         if (i >= nchunks) return;
         __syncthreads();                      // chunk i landed; buffer (i+1)%3 free
         if (i + 2 < nchunks) VIHMC_CBB_GLOAD(gn, i + 2)
@@ -535,9 +542,9 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
             VIHMC_CBB_GLDS(i + 1, (i + 1) % 3)
         }
         const unsigned char* img = smb + (i % 3) * CB_QIMG;
-        bf16x8 ga[2][3];
+        bf16x8 ga[CBB_NS][3];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < CBB_NS; ++s) {
             bf16x4 l0, l1, l2, h0, h1, h2;
             split4(f32x4{gv[s][0], gv[s][1], gv[s][2], gv[s][3]}, l0, l1, l2);
             split4(f32x4{gv[s][4], gv[s][5], gv[s][6], gv[s][7]}, h0, h1, h2);
@@ -555,8 +562,8 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
                 const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 16 * CB_PITCH));
                 qb[p] = cat8(lo, hi);
             }
-            dacc[0][t] = six(ga[0], qb, dacc[0][t]);
-            dacc[1][t] = six(ga[1], qb, dacc[1][t]);
+#pragma unroll
+            for (int s = 0; s < CBB_NS; ++s) dacc[s][t] = six(ga[s], qb, dacc[s][t]);
         }
         if (CB_ASM_DMA) bf6::wait_vmcnt0();   // this chunk's DMA (i+1) and G loads (i+2) done
     };
@@ -567,7 +574,7 @@ __global__ __launch_bounds__(512, 1) void k_contract_bf_b(ContractProb P) {
     }
     float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < CBB_NS; ++s)
 #pragma unroll
         for (int t = 0; t < 7; ++t) {
             const int j = 16 * t + lr;
@@ -593,7 +600,7 @@ extern "C" int vihmc_debug_cb_stamps(void* stamps, size_t stamp_bytes, void* rea
 
 hipError_t launch_contract_bf_b(const ContractProb& p, int C, hipStream_t s) {
     if (p.W != 100 || !p.load_g || !p.qimg || p.q_per_chunk % CB_QC) return hipErrorInvalidValue;
-    dim3 g(C * p.o_tiles * p.q_chunks), blk(512);
+    dim3 g(C * p.o_tiles * p.q_chunks), blk(CBB_THREADS);
     hipLaunchKernelGGL(k_contract_bf_b, g, blk, 3 * CB_QIMG, s, p);
     return hipGetLastError();
 }
