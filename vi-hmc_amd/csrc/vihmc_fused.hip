@@ -365,6 +365,9 @@ __device__ __forceinline__ void bf_split_operand(const float4 (&h)[7], bf16x8 (&
 #ifndef FWD_TAILF32
 #define FWD_TAILF32 1
 #endif
+#ifndef FWD_BF_NW
+#define FWD_BF_NW 12       // waves per workgroup of the bf16x6 forward (16 rows each): 12 = 3 per SIMD at 168 VGPRs
+#endif
 #ifndef FWD_DMA_ONLY
 #define FWD_DMA_ONLY 0     // timing builds: the register-staging path compiled out with FWD_TAILF32 = 0 too
 #endif
@@ -616,10 +619,11 @@ size_t fwd_fused_bf_lds_bytes() { return 2 * (size_t)FWD_WIMG; }
 static_assert(BBUF <= FWD_WIMG && FWD_WTAIL + FW * 16 <= FWD_WIMG && FWD_WIMG % 1024 == 0 &&
               2 * FWD_WIMG <= 160 * 1024, "weight image");
 bool fwd_fused_bf_needs_wimg() { return FWD_TAILF32 != 0; }
+int fwd_fused_bf_waves() { return FWD_BF_NW; }
 
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s) {
     dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk));
-    hipLaunchKernelGGL(k_fwd_fused_bf<12>, g, dim3(12 * 64), fwd_fused_bf_lds_bytes(), s, a);
+    hipLaunchKernelGGL(k_fwd_fused_bf<FWD_BF_NW>, g, dim3(FWD_BF_NW * 64), fwd_fused_bf_lds_bytes(), s, a);
     return hipGetLastError();
 }
 

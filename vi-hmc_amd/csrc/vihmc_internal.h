@@ -157,6 +157,7 @@ constexpr int FWD_WIMG = 69632;                     // one pre-split weight imag
                                                     // bias [112], zero padded to 68 KB (whole 1-KB DMA pieces)
 hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s);
 bool fwd_fused_bf_needs_wimg();                     // the bf16x6 forward reads the fp32 k tail of the image
+int fwd_fused_bf_waves();                           // its waves per workgroup (16 rows each)
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s);             // bf16x6, 12 waves
 size_t fwd_fused_lds_bytes();

@@ -527,7 +527,7 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s) {
         if (v == 4 || v == 12 || v == 16) nw = v;
     }
     if (p->fwd_bf16x6 && nw == 12 && (!fwd_fused_bf_needs_wimg() || (p->fwd_wimg && p->wimg))) {
-        for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * 12);
+        for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * fwd_fused_bf_waves());
         if (p->fwd_wimg && p->wimg) {
             // pre-split weight images, DMA-staged by the forward (FWD_WIMG bytes per fused layer)
             a.net[0].wimg = p->wimg;
