@@ -354,7 +354,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
                 for (int p = 0; p < 3; ++p) da[s2][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * (tn0 + (two ? s2 : 0)));
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                if (t >= ntj) break;
+                if (t >= ntj || 16 * (tj0 + t) >= NI4) break;   // column tiles past n_in (trunk layer 0: 5 inputs)
                 bf16x8 hb[3];
 #pragma unroll
                 for (int p = 0; p < 3; ++p) hb[p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 16 * (tj0 + t));
