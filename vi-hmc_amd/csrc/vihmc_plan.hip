@@ -584,7 +584,10 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
             q.K = L.n_in;
             q.act = L.act;
             q.ntiles = cdiv(n.rows, ROWDOT_WAVES * 16 * ms);
-            q.tpw = tpw;
+            // long contractions (the branch input layer: K = 101 on the f32 MFMA) one tile per workgroup: with
+            // two they set the launch, 45 -> 35.5 us (the trunk input layer, K = 5, shares it at two tiles per
+            // workgroup; the two nets as separate launches took 17 + 30 us)
+            q.tpw = L.n_in >= 64 && j == 0 ? 1 : tpw;
             q.tiles = cdiv(q.ntiles, q.tpw);
             nt = std::max(nt, nt_of(L.n_out));
         }
