@@ -129,7 +129,7 @@ struct vihmc_plan {
     std::vector<std::pair<int, hipGraphExec_t>> graphs;
     hipStream_t cap_stream = nullptr;
     // bf16x6 forward: weights pre-split once per evaluation (k_split_wimg) and DMA-staged; VIHMC_FWD_WIMG=0
-    // restores per-workgroup register staging + split
+    // runs the fp32-MFMA fused forward instead (the bf16x6 one reads the images' fp32 k tail)
     unsigned char* wimg = nullptr;
     int64_t wimg_cs = 0;
     int fwd_wimg = [] {
