@@ -31,7 +31,8 @@
 #include "vihmc_bf16x6.h"
 
 #ifndef CB_ABL
-#define CB_ABL 0        // timing-only ablations: 1 no G^T stores, 2 no D MFMAs, 3 no S MFMAs (wrong results)
+#define CB_ABL 0        // timing-only ablations: 1 no G^T stores, 2 no D MFMAs, 3 no S MFMAs, 4 no fp64 ΣG
+                        // (wrong results)
 #endif
 
 namespace vihmc {
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                         rv = ok ? rv : 0.f;
                         g[r] = P.gscale * rv;
                         ps = fmaf(rv, rv, ps);
-                        gsum += (double)g[r];  // G terms cancel: exact-order fp64, not fp32 partials
+                        if (CB_ABL != 4) gsum += (double)g[r];  // G terms cancel: exact-order fp64, not fp32 partials
                     }
                     if (!CBA_GSPLIT) reinterpret_cast<f32x4*>(gimg)[sub * 64 + lane] = g;
                     gs[sub] = g;
