@@ -109,6 +109,27 @@ def test_bf16x6_paths_match_fp32_mfma_paths(cuda_device):
     assert dg.max() < 2e-5
 
 
+def test_forward_without_weight_images_matches(cuda_device, monkeypatch):
+    """VIHMC_FWD_WIMG=0 at plan creation: the hidden layers run the fp32-MFMA fused forward (the bf16x6 one
+    needs the pre-split images for its f32 k tail) -- same evaluation to fp32-level agreement."""
+    c = deeponet_case("deeponet_burgers")
+    rng = np.random.default_rng(11)
+    C = 4
+    base = c.thetas[0]
+    th = torch.tensor(np.stack([base + 0.01 * rng.standard_normal(base.size).astype(np.float32) for _ in range(C)]),
+                      device=cuda_device)
+    res = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("VIHMC_FWD_WIMG", env)
+        eng = engine_for(c, max_chains=C)
+        lp, g = eng.logp_grad(th)
+        res.append((lp.double().cpu().numpy(), g.double().cpu().numpy()))
+        eng.close()
+    dlp = np.abs(res[1][0] - res[0][0]) / np.abs(res[0][0])
+    dg = np.linalg.norm(res[1][1] - res[0][1], axis=1) / np.linalg.norm(res[0][1], axis=1)
+    assert dlp.max() < 2e-6 and dg.max() < 2e-5, (dlp.max(), dg.max())
+
+
 @pytest.mark.parametrize("name", ["deeponet_small", "deeponet_odd_full"])
 def test_deeponet_engine_vs_fp64_oracle_many_chains(name, cuda_device):
     """C chains with independent thetas in one launch == each chain against the fp64 oracle."""
