@@ -229,6 +229,12 @@ class _EngineNLL(torch.autograd.Function):
         return (-ctx.scale) * go[:, None] * g, None, None
 
 
+def _ordered_keys(rows: torch.Tensor) -> torch.Tensor:
+    """(t, x) fp32 rows [..., 2] -> int64 keys whose signed order is the unsigned order of (bits(t), bits(x))."""
+    bits = rows.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    return ((bits[..., 0] << 32) | bits[..., 1]) ^ (-(2 ** 63))
+
+
 def _grid_keys(rows) -> np.ndarray:
     r = np.ascontiguousarray(np.asarray(rows, np.float32).reshape(-1, 2))
     u = r.view(np.uint32).astype(np.uint64)
@@ -245,6 +251,7 @@ class BatchEngines:
         self.feats = trunk_features(self.grid)
         self.key = _grid_keys(self.grid)
         self.order = np.argsort(self.key, kind="stable")
+        self._sorted = {}                   # device -> (sorted ordered keys, order)
         self.tau_out, self.max_chains = float(tau_out), int(max_chains)
         self.device = device
         self._eng: Dict[int, DeepONetEngine] = {}
@@ -263,19 +270,33 @@ class BatchEngines:
             self._eng[B] = eng
         return eng
 
+    def _work_device(self) -> torch.device:
+        dev = torch.device(self.device) if not isinstance(self.device, torch.device) else self.device
+        return dev if dev.type == "cuda" and torch.cuda.is_available() else torch.device("cpu")
+
     def canonical(self, x_trunk, y) -> torch.Tensor:
-        """y [B, P] in each item's point order -> the plan's grid order (CPU tensor)."""
-        xt = np.asarray(torch.as_tensor(x_trunk).detach().cpu(), np.float32).reshape(-1, self.P, 2)
-        yy = torch.as_tensor(y).detach().cpu().to(torch.float32).reshape(xt.shape[0], self.P)
-        keys = _grid_keys(xt).reshape(xt.shape[0], self.P)
-        pos = np.minimum(np.searchsorted(self.key[self.order], keys), self.P - 1)
-        idx = self.order[pos]
-        if not np.array_equal(self.key[idx], keys) or not all(np.unique(r).size == self.P for r in idx):
+        """y [B, P] in each item's point order -> the plan's grid order (on the plan's device when it has one).
+
+        Each item's (t, x) rows are located in the grid by their float bit patterns (a 64-bit key per row,
+        binary search in the sorted grid keys), then checked to be a permutation of the grid."""
+        dev = self._work_device()
+        sk = self._sorted.get(dev)
+        if sk is None:
+            sk = (_ordered_keys(torch.from_numpy(self.grid))[torch.from_numpy(self.order)].to(dev),
+                  torch.from_numpy(self.order.astype(np.int64)).to(dev))
+            self._sorted[dev] = sk
+        skeys, order = sk
+        xt = torch.as_tensor(x_trunk).detach().to(dev, torch.float32).reshape(-1, self.P, 2)
+        B = xt.shape[0]
+        yy = torch.as_tensor(y).detach().to(dev, torch.float32).reshape(B, self.P)
+        keys = _ordered_keys(xt).reshape(B, self.P)
+        pos = torch.searchsorted(skeys, keys).clamp_(max=self.P - 1)
+        idx = order[pos]
+        seen = torch.bincount((idx + self.P * torch.arange(B, device=dev)[:, None]).reshape(-1), minlength=B * self.P)
+        if not bool(torch.equal(skeys[pos], keys)) or not bool((seen == 1).all()):
             raise NotImplementedError("every item must carry the whole trunk grid once (p = P); per-item trunk "
                                       "subsets are not supported in training")
-        out = torch.empty_like(yy)
-        out.scatter_(1, torch.from_numpy(idx.astype(np.int64)), yy)
-        return out
+        return torch.empty_like(yy).scatter_(1, idx, yy)
 
     def load(self, batch) -> DeepONetEngine:
         xb = torch.as_tensor(batch[0]).detach().to(torch.float32).reshape(-1, self.spec.in_branch)
