@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--chains", type=int, nargs="+", default=[1, 16])
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--no-timing", action="store_true", help="leave the HIP-event kernel timing off (graph path)")
+    ap.add_argument("--host", action="store_true",
+                    help="also time the PCIe-inclusive path: theta from pinned host memory, logp + grad copied back")
     args = ap.parse_args()
     spec = DeepONetSpec()
     prob = deeponet_problem(seed=0)
@@ -47,6 +49,20 @@ def main():
         print(f"C={C:3d}  {dt * 1e3:8.3f} ms/eval  {C / dt:9.1f} grad-evals/s  "
               f"{fl * C / dt / 1e12:6.2f} TFLOP/s algorithmic  contractA {kms / max(n, 1):.3f} ms  "
               f"logp0={lp[0].item():.4f}", flush=True)
+        if args.host:
+            th_h = th.cpu().pin_memory()
+            lp_h = torch.empty(C, pin_memory=True)
+            g_h = torch.empty(th.shape, pin_memory=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.iters):
+                lp, g = eng.logp_grad(th_h.to("cuda:0", non_blocking=True))
+                lp_h.copy_(lp, non_blocking=True)
+                g_h.copy_(g, non_blocking=True)
+            torch.cuda.synchronize()
+            dth = (time.perf_counter() - t0) / args.iters
+            print(f"C={C:3d}  host in/out (PCIe-inclusive): {dth * 1e3:8.3f} ms/eval  {C / dth:9.1f} grad-evals/s  "
+                  f"({2 * th.numel() * 4 / 1e6:.2f} MB per eval over PCIe)", flush=True)
 
 
 if __name__ == "__main__":
