@@ -421,6 +421,34 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
 // Split rows [rows][ld] (width 100) of every chain into the blocked bf16x6 image: block b holds rows
 // 32b .. 32b+31 as planes [3][32][112] bf16 (features 100..111 and rows past `rows` zero) followed by the
 // fp32 tail [32][4] (features 96..99), CONTRACT_SPLIT_BLOCK bytes per block.
+#ifndef CB_SPLIT8
+#define CB_SPLIT8 1         // 8 features per lane, 16-B stores, one pass of 448 lanes per block (0: 4 per lane, 256 lanes)
+#endif
+#if CB_SPLIT8
+constexpr int CBS_THREADS = CB_QC * 14;     // 14 groups of 8 features per 112-feature image row
+__global__ __launch_bounds__(CBS_THREADS) void k_split_blocks(const float* src, int64_t src_cs, int ld, int rows,
+                                                             unsigned char* dst, int64_t dst_cs, int nblk) {
+    const int c = blockIdx.x / nblk, blk = blockIdx.x - c * nblk;
+    const int r = threadIdx.x / 14, g = threadIdx.x - r * 14, row = blk * CB_QC + r;
+    const float* sr = src + c * src_cs + (int64_t)row * ld + 8 * g;
+    unsigned char* d = dst + c * dst_cs + (int64_t)blk * CB_BLOCK;
+    f32x4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
+    if (row < rows && g < 13) {                    // features 8g .. 8g+7; group 12 holds 96..99 only
+        x0 = *reinterpret_cast<const f32x4*>(sr);
+        if (g < 12) x1 = *reinterpret_cast<const f32x4*>(sr + 4);
+    }
+    bf16x4 a0, a1, a2, b0, b1, b2;
+    split4(x0, a0, a1, a2);
+    split4(x1, b0, b1, b2);
+    unsigned char* o = d + r * CB_PITCH + 16 * g;
+    struct alignas(16) bf16x4x2 { bf16x4 lo, hi; };
+    *reinterpret_cast<bf16x4x2*>(o) = bf16x4x2{a0, b0};
+    *reinterpret_cast<bf16x4x2*>(o + CB_PLANE) = bf16x4x2{a1, b1};
+    *reinterpret_cast<bf16x4x2*>(o + 2 * CB_PLANE) = bf16x4x2{a2, b2};
+    if (g == 12) *reinterpret_cast<f32x4*>(d + CB_TAIL + r * 16) = x0;
+}
+#else
+constexpr int CBS_THREADS = 256;
 __global__ __launch_bounds__(256) void k_split_blocks(const float* src, int64_t src_cs, int ld, int rows,
                                                      unsigned char* dst, int64_t dst_cs, int nblk) {
     const int c = blockIdx.x / nblk, blk = blockIdx.x - c * nblk;
@@ -439,11 +467,13 @@ __global__ __launch_bounds__(256) void k_split_blocks(const float* src, int64_t 
         if (g == 24) *reinterpret_cast<f32x4*>(d + CB_TAIL + r * 16) = x;
     }
 }
+#endif
 
 hipError_t launch_split_blocks(const float* src, int64_t src_cs, int ld, int rows, unsigned char* dst,
                                int64_t dst_cs, int C, hipStream_t s) {
     const int nblk = (rows + CB_QC - 1) / CB_QC;
-    hipLaunchKernelGGL(k_split_blocks, dim3(C * nblk), dim3(256), 0, s, src, src_cs, ld, rows, dst, dst_cs, nblk);
+    hipLaunchKernelGGL(k_split_blocks, dim3(C * nblk), dim3(CBS_THREADS), 0, s, src, src_cs, ld, rows, dst, dst_cs,
+                       nblk);
     return hipGetLastError();
 }
 
