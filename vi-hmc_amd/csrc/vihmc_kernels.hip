@@ -162,7 +162,11 @@ __global__ __launch_bounds__(256) void k_contract_stats(const double* stats, int
 
 // Gradient gather + prior: grid (GATHER_SPLIT slices, C); each block writes its partial log-prior
 // and the last kernel of the pair adds them in a fixed order.
-constexpr int GATHER_SPLIT = 16;
+#ifndef GATHER_SPLIT_N
+#define GATHER_SPLIT_N 64      // K slices per chain (16: 256 blocks at C = 16, 8.8 us)
+#endif
+constexpr int GATHER_SPLIT = GATHER_SPLIT_N;
+static_assert(GATHER_SPLIT <= GATHER_SPLIT_MAX, "lp_part slots");
 
 __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap,
                                                       const float* theta, int K, const float* prior_mu,
@@ -185,13 +189,14 @@ __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t g
     if (threadIdx.x == 0) lp_part[c * gridDim.x + blockIdx.x] = lp;
 }
 
-__global__ void k_logp_finalize(const double* lp_part, int nparts, const float* lik, double prior_const,
-                                float prior_scale, float* logp, int C) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double lp = 0.0;
-    for (int i = 0; i < nparts; ++i) lp += lp_part[c * nparts + i];
-    logp[c] = (float)((double)lik[c] + (lp + prior_const) / (double)prior_scale);
+// One wave per chain: lane i holds partial i (nparts <= 64), summed by a fixed xor butterfly (deterministic).
+__global__ __launch_bounds__(64) void k_logp_finalize(const double* lp_part, int nparts, const float* lik,
+                                                      double prior_const, float prior_scale, float* logp) {
+    const int c = blockIdx.x, lane = threadIdx.x;
+    double lp = lane < nparts ? lp_part[c * nparts + lane] : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lp += __shfl_xor(lp, o, 64);
+    if (lane == 0) logp[c] = (float)((double)lik[c] + (lp + prior_const) / (double)prior_scale);
 }
 
 // =============================================================================================
@@ -354,8 +359,9 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
                        prior_inv_var, prior_scale, grad, lp_part);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    VIHMC_LAUNCH(k_logp_finalize, dim3((C + 63) / 64), dim3(64), 0, s, lp_part, GATHER_SPLIT, lik, prior_const,
-                 prior_scale, logp, C);
+    static_assert(GATHER_SPLIT <= 64, "one lane per partial");
+    VIHMC_LAUNCH(k_logp_finalize, dim3(C), dim3(64), 0, s, lp_part, GATHER_SPLIT, lik, prior_const, prior_scale,
+                 logp);
 }
 
 size_t mlp_lds_bytes(int D, int n_layers, int maxw) {
