@@ -128,6 +128,7 @@ def sample(log_prob_func: Union[Callable, List[Callable]], params_init, num_samp
     num_rejected = 0
     accepts = []
     step_sizes = []
+    rhos, logus = [], []
     for n in range(num_samples):
         try:
             momentum = gibbs(params, mass, generator)
@@ -138,7 +139,10 @@ def sample(log_prob_func: Union[Callable, List[Callable]], params_init, num_samp
             momentum = lp_momenta[-1]
             new_ham = hamiltonian(params, momentum, log_prob_func, inv_mass)
             rho = min(0., float(-new_ham + ham))
-            if rho >= torch.log(torch.rand(1, generator=generator)):
+            logu = torch.log(torch.rand(1, generator=generator))
+            rhos.append(rho)
+            logus.append(float(logu))
+            if rho >= logu:
                 accepts.append(True)
                 if n > burn:
                     ret_params.append(lp_params[-1])
@@ -158,6 +162,8 @@ def sample(log_prob_func: Union[Callable, List[Callable]], params_init, num_samp
                 if n == burn:
                     step_size = eps_bar
         except LogProbError:
+            rhos.append(float("nan"))
+            logus.append(float("nan"))
             accepts.append(False)
             num_rejected += 1
             params = ret_params[-1].detach().requires_grad_()
@@ -169,5 +175,5 @@ def sample(log_prob_func: Union[Callable, List[Callable]], params_init, num_samp
         step_sizes.append(step_size)
     out = [t.detach() for t in ret_params]
     if return_stats:
-        return out, dict(num_rejected=num_rejected, accepts=accepts, step_sizes=step_sizes)
+        return out, dict(num_rejected=num_rejected, accepts=accepts, step_sizes=step_sizes, rhos=rhos, logus=logus)
     return out

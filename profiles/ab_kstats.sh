@@ -8,6 +8,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
+export VIHMC_ALLOW_DIAG=1   # timing-only ablation variants are timed here, never used for results
 for f in "$@"; do
   if [ "$f" = base ]; then unset VIHMC_LIB; else export VIHMC_LIB=$ROOT/_var/$f; fi
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$f -o s -- \

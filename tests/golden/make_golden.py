@@ -246,6 +246,79 @@ def deeponet_split_cases(out):
                         spec=np.array([16, 16, 12, 5, 3, 3, 16]), **res)
 
 
+def split_theta1(th0, seed=8):
+    return (th0 + 0.01 * np.random.default_rng(seed).standard_normal(th0.size)).astype(np.float32)
+
+
+def deeponet_split_burgers_cases(out):
+    """Config 4 at the reference shape (Operator_network/HMC/main_HMC_splitting.py:323-369 with
+    config_splitting.py): full-parameter closures, D = 172,401, two contiguous shards of N/2 = 500 functions
+    over all P = 10,201 points, prior N(0, prior_var**0.5) divided by num_splits = 2 -- and the same with
+    cfg.load_prior (tau_list = [means_flattened, stds_flattened], two D-length vectors, :341-345).
+    Inputs are regenerated from the seed (sha-pinned); outputs stored as logp, a gradient subsample and
+    the gradient norm per shard and theta."""
+    M = import_ref("Operator_network/HMC", "main_HMC_splitting")
+    cfg = M.cfg
+    ref = DeepONetSpec()
+    cfg.branch_depth, cfg.trunk_depth, cfg.activation, cfg.sample_data, cfg.dataset = 9, 9, "tanh", False, "Burgers"
+    prob = deeponet_problem(seed=0, k=None)
+    net = M.DeepONet(100, 100, 101, 5, 9, 9, "tanh", 100)
+    half = prob.N // 2
+    shards = [(torch.from_numpy(prob.branch_in[m * half:(m + 1) * half]), torch.from_numpy(prob.trunk_in),
+               torch.from_numpy(prob.y[m * half:(m + 1) * half])) for m in range(2)]
+    th0 = prob.mu.copy()
+    th1 = split_theta1(th0)
+    sub = np.sort(np.random.default_rng(9).choice(ref.n_params, 4096, replace=False))
+    res = {}
+    for lp_mode in (False, True):
+        cfg.load_prior = lp_mode
+        tau_list = ([torch.from_numpy(prob.mu.copy()), torch.from_numpy(prob.sigma.copy())] if lp_mode
+                    else [torch.tensor(cfg.prior_var)])
+        fns = M.define_split_model_log_prob(net, cfg.loss, shards, 2, tau_list, cfg.tau_out, device="cpu",
+                                            verbose=False)
+        tag = "lp_" if lp_mode else ""
+        for t, th in enumerate((th0, th1)):
+            for m, fn in enumerate(fns):
+                lp, g = ref_logp_grad(fn, th)
+                res[f"{tag}logp{t}_shard{m}"] = lp
+                res[f"{tag}grad{t}_shard{m}_sub"] = g[sub]
+                res[f"{tag}grad{t}_shard{m}_norm"] = np.float64(np.linalg.norm(g.astype(np.float64)))
+                print("split burgers", tag, t, m, lp)
+    np.savez_compressed(os.path.join(out, "deeponet_split_burgers.npz"), seed=0, n=1000, nt=101, nx=101,
+                        theta1_seed=8, grad_subsample=sub, prior_var=cfg.prior_var, tau_out=cfg.tau_out,
+                        loss=cfg.loss, spec=np.array([100, 100, 101, 5, 9, 9, 100]),
+                        sha_branch=sha(prob.branch_in), sha_trunk=sha(prob.trunk_in), sha_y=sha(prob.y),
+                        sha_mu=sha(prob.mu), sha_sigma=sha(prob.sigma), theta0_sha=sha(th0), theta1_sha=sha(th1),
+                        **res)
+
+
+def deeponet_split_loadprior_case(out):
+    """Small split closures with cfg.load_prior: Normal(means[D], stds[D]) / num_splits per shard."""
+    M = import_ref("Operator_network/HMC", "main_HMC_splitting")
+    cfg = M.cfg
+    cfg.branch_depth, cfg.trunk_depth, cfg.activation, cfg.load_prior, cfg.sample_data = 3, 3, "tanh", True, False
+    cfg.dataset = "Burgers"
+    small = DeepONetSpec(width_branch=16, width_trunk=16, in_branch=12, in_trunk=5, depth_branch=3, depth_trunk=3)
+    prob = deeponet_problem(seed=16, n=8, nt=5, nx=7, spec=small, k=None)
+    sigma = (0.05 + 0.1 * np.abs(prob.mu)).astype(np.float32)       # non-constant stds
+    net = M.DeepONet(16, 16, 12, 5, 3, 3, "tanh", None)
+    shards = [(torch.from_numpy(prob.branch_in[4 * i:4 * i + 4]), torch.from_numpy(prob.trunk_in),
+               torch.from_numpy(prob.y[4 * i:4 * i + 4])) for i in range(2)]
+    fns = M.define_split_model_log_prob(net, cfg.loss, shards, 2, [torch.from_numpy(prob.mu.copy()),
+                                                                  torch.from_numpy(sigma)], cfg.tau_out,
+                                        device="cpu", verbose=False)
+    th = split_theta1(prob.mu, 16)
+    res = {}
+    for m, fn in enumerate(fns):
+        lp, g = ref_logp_grad(fn, th)
+        res[f"logp_shard{m}"], res[f"grad_shard{m}"] = lp, g
+        print("split load_prior shard", m, lp)
+    cfg.load_prior = False
+    np.savez_compressed(os.path.join(out, "deeponet_split_loadprior.npz"), branch_in=prob.branch_in,
+                        trunk_in=prob.trunk_in, y=prob.y, mu=prob.mu, sigma=sigma, theta=th, tau_out=cfg.tau_out,
+                        loss=cfg.loss, spec=np.array([16, 16, 12, 5, 3, 3, 16]), **res)
+
+
 def init_cases(out):
     """Reference model construction consumes the torch RNG (nn.Linear init): flat parameter vectors of
     the reference DeepONet (model.py:11-75) and BNN get_model (main_VI_HMC.py:297-334) after
@@ -426,9 +499,15 @@ if __name__ == "__main__":
     if "--init-only" in sys.argv:
         init_cases(HERE)
         sys.exit(0)
+    if "--split-only" in sys.argv:
+        deeponet_split_loadprior_case(HERE)
+        deeponet_split_burgers_cases(HERE)
+        sys.exit(0)
     init_cases(HERE)
     bnn_cases(HERE)
     deeponet_cases(HERE, full_size="--no-full" not in sys.argv)
     deeponet_split_cases(HERE)
+    deeponet_split_loadprior_case(HERE)
+    deeponet_split_burgers_cases(HERE)
     sensitivity_cases(HERE)
     vi_cases(HERE)

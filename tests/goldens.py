@@ -62,6 +62,30 @@ def deeponet_case(name: str):
                            loss=str(g["loss"]), tau_out=float(g["tau_out"]), full=len(prob.grad_ind) == spec.n_params)
 
 
+def split_theta1(th0, seed=8):
+    return (th0 + 0.01 * np.random.default_rng(seed).standard_normal(th0.size)).astype(np.float32)
+
+
+def split_burgers_case():
+    """Config 4 at the reference shape (make_golden.deeponet_split_burgers_cases): the full-parameter
+    Burgers problem split into two contiguous shards of N/2 functions, inputs regenerated from the seed
+    and checked against the fixture's SHA-256s."""
+    g = load("deeponet_split_burgers")
+    spec = spec_of(g)
+    p = deeponet_problem(seed=int(g["seed"]), n=int(g["n"]), nt=int(g["nt"]), nx=int(g["nx"]), spec=spec, k=None)
+    for key, arr in (("sha_branch", p.branch_in), ("sha_trunk", p.trunk_in), ("sha_y", p.y), ("sha_mu", p.mu),
+                     ("sha_sigma", p.sigma)):
+        assert sha(arr) == str(g[key]), f"deeponet_split_burgers: regenerated input {key} drifted"
+    th0 = p.mu.copy()
+    thetas = [th0, split_theta1(th0, int(g["theta1_seed"]))]
+    for t, th in enumerate(thetas):
+        assert sha(th) == str(g[f"theta{t}_sha"])
+    half = p.N // 2
+    shards = [(p.branch_in[m * half:(m + 1) * half], p.trunk_in, p.y[m * half:(m + 1) * half]) for m in range(2)]
+    return SimpleNamespace(g=g, spec=spec, prob=p, thetas=thetas, shards=shards, loss=str(g["loss"]),
+                           tau_out=float(g["tau_out"]), prior_sd=float(np.sqrt(g["prior_var"])))
+
+
 def bnn_case(name: str):
     g = load(name)
     data = load("bnn_data")

@@ -53,3 +53,10 @@ def test_engine_refuses_cpu_device():
     from vihmc.layout import DeepONetSpec
     with pytest.raises(RuntimeError):
         DeepONetEngine(DeepONetSpec(), None, None, None, None, [0], device="cpu")
+
+
+def test_shipped_library_has_no_diagnostic_switches():
+    """Timing-only ablations (FWD_ABL, CB_ABL, BB_ABL) and stamp instrumentation are never in the product
+    build: the version string reports them and vihmc._lib refuses such a library."""
+    from vihmc import _lib
+    assert "diag=0,0,0" in _lib.lib().vihmc_version().decode()

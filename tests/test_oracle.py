@@ -7,7 +7,7 @@ by the reference's own rounding -> logp 2e-5 relative (+1e-3 absolute), gradient
 import numpy as np
 import pytest
 
-from goldens import BNN_CASES, DEEPONET_CASES, bnn_case, deeponet_case, load, spec_of
+from goldens import BNN_CASES, DEEPONET_CASES, bnn_case, deeponet_case, load, spec_of, split_burgers_case
 from oracle.bnn_ref import TorchBNNRef, mlp_layout, np_bnn_logp_grad
 from oracle.deeponet_ref import TorchDeepONetRef, deeponet_layout, np_logp_grad
 
@@ -97,6 +97,43 @@ def test_deeponet_split_shards_golden():
                                  full=True)
         assert lp == pytest.approx(float(g[f"logp_shard{m}"]), rel=2e-5, abs=1e-3)
         assert rel_norm(gr, g[f"grad_shard{m}"]) < 1e-4
+
+
+def test_deeponet_split_loadprior_golden():
+    """Split closures with cfg.load_prior: prior Normal(means[D], stds[D]) / num_splits per shard
+    (Operator_network/HMC/main_HMC_splitting.py:122-129,341-345)."""
+    g = load("deeponet_split_loadprior")
+    spec = spec_of(g)
+    lay = layout_of(spec)
+    idx = np.arange(spec.n_params)
+    for m in range(2):
+        sl = slice(4 * m, 4 * (m + 1))
+        lp, gr, _ = np_logp_grad(lay, g["branch_in"][sl], g["trunk_in"], g["y"][sl], None, idx, g["theta"], g["mu"],
+                                 g["sigma"], str(g["loss"]), float(g["tau_out"]), prior_scale=2.0, full=True)
+        assert lp == pytest.approx(float(g[f"logp_shard{m}"]), rel=2e-5, abs=1e-3)
+        assert rel_norm(gr, g[f"grad_shard{m}"]) < 1e-4
+
+
+@pytest.mark.parametrize("load_prior", [False, True])
+def test_deeponet_split_burgers_golden(load_prior):
+    """Config 4 at the reference shape: D = 172,401, two shards of N/2 = 500 functions x P = 10,201 points
+    (the torch restatement: fp32, the reference's ops)."""
+    c = split_burgers_case()
+    g, p = c.g, c.prob
+    lay = layout_of(c.spec)
+    pm, ps = (p.mu, p.sigma) if load_prior else (0.0, c.prior_sd)
+    tag = "lp_" if load_prior else ""
+    sub = g["grad_subsample"]
+    for m, (x1, x2, y) in enumerate(c.shards):
+        ref = TorchDeepONetRef(lay, x1, x2, y, None, np.arange(c.spec.n_params), pm, ps, c.loss, c.tau_out,
+                               prior_scale=2.0, full=True)
+        for t, th in enumerate(c.thetas):
+            lp, gr = ref.logp_grad(th)
+            assert lp == pytest.approx(float(g[f"{tag}logp{t}_shard{m}"]), rel=1e-6)
+            gs = g[f"{tag}grad{t}_shard{m}_sub"]
+            np.testing.assert_allclose(gr[sub], gs, rtol=1e-4, atol=1e-5 * np.abs(gs).max())
+            assert np.linalg.norm(gr.astype(np.float64)) == pytest.approx(float(g[f"{tag}grad{t}_shard{m}_norm"]),
+                                                                          rel=1e-5)
 
 
 @pytest.mark.parametrize("name", BNN_CASES)

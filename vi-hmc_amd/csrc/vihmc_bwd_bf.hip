@@ -434,4 +434,7 @@ hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// timing-only / instrumentation switches this translation unit was built with (0 = product build)
+int diag_switches_bwd_bf() { return BB_ABL | (BB_STAMP << 8); }
+
 }  // namespace vihmc

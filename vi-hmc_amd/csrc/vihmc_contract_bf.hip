@@ -643,4 +643,7 @@ hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s) {
     return hipGetLastError();
 }
 
+// timing-only / instrumentation switches this translation unit was built with (0 = product build)
+int diag_switches_contract_bf() { return CB_ABL | (CB_STAMP << 8); }
+
 }  // namespace vihmc

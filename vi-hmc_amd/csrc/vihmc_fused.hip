@@ -638,4 +638,7 @@ hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s) {
     return hipGetLastError();
 }
 
+// timing-only / instrumentation switches this translation unit was built with (0 = product build)
+int diag_switches_fused() { return FWD_ABL; }
+
 }  // namespace vihmc

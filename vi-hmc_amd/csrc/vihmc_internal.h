@@ -157,7 +157,14 @@ constexpr int FWD_WIMG = 69632;                     // one pre-split weight imag
                                                     // bias [112], zero padded to 68 KB (whole 1-KB DMA pieces)
 hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s);
 bool fwd_fused_bf_needs_wimg();                     // the bf16x6 forward reads the fp32 k tail of the image
-int fwd_fused_bf_waves();                           // its waves per workgroup (16 rows each)
+int fwd_fused_bf_waves();
+// Nonzero when a translation unit was built with a timing-only ablation (FWD_ABL, CB_ABL, BB_ABL: wrong
+// results) or phase-stamp instrumentation (CB_STAMP, BB_STAMP). vihmc_version() reports them and plan
+// creation refuses such a library unless VIHMC_ALLOW_DIAG=1 (the A/B scripts' variant builds).
+int diag_switches_fused();
+int diag_switches_contract_bf();
+int diag_switches_bwd_bf();
+int diag_switches();                           // its waves per workgroup (16 rows each)
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s);             // bf16x6, 12 waves
 size_t fwd_fused_lds_bytes();

@@ -197,6 +197,10 @@ struct vihmc_plan {
     }
 };
 
+namespace vihmc {
+int diag_switches() { return diag_switches_fused() | diag_switches_contract_bf() | diag_switches_bwd_bf(); }
+}  // namespace vihmc
+
 namespace {
 
 int prior_setup(vihmc_plan* p, const float* prior_mu, const float* prior_sd) {
@@ -216,6 +220,12 @@ int prior_setup(vihmc_plan* p, const float* prior_mu, const float* prior_sd) {
 }
 
 int check_lik(const vihmc_lik_desc& l) {
+    if (vihmc::diag_switches()) {
+        const char* e = std::getenv("VIHMC_ALLOW_DIAG");
+        if (!(e && e[0] == '1'))
+            return fail(std::string("library built with timing-only diagnostic switches (") + vihmc_version() +
+                        "): results are wrong by design; set VIHMC_ALLOW_DIAG=1 for A/B timing only");
+    }
     if (l.loss != VIHMC_LOSS_NLL && l.loss != VIHMC_LOSS_REGRESSION) return fail("unsupported loss kind");
     if (!(l.prior_scale > 0.f)) return fail("prior_scale must be > 0");
     return 0;
@@ -1170,6 +1180,11 @@ int vihmc_graph_enable(vihmc_plan* p, int on) {
 
 void vihmc_plan_destroy(vihmc_plan* p) { delete p; }
 const char* vihmc_last_error(void) { return g_err.c_str(); }
-const char* vihmc_version(void) { return "vihmc 0.1.0 gfx950"; }
+const char* vihmc_version(void) {
+    static std::string v = "vihmc 0.2.0 gfx950 diag=" + std::to_string(vihmc::diag_switches_fused()) + "," +
+                           std::to_string(vihmc::diag_switches_contract_bf()) + "," +
+                           std::to_string(vihmc::diag_switches_bwd_bf());
+    return v.c_str();
+}
 
 }  // extern "C"

@@ -153,12 +153,16 @@ def _prior_from_tau_list(cfg, tau_list, K):
 
 
 def define_model_log_prob(model, model_loss, tr_data, tau_list, tau_out, predict=False, prior_scale=1.0,
-                          device="cpu", cfg=None, mu=None, sigma=None, grad_ind=None, max_chains=1):
+                          device="cpu", cfg=None, mu=None, sigma=None, grad_ind=None, max_chains=1, full=False):
     """main_VI_HMC_burgers.py:27-180. Reads ``means_flattened_{uid}``, ``stds_flattened_{uid}`` and
     ``gradient_indices_{uid}.npy`` from ``cfg.prior_file`` unless mu/sigma/grad_ind are given.
-    Passing ``grad_ind=None`` with ``mu=None`` and cfg=None selects full-parameter HMC (mus=None)."""
+    ``full=True`` (or ``mu=None`` with no artefact file) selects full-parameter HMC (the ``mus=None``
+    branch, Operator_network/HMC/main_HMC_splitting.py:79-206): no artefacts are read, and
+    ``cfg.load_prior`` then means tau_list = [means[D], stds[D]] (main_HMC_splitting.py:341-345)."""
     spec = spec_of(model)
-    if mu is None and cfg is not None and getattr(cfg, "prior_file", None):
+    if full:
+        mu = grad_ind = None
+    elif mu is None and cfg is not None and getattr(cfg, "prior_file", None):
         mu, sigma, gi = load_vi_artefacts(cfg.prior_file, cfg.prior_uid)
         grad_ind = gi if grad_ind is None else grad_ind
     full = mu is None
@@ -195,13 +199,14 @@ def define_model_log_prob(model, model_loss, tr_data, tau_list, tau_out, predict
 def define_split_model_log_prob(model, model_loss, train_loader, num_splits, tau_list, tau_out, predict=False,
                                 device="cpu", verbose=True, cfg=None):
     """Operator_network/HMC/main_HMC_splitting.py:209-258: full-parameter closures over data shards,
-    each with prior_scale=num_splits."""
+    each with prior_scale=num_splits. ``cfg`` carries load_prior / sample_data as in the reference's
+    define_model_log_prob (:115-206); the VI artefact files are never read on this path."""
     out = []
     for i, data in enumerate(train_loader):
         if i > num_splits - 1:
             break
         out.append(define_model_log_prob(model, model_loss, data, tau_list, tau_out, predict=predict,
-                                         prior_scale=num_splits, device=device, cfg=None))
+                                         prior_scale=num_splits, device=device, cfg=cfg, full=True))
     if verbose:
         print("Number of splits: ", len(out), " , each of batch size ", train_loader[0][0].shape[0], "\n")
     return out
