@@ -46,6 +46,12 @@ def parse():
                          "ESS/s (Geyer initial monotone sequence; 0 = skip)")
     ap.add_argument("--no-gather", dest="gather", action="store_false",
                     help="skip the RCCL all-gather of the sample pool after the timed region (N > 1)")
+    ap.add_argument("--cpu-procs", type=int, default=14,
+                    help="one-thread CPU processes of the multi-chain CPU throughput baseline (0 = skip); the GPU "
+                         "box's CPU share is 16 cores, and a ROCm torch import counts against its limit of 16 "
+                         "processes per GPU (this one included)")
+    ap.add_argument("--no-side-legs", dest="side_legs", action="store_false",
+                    help="skip the single-chain (configs 2 and 4) and BNN (configs 2-3) legs reported beside the line")
     return ap.parse_args()
 
 
@@ -79,6 +85,176 @@ def cpu_baseline(prob, L, step_size, seconds):
             "sample": f"1 chain x {n} HMC samples (L={L}; hamiltorch: L+1 grad + 2 value evals each) in {dt:.1f} s, "
                       f"oracle/deeponet_ref.TorchDeepONetRef (reference torch ops) + oracle/hamiltorch_ref.sample, "
                       f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
+
+
+def cpu_throughput(procs, seconds, L, step_size):
+    """One process per core at one thread, one chain each: oracle/cpu_throughput.py."""
+    sys.path.insert(0, ROOT)
+    from oracle.cpu_throughput import run_parallel
+    r = run_parallel(procs, seconds, L, step_size)
+    return {"value": r["value"], "unit": "leapfrog-steps/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} processes x 1 thread x 1 chain, {r['samples']} HMC samples in <= {r['seconds_max']:.1f} s "
+                      f"(L={L}, hamiltorch loop + the reference torch ops, oracle/cpu_throughput.py)"}
+
+
+# ------------------------------------------------------------------------------------------------
+# kernel classes (include/vihmc.h VIHMC_T_*) priced on the roofline
+# ------------------------------------------------------------------------------------------------
+KCLASS = {0: ("contract_a", "k_contract_bf", "side-A contraction: S = Z_b Z_t^T + b, Gaussian NLL, G, dZ_trunk"),
+          1: ("contract_b", "k_contract_bf_b", "side-B contraction: dZ_branch = G Z_trunk"),
+          2: ("bwd", "k_bwd_bf", "layer backward (dX and dW of both MLPs), one launch per layer"),
+          3: ("fwd", "k_fwd_fused_bf", "fused hidden-layer forward of both MLPs (layers 1..8)")}
+T_EVAL = 4
+CAL_STEPS = 2          # untimed HMC iterations with every kernel class under HIP events
+
+
+def mfma_peak(bf16x6: int) -> float:
+    # bf16x6: each fp32 product costs 6 bf16 MFMA products, so the fp32-equivalent ceiling is the bf16 dense peak
+    # / 6 (= 419.4 TFLOP/s); the fp32 MFMA form is priced against the fp32 peak
+    return BF16_PEAK_TFLOPS / BF16X6_PRODUCTS if bf16x6 else FP32_PEAK_TFLOPS
+
+
+def class_table(eng, spec, prob, C, evals):
+    """Per-class HIP-event times recorded over `evals` evaluations -> per-launch roofline numbers."""
+    fl = spec.flops_by_kernel(prob.N, prob.P)
+    forms = {"contract_a": eng.get_option("contract_bf16x6"), "contract_b": eng.get_option("contract_bf16x6"),
+             "bwd": eng.get_option("bwd_bf16x6"), "fwd": eng.get_option("fwd_bf16x6")}
+    ev_ms, ev_n = eng.timing_class(T_EVAL)
+    eval_ms = ev_ms / max(ev_n, 1)
+    out = {}
+    for cls, (key, kname, what) in KCLASS.items():
+        ms, n = eng.timing_class(cls)
+        if n == 0:
+            continue
+        per_eval = n / evals
+        flops = C * fl[key] / per_eval                      # per launch
+        avg = ms / n
+        ach = flops / (avg / 1e3) / 1e12
+        pk = mfma_peak(forms[key])
+        out[key] = {"kernel": kname, "what": what, "avg_launch_ms": avg, "launches_per_eval": per_eval,
+                    "flops_per_launch": flops, "achieved": ach, "peak": pk, "frac": ach / pk,
+                    "share_of_eval": ms / max(ev_ms, 1e-12)}
+    total = C * spec.flops_per_grad_eval(prob.N, prob.P)
+    ach = total / (eval_ms / 1e3) / 1e12
+    out["eval"] = {"kernel": "whole evaluation (all launches, scatter -> gather)", "avg_ms": eval_ms,
+                   "flops": total, "achieved": ach, "peak": mfma_peak(1), "frac": ach / mfma_peak(1)}
+    return out
+
+
+def load_traffic(kname, C):
+    """PMC-measured HBM bytes per launch of `kname` at this chain count (profiles/traffic.json, written by
+    profiles/traffic_from_pmc.py from separate FETCH_SIZE / WRITE_SIZE passes of this bench), or None."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        tj = json.load(f)
+    k = tj.get("kernels", {}).get(kname)
+    if k is None or tj.get("chains_per_gpu") != C:
+        return None, None
+    return k["hbm_bytes_per_launch"], tj.get("source")
+
+
+def _timed_steps(runner, warm, steps):
+    for _ in range(warm):
+        runner.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.step()
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def leg_deeponet_c1(prob, spec, dev, L, eps, steps=20):
+    """The VI-HMC DeepONet config at ONE chain per GPU (single-chain latency)."""
+    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner
+    eng = DeepONetEngine(spec, prob.branch_in, trunk_features(prob.trunk_in), prob.y, prob.mu, prob.grad_ind, 0.0,
+                         0.1, "NLL", 1.0, max_chains=1, device=dev)
+    ev = EngineEvaluator(eng)
+    th0 = torch.tensor(prob.mu[prob.grad_ind], device=dev)[None]
+    r = HMCRunner(ev, th0, steps + 3, L, eps, rng=ChainRNG(1, eng.K, dev, seeds=[1000]))
+    eng.timing(T_EVAL, True)
+    dt = _timed_steps(r, 3, steps)
+    ms, n = eng.timing_class(T_EVAL)
+    ev_ms = ms / max(n, 1)
+    fl = spec.flops_per_grad_eval(prob.N, prob.P)
+    eng.timing(-1, False)
+    eng.close()
+    return {"workload": "DeepONet VI-HMC Burgers (config 5 network / data), 1 chain per GPU", "chains": 1,
+            "leapfrog_steps_per_s": steps * L / dt, "ms_per_eval": ev_ms, "ms_per_hmc_step": dt / steps * 1e3,
+            "eval_tflops_algorithmic": fl / (ev_ms / 1e3) / 1e12, "frac_of_bf16x6_ceiling": fl / (ev_ms / 1e3) / 1e12 /
+            mfma_peak(1)}
+
+
+def leg_split_c1(spec, dev, L, eps, steps=10):
+    """Config 4: full-parameter DeepONet HMC, Burgers, 2 data shards of N/2, Integrator.SPLITTING, 1 chain."""
+    from vihmc.data import deeponet_problem
+    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner, Integrator
+    prob = deeponet_problem(seed=0, k=None)
+    half = prob.N // 2
+    tf = trunk_features(prob.trunk_in)
+    engs = [DeepONetEngine(spec, prob.branch_in[m * half:(m + 1) * half], tf, prob.y[m * half:(m + 1) * half],
+                           prob.mu, prob.grad_ind, 0.0, 0.1, "NLL", 1.0, prior_scale=2.0, max_chains=1, device=dev)
+            for m in range(2)]
+    evs = [EngineEvaluator(e) for e in engs]
+    th0 = torch.tensor(prob.mu, device=dev)[None]
+    r = HMCRunner(evs, th0, steps + 2, L, eps, integrator=Integrator.SPLITTING,
+                  rng=ChainRNG(1, spec.n_params, dev, seeds=[1000]))
+    for e in engs:
+        e.timing(T_EVAL, True)
+    for e in evs:
+        e.n_grad = e.n_value = 0
+    dt = _timed_steps(r, 2, steps)
+    ms = sum(e.timing_class(T_EVAL)[0] for e in engs)
+    n = sum(e.timing_class(T_EVAL)[1] for e in engs)
+    n_grad = sum(e.n_grad for e in evs)
+    out = {"workload": "config 4: full-parameter DeepONet HMC (D = 172,401), Burgers, 2 shards of N/2 = 500, "
+                       "Integrator.SPLITTING, 1 chain", "chains": 1, "leapfrog_steps_per_s": steps * L / dt,
+           "half_shard_grad_evals_per_s": n_grad / dt, "ms_per_half_shard_eval": ms / max(n, 1),
+           "ms_per_hmc_step": dt / steps * 1e3,
+           "note": "a leapfrog step = 2M = 4 half-shard gradient evaluations (3 with the end-point gradient reused)"}
+    for e in engs:
+        e.close()
+    return out
+
+
+def leg_bnn(dev, C, steps=10, L=196, eps=5e-4):
+    """BNN VI-HMC (Neural_network/VI_HMC, configs 2 and 3): width [10, 10] tanh, 20 shipped training points,
+    NLL variance 0.0025, prior N(0, 1), K = 90 sensitive parameters of D = 141 (seeded), L = 196, eps = 5e-4."""
+    from vihmc.data import bnn_data, bnn_init
+    from vihmc.engine import MLPEngine, prior_per_tensor
+    from vihmc.layout import MLPSpec
+    from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner
+    spec = MLPSpec()
+    x, y, _, _ = bnn_data()
+    mu = bnn_init(spec, seed=0)
+    D = spec.n_params
+    idx = np.sort(np.random.default_rng(11).choice(D, 90, replace=False))
+    K = idx.size
+    eng = MLPEngine(spec, x, y, mu, idx, 0.0, prior_per_tensor(spec.tensor_sizes, K, [1.0] * 6), "NLL", 0.0025,
+                    max_chains=C, device=dev)
+    ev = EngineEvaluator(eng)
+    th0 = torch.tensor(mu[idx], device=dev)[None].repeat(C, 1)
+    r = HMCRunner(ev, th0, steps + 2, L, eps, rng=ChainRNG(C, K, dev, seeds=[1000 + c for c in range(C)]))
+    eng.timing(eng.T_MLP, True)
+    dt = _timed_steps(r, 2, steps)
+    ms, n = eng.timing_class(eng.T_MLP)
+    eng.timing(-1, False)
+    avg = ms / max(n, 1)
+    # algorithmic bytes per launch: theta in + grad out per chain, x / y / frozen weights / index map once
+    byts = C * 2 * 4 * K + 2 * 4 * x.size + 4 * D + 4 * K
+    lf = C * L * steps / dt
+    eng.close()
+    return {"workload": f"BNN VI-HMC (configs 2-3), {C} chain(s) per GPU, L = {L}", "chains": C,
+            "leapfrog_steps_per_s": lf, "us_per_leapfrog_step": 1e6 * dt / (L * steps),
+            "kernel_avg_us": avg * 1e3, "kernel_share_of_wall": ms / 1e3 / dt,
+            "algorithmic_bytes_per_launch": byts,
+            "hbm_frac": byts / (avg / 1e3) / 1e9 / HBM_PEAK_GBS,
+            "note": "latency-bound: one k_mlp launch per leapfrog step (one wave per chain) plus the torch "
+                    "elementwise updates; the HBM fraction is from algorithmic bytes"}
 
 
 def ess_phase(args, ev, runner, K, dev, chains, world):
@@ -145,14 +321,24 @@ def main():
     chains = list(range(rank * C, (rank + 1) * C))
     theta0 = torch.tensor(prob.mu[prob.grad_ind], device=dev).repeat(C, 1)
     ev = EngineEvaluator(eng)
-    n_total = args.warmup + args.steps
+    n_total = args.warmup + CAL_STEPS + args.steps
     runner = HMCRunner(ev, theta0, n_total, args.L, args.step_size, burn=0,
                        rng=ChainRNG(C, eng.K, dev, seeds=[1000 + c for c in chains]))
     for _ in range(args.warmup):
         runner.step()
     torch.cuda.synchronize()
+    # calibration (untimed): every kernel class and the whole evaluation under HIP events for a few steps,
+    # to find the kernel class with the largest share of the evaluation -- the one the roofline prices
+    cal_steps = CAL_STEPS
+    eng.timing(-1, True)
+    for _ in range(cal_steps):
+        runner.step()
+    torch.cuda.synchronize()
+    cal = class_table(eng, spec, prob, C, cal_steps * args.L)
+    eng.timing(-1, False)
+    dom_cls = max(KCLASS, key=lambda k: cal.get(KCLASS[k][0], {}).get("share_of_eval", -1.0))
     ev.n_grad = 0
-    eng.timing(0, True)
+    eng.timing(dom_cls, True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -163,8 +349,8 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    k_ms, k_n = eng.timing_read()
-    eng.timing(0, False)
+    k_ms, k_n = eng.timing_class(dom_cls)
+    eng.timing(-1, False)
     grad_evals = ev.n_grad
     T = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
@@ -182,9 +368,15 @@ def main():
         extra["allgather_ms"] = (time.perf_counter() - g0) * 1e3
         extra["allgather_bytes"] = pool.numel() * 4
     res = runner.result()
-    acc_rate = float(res.accepted[:, args.warmup:].float().mean())
+    acc_rate = float(res.accepted[:, args.warmup + cal_steps:].float().mean())
     if args.ess_steps > 0:
         extra.update(ess_phase(args, ev, runner, eng.K, dev, chains, world))
+    side = {}
+    if world == 1 and args.side_legs:
+        side["deeponet_1_chain"] = leg_deeponet_c1(prob, spec, dev, args.L, args.step_size)
+        side["config4_split_1_chain"] = leg_split_c1(spec, dev, args.L, args.step_size)
+        side["bnn_config2_1_chain"] = leg_bnn(dev, 1)
+        side["bnn_config3_8_chains"] = leg_bnn(dev, 8)
 
     if rank != 0:
         if world > 1:
@@ -192,23 +384,18 @@ def main():
         return
     leapfrog = world * C * args.L * args.steps
     value = leapfrog / T
-    flops_contract = C * 4.0 * prob.N * prob.P * spec.out            # S + dZ_trunk, algorithmic, per launch
+    key, kname, what = KCLASS[dom_cls]
+    fl = spec.flops_by_kernel(prob.N, prob.P)
+    per_eval = cal[key]["launches_per_eval"]
+    flops_launch = C * fl[key] / per_eval
     avg_s = (k_ms / max(k_n, 1)) / 1e3
-    achieved = flops_contract / avg_s / 1e12 if k_n else None
+    achieved = flops_launch / avg_s / 1e12 if k_n else None
     evals_per_s = world * grad_evals / T
-    bf = eng.get_option("contract_bf16x6")
-    # bf16x6: each fp32 product costs 6 bf16 MFMA products, so the fp32-equivalent ceiling of the kernel is
-    # the bf16 dense peak / 6 (= 419.4 TFLOP/s); the fp32 MFMA path is priced against the fp32 peak
-    peak = BF16_PEAK_TFLOPS / BF16X6_PRODUCTS if bf else FP32_PEAK_TFLOPS
-    kname = ("k_contract_bf: side-A contraction on the bf16 MFMA, bf16x6 fp32 emulation" if bf else
-             "k_contract_ws: side-A contraction on the fp32 MFMA")
-    traffic = None
-    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic_contract.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
-            tj = json.load(f)
-        if tj.get("chains_per_gpu") == C and tj.get("contract_bf16x6", 0) == bf:
-            traffic = tj["hbm_bytes_per_launch"]     # PMC-measured bytes per side-A launch (same config)
+    form_key = {"contract_a": "contract_bf16x6", "contract_b": "contract_bf16x6", "bwd": "bwd_bf16x6",
+                "fwd": "fwd_bf16x6"}[key]
+    bf = eng.get_option(form_key)
+    peak = mfma_peak(bf)
+    traffic, tsrc = load_traffic(kname, C)
     line = {
         "metric": METRIC,
         "value": value,
@@ -230,20 +417,31 @@ def main():
         "hamiltorch_equiv_grad_evals_per_s": world * C * (args.L + 1) * args.steps / T,
         "eval_tflops_algorithmic": evals_per_s * spec.flops_per_grad_eval(prob.N, prob.P) / 1e12,
         "accept_rate": acc_rate,
-        "roofline": {"kernel": kname + " (branch x trunk S, Gaussian NLL, G, dZ_trunk)",
+        "roofline": {"kernel": f"{kname}: {what}", "selected_as": "largest share of the evaluation's GPU time "
+                     f"({cal[key]['share_of_eval']:.3f}, HIP-event calibration before the timed region)",
                      "bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": (achieved / peak) if achieved else None, "traffic": traffic,
                      "peak_basis": ("fp32-equivalent: bf16 dense MFMA peak 2516.6 / 6 bf16 products per fp32 product"
                                     if bf else "fp32 MFMA dense peak"),
                      "achieved_vs_fp32_mfma_peak": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
-                     "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE; profiles/traffic_contract.json)",
-                     "avg_launch_ms": avg_s * 1e3, "launches": k_n,
-                     "flops_per_launch": flops_contract},
+                     "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes; "
+                                     f"profiles/traffic.json: {tsrc})",
+                     "avg_launch_ms": avg_s * 1e3, "launches": k_n, "launches_per_eval": per_eval,
+                     "flops_per_launch": flops_launch},
+        "roofline_all": cal,
     }
     line.update(extra)
+    if side:
+        line["side_legs"] = side
     if world == 1 and args.cpu_seconds > 0:
-        line["cpu_baseline"] = cpu_baseline(prob, args.L, args.step_size, args.cpu_seconds)
-        line["speedup_vs_cpu"] = value / line["cpu_baseline"]["value"]
+        cb = cpu_baseline(prob, args.L, args.step_size, args.cpu_seconds)
+        line["cpu_baseline"] = cb
+        line["speedup_vs_cpu"] = value / cb["value"]
+        line["speedup_per_chain_vs_cpu"] = value / C / cb["value"]
+        if args.cpu_procs > 0:
+            mp = cpu_throughput(args.cpu_procs, args.cpu_seconds, args.L, args.step_size)
+            line["cpu_baseline_throughput"] = mp
+            line["speedup_vs_cpu_throughput"] = value / mp["value"]
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

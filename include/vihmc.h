@@ -117,6 +117,17 @@ int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float
  * Replaces log_prob_func(..., predict=True) -> (logp, output) (main_VI_HMC_burgers.py:175-176). */
 int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* out, void* stream);
 
+/* BNN plans: one whole leapfrog trajectory of every chain in ONE launch (hamiltorch leapfrog,
+ * Sampler.HMC with the implicit integrator): from theta_in [C, K], the fresh momentum
+ * p_in [C, K] and the gradient g_in [C, K] at theta_in, L steps of size eps[c] (device [C]; inv_mass [K]
+ * device or NULL) -> theta_out, p_out (after the final half-step), g_out and logp_out [C] at theta_out.
+ * Every product and sum is rounded separately (no fused multiply-add), so the result is bitwise the step-by-
+ * step path (L vihmc_logp_grad calls between the torch updates). Replaces hamiltorch's leapfrog loop over
+ * params_grad for the BNN configs (Neural_network/{HMC,VI_HMC}); fails for DeepONet plans. */
+int vihmc_mlp_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, const float* p_in, float* p_out,
+                         const float* g_in, float* g_out, float* logp_out, const float* eps, const float* inv_mass,
+                         int L, int C, void* stream);
+
 /* Plan introspection: 0 = DeepONet, 1 = MLP; D; K; max_chains; device bytes owned. */
 /* Sensitivity scores of every parameter at theta (chain 0 of the plan, [K] device):
  *   out[d] = sigma[d]^2 * mean over outputs of (d f / d theta_d)^2,  d < D, flat (named_parameters) order.
@@ -141,11 +152,25 @@ int     vihmc_plan_K(const vihmc_plan* p);
 int     vihmc_plan_max_chains(const vihmc_plan* p);
 int64_t vihmc_plan_device_bytes(const vihmc_plan* p);
 
-/* Kernel-level timing hook for the roofline: HIP events bracket every launch of kernel `which`
- * (0 = fused contraction, owner=trunk) on the plan's stream when enabled; the accumulated time in ms
- * and launch count are read back with vihmc_timing_read (this syncs the events). */
+/* Kernel-level timing hook for the roofline: when a class is enabled, HIP events bracket every launch of
+ * that kernel class on the evaluation's stream. vihmc_timing_enable(p, which, on) turns class `which` (or all
+ * classes, which = -1) on / off and discards recorded events; vihmc_timing_read_class sums the recorded
+ * launches of one class (-1: all) without discarding them (it syncs their events); vihmc_timing_read sums all
+ * and discards; vihmc_timing_reset discards. The evaluation is not captured into a hipGraph while timing. */
+enum {
+    VIHMC_T_CONTRACT_A = 0,   /* side-A contraction: S, Gaussian NLL, G, dZ_trunk (k_contract_bf / k_contract_ws) */
+    VIHMC_T_CONTRACT_B = 1,   /* side-B contraction: dZ_branch = G Z_trunk (k_contract_bf_b / k_contract2) */
+    VIHMC_T_BWD = 2,          /* layer backward, one launch per layer (k_bwd_bf / k_bwd_ws); one event pair brackets
+                                 the consecutive layer launches and counts them all (boundaries included) */
+    VIHMC_T_FWD = 3,          /* fused hidden-layer forward (k_fwd_fused_bf / k_fwd_fused) */
+    VIHMC_T_EVAL = 4,         /* one whole DeepONet evaluation, first to last launch */
+    VIHMC_T_MLP = 5,          /* BNN evaluation (k_mlp) */
+    VIHMC_T_COUNT = 6
+};
 int vihmc_timing_enable(vihmc_plan* p, int which, int on);
 int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches);
+int vihmc_timing_read_class(vihmc_plan* p, int which, double* total_ms, int64_t* launches);
+int vihmc_timing_reset(vihmc_plan* p);
 
 /* hipGraph replay of vihmc_logp_grad (gradient evaluations only): one graph per chain count, captured
  * on first use, over plan-owned theta/logp/grad buffers that the call copies in / out on `stream`.

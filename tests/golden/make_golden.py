@@ -319,6 +319,29 @@ def deeponet_split_loadprior_case(out):
                         loss=cfg.loss, spec=np.array([16, 16, 12, 5, 3, 3, 16]), **res)
 
 
+def deeponet_nuts_case(out):
+    """Operator_network/HMC/NUTS_DeepOnets.py:78-200 closure: full parameters, per-tensor prior
+    Normal(0, tau * 0.5) (the reference's std = tau/2 quirk), small DeepONet."""
+    M = import_ref("Operator_network/HMC", "NUTS_DeepOnets")
+    cfg = M.cfg
+    cfg.branch_depth, cfg.trunk_depth, cfg.activation, cfg.load_prior, cfg.dataset = 3, 3, "tanh", False, "Burgers"
+    small = DeepONetSpec(width_branch=16, width_trunk=16, in_branch=12, in_trunk=5, depth_branch=3, depth_trunk=3)
+    prob = deeponet_problem(seed=17, n=6, nt=5, nx=7, spec=small, k=None)
+    net = M.DeepONet(16, 16, 12, 5, 3, 3, "tanh", None)
+    sizes = [p.nelement() for p in net.parameters()]
+    shapes = [p.shape for p in net.parameters()]
+    taus = [0.01 * (1 + 0.5 * i) for i in range(len(sizes))]         # distinct per tensor
+    tau_list = [torch.tensor(t) for t in taus]
+    tr = (torch.from_numpy(prob.branch_in), torch.from_numpy(prob.trunk_in), torch.from_numpy(prob.y))
+    fn = M.define_model_log_prob(net, cfg.loss, tr, sizes, shapes, tau_list, cfg.tau_out, device="cpu")
+    th = split_theta1(prob.mu, 17)
+    lp, g = ref_logp_grad(fn, th)
+    print("nuts closure", lp)
+    np.savez_compressed(os.path.join(out, "deeponet_nuts.npz"), branch_in=prob.branch_in, trunk_in=prob.trunk_in,
+                        y=prob.y, theta=th, taus=np.asarray(taus, np.float32), sizes=np.asarray(sizes),
+                        tau_out=cfg.tau_out, loss=cfg.loss, spec=np.array([16, 16, 12, 5, 3, 3, 16]), logp=lp, grad=g)
+
+
 def init_cases(out):
     """Reference model construction consumes the torch RNG (nn.Linear init): flat parameter vectors of
     the reference DeepONet (model.py:11-75) and BNN get_model (main_VI_HMC.py:297-334) after
@@ -503,11 +526,15 @@ if __name__ == "__main__":
         deeponet_split_loadprior_case(HERE)
         deeponet_split_burgers_cases(HERE)
         sys.exit(0)
+    if "--nuts-only" in sys.argv:
+        deeponet_nuts_case(HERE)
+        sys.exit(0)
     init_cases(HERE)
     bnn_cases(HERE)
     deeponet_cases(HERE, full_size="--no-full" not in sys.argv)
     deeponet_split_cases(HERE)
     deeponet_split_loadprior_case(HERE)
     deeponet_split_burgers_cases(HERE)
+    deeponet_nuts_case(HERE)
     sensitivity_cases(HERE)
     vi_cases(HERE)

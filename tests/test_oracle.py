@@ -136,6 +136,19 @@ def test_deeponet_split_burgers_golden(load_prior):
                                                                           rel=1e-5)
 
 
+def test_deeponet_nuts_closure_golden():
+    """NUTS_DeepOnets.py closure: full parameters, prior of tensor i = Normal(0, tau_i * 0.5) (reference quirk)."""
+    from vihmc.engine import prior_per_tensor
+    g = load("deeponet_nuts")
+    spec = spec_of(g)
+    D = spec.n_params
+    ps = prior_per_tensor(list(g["sizes"]), D, list(0.5 * g["taus"].astype(np.float64)))
+    lp, gr, _ = np_logp_grad(layout_of(spec), g["branch_in"], g["trunk_in"], g["y"], None, np.arange(D), g["theta"], 0.0,
+                             ps, str(g["loss"]), float(g["tau_out"]), full=True)
+    assert lp == pytest.approx(float(g["logp"]), rel=2e-5, abs=1e-3)
+    assert rel_norm(gr, g["grad"]) < 1e-4
+
+
 @pytest.mark.parametrize("name", BNN_CASES)
 def test_bnn_oracles_match_golden(name):
     c = bnn_case(name)

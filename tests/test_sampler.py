@@ -152,3 +152,23 @@ def test_sample_entry_point_generic_closure():
     assert len(out) == len(ref)
     for a, b in zip(out, ref):
         torch.testing.assert_close(a, b, rtol=0, atol=1e-5)
+
+
+def test_sample_entry_point_global_rng_skips_draw_on_logprob_error():
+    """hamiltorch's drop-in (rng='global'): after a LogProbError no accept uniform is drawn, so the global
+    CPU stream -- and every later momentum and accept draw -- stays aligned with hamiltorch's."""
+    base, th0, _ = bnn_fn()
+    thr = float(th0[0]) + 2e-3
+
+    def fn(p):
+        lp = base(p)
+        return torch.where(p[0] > thr, torch.full_like(lp, float("nan")), lp)
+
+    torch.manual_seed(3)
+    out = S.sample(fn, th0, num_samples=14, num_steps_per_sample=6, step_size=2e-3, burn=2, verbose=True)
+    torch.manual_seed(3)
+    ref, st = HR.sample(fn, th0, 14, 6, 2e-3, burn=2, return_stats=True)
+    assert any(r != r for r in st["rhos"]), "test needs at least one LogProbError"
+    assert len(out) == len(ref)
+    for a, b in zip(out, ref):
+        torch.testing.assert_close(a, b, rtol=0, atol=1e-5)

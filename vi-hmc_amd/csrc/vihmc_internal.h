@@ -157,14 +157,14 @@ constexpr int FWD_WIMG = 69632;                     // one pre-split weight imag
                                                     // bias [112], zero padded to 68 KB (whole 1-KB DMA pieces)
 hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s);
 bool fwd_fused_bf_needs_wimg();                     // the bf16x6 forward reads the fp32 k tail of the image
-int fwd_fused_bf_waves();
+int fwd_fused_bf_waves();                           // its waves per workgroup (16 rows each)
 // Nonzero when a translation unit was built with a timing-only ablation (FWD_ABL, CB_ABL, BB_ABL: wrong
 // results) or phase-stamp instrumentation (CB_STAMP, BB_STAMP). vihmc_version() reports them and plan
 // creation refuses such a library unless VIHMC_ALLOW_DIAG=1 (the A/B scripts' variant builds).
 int diag_switches_fused();
 int diag_switches_contract_bf();
 int diag_switches_bwd_bf();
-int diag_switches();                           // its waves per workgroup (16 rows each)
+int diag_switches();
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s);             // bf16x6, 12 waves
 size_t fwd_fused_lds_bytes();
@@ -181,6 +181,15 @@ struct MlpArgs {
 };
 hipError_t launch_mlp(const MlpArgs& a, int C, int maxw, hipStream_t s);
 size_t mlp_lds_bytes(int D, int n_layers, int maxw);
+// A whole leapfrog trajectory of every chain in one launch (k_mlp_traj): hamiltorch's op sequence in fp32
+// with no fused multiply-adds, so positions / momenta / gradients are bitwise those of L separate
+// evaluations driven by the torch elementwise updates.
+struct MlpTrajArgs {
+    const float* th_in; float* th_out; const float* p_in; float* p_out; const float* g_in; float* g_out;
+    float* lp_out; const float* eps; const float* inv_mass; int32_t L;
+    int32_t ws_floats;             // set by launch_mlp_traj: the evaluation workspace (mlp_lds_bytes) in floats
+};
+hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int maxw, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // Sensitivity scores (vihmc_sens.hip): mean over the selected outputs f[n][p] of (df/dtheta)^2 for every

@@ -215,9 +215,13 @@ __device__ __forceinline__ float act_grad_z(int act, float z, float h) {
 // (lanes reading different units at the same row) on distinct banks.
 constexpr int MLP_SLD = 65;
 
-__global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
+// One log-posterior (+ gradient) evaluation of chain c by one wave. On entry w[] holds the chain's full weight
+// vector (frozen values with its sampled entries written); theta_at(k) is its k-th sampled value (prior term).
+// grad_out(k, value) receives the gradient at the sampled indices; returns logp (lane 0's value is the result).
+template <class ThetaAt, class GradOut>
+__device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* sm, int c, ThetaAt theta_at,
+                                                GradOut grad_out, bool want_grad, float* out) {
     constexpr int SLD = MLP_SLD;
-    extern __shared__ float sm[];
     const int NL = a.n_layers;
     float* w = sm;
     float* gw = w + a.D;
@@ -225,15 +229,9 @@ __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
     float* zs = hs + (NL + 1) * W * SLD;
     float* ds = zs + NL * W * SLD;
     float* gs = ds + W * SLD;
-    const int c = blockIdx.x, lane = threadIdx.x;
-    for (int i = lane; i < a.D; i += 64) {
-        w[i] = a.frozen[i];
-        gw[i] = 0.f;
-    }
+    const int lane = threadIdx.x;
+    for (int i = lane; i < a.D; i += 64) gw[i] = 0.f;
     __syncthreads();
-    for (int k = lane; k < a.K; k += 64) w[a.idx[k]] = a.theta[(int64_t)c * a.K + k];
-    __syncthreads();
-    const bool want_grad = a.grad != nullptr;
     const float v = fmaxf(a.tau_out, 1e-6f);
     const float gscale = (a.loss == 0) ? -1.f / v : -a.tau_out;
     double ssq = 0.0;
@@ -263,7 +261,7 @@ __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
             if (ok) {
                 ssq += (double)rv * (double)rv;
                 g = gscale * rv;
-                if (a.out) a.out[((int64_t)c * a.N + row) * a.out_dim + o] = pred;
+                if (out) out[((int64_t)c * a.N + row) * a.out_dim + o] = pred;
             }
             gs[o * SLD + lane] = g;
         }
@@ -311,14 +309,70 @@ __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
     const float inv_scale = 1.f / a.prior_scale;
     double lp = 0.0;
     for (int k = lane; k < a.K; k += 64) {
-        const float th = a.theta[(int64_t)c * a.K + k];
+        const float th = theta_at(k);
         const float dd = th - a.prior_mu[k];
         const float iv = a.prior_inv_var[k];
         lp += -0.5 * (double)dd * (double)dd * (double)iv;
-        if (want_grad) a.grad[(int64_t)c * a.K + k] = gw[a.idx[k]] - dd * iv * inv_scale;
+        if (want_grad) grad_out(k, gw[a.idx[k]] - dd * iv * inv_scale);
     }
     lp = wave_sum(lp);
-    if (lane == 0) a.logp[c] = (float)(ll + (lp + a.prior_const) / (double)a.prior_scale);
+    return ll + (lp + a.prior_const) / (double)a.prior_scale;
+}
+
+__global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
+    extern __shared__ float sm[];
+    float* w = sm;
+    const int c = blockIdx.x, lane = threadIdx.x;
+    for (int i = lane; i < a.D; i += 64) w[i] = a.frozen[i];
+    __syncthreads();
+    for (int k = lane; k < a.K; k += 64) w[a.idx[k]] = a.theta[(int64_t)c * a.K + k];
+    __syncthreads();
+    const float* th = a.theta + (int64_t)c * a.K;
+    float* gr = a.grad ? a.grad + (int64_t)c * a.K : nullptr;
+    const double lp = mlp_eval_core(
+        a, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gr[k] = g; }, gr != nullptr, a.out);
+    if (lane == 0) a.logp[c] = (float)lp;
+}
+
+// A leapfrog trajectory per chain (hamiltorch leapfrog, Sampler.HMC, non-splitting integrator):
+//   p += (eps/2) g(th0);  L x { th += eps p  [eps inv_mass p];  g = grad log p(th);  p += eps g };  p -= (eps/2) g
+// every product and sum rounded separately (__fmul_rn / __fadd_rn: no contraction into fma), as the torch
+// elementwise ops round them, so the result is bitwise the step-by-step path. theta / momentum / gradient of
+// the chain live in LDS after the evaluation's workspace; one wave per chain, no host round trip per step.
+__global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t) {
+    extern __shared__ float sm[];
+    const int c = blockIdx.x, lane = threadIdx.x, K = a.K;
+    float* w = sm;
+    float* th = sm + t.ws_floats;
+    float* pm = th + K;
+    float* gk = pm + K;
+    for (int i = lane; i < a.D; i += 64) w[i] = a.frozen[i];
+    const float e = t.eps[c], he = 0.5f * e;
+    const int64_t off = (int64_t)c * K;
+    for (int k = lane; k < K; k += 64) {
+        th[k] = t.th_in[off + k];
+        gk[k] = t.g_in[off + k];
+        pm[k] = __fadd_rn(t.p_in[off + k], __fmul_rn(he, gk[k]));
+    }
+    double lp = 0.0;
+    for (int s = 0; s < t.L; ++s) {
+        for (int k = lane; k < K; k += 64) {
+            const float step = t.inv_mass ? __fmul_rn(__fmul_rn(e, t.inv_mass[k]), pm[k]) : __fmul_rn(e, pm[k]);
+            th[k] = __fadd_rn(th[k], step);
+        }
+        __syncthreads();
+        for (int k = lane; k < K; k += 64) w[a.idx[k]] = th[k];
+        __syncthreads();
+        lp = mlp_eval_core(
+            a, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gk[k] = g; }, true, nullptr);
+        for (int k = lane; k < K; k += 64) pm[k] = __fadd_rn(pm[k], __fmul_rn(e, gk[k]));
+    }
+    for (int k = lane; k < K; k += 64) {
+        t.th_out[off + k] = th[k];
+        t.g_out[off + k] = gk[k];
+        t.p_out[off + k] = __fsub_rn(pm[k], __fmul_rn(he, gk[k]));
+    }
+    if (lane == 0) t.lp_out[c] = (float)lp;
 }
 
 // =============================================================================================
@@ -372,6 +426,15 @@ hipError_t launch_mlp(const MlpArgs& a, int C, int maxw, hipStream_t s) {
     const size_t shm = mlp_lds_bytes(a.D, a.n_layers, maxw);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
     VIHMC_LAUNCH(k_mlp, dim3(C), dim3(64), shm, s, a, maxw);
+}
+
+hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int maxw, hipStream_t s) {
+    const size_t ws = mlp_lds_bytes(a.D, a.n_layers, maxw);
+    const size_t shm = ws + 3 * sizeof(float) * (size_t)a.K;
+    if (shm > 160 * 1024 || t.L < 1) return hipErrorInvalidValue;
+    MlpTrajArgs tt = t;
+    tt.ws_floats = (int32_t)(ws / sizeof(float));
+    VIHMC_LAUNCH(k_mlp_traj, dim3(C), dim3(64), shm, s, a, maxw, tt);
 }
 
 }  // namespace vihmc

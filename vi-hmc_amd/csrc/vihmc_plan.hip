@@ -118,9 +118,12 @@ struct vihmc_plan {
     MlpArgs mlp{};
     int maxw = 0;
 
-    // timing hook
-    int timing_on = 0, timing_which = 0;
+    // timing hook: HIP events bracket every launch of the enabled kernel classes (vihmc.h VIHMC_T_*) on the
+    // evaluation's stream; ev_cls[i] is the class of the event pair (2i, 2i+1)
+    int timing_on = 0;              // bit mask of enabled classes
     std::vector<hipEvent_t> ev_pool;
+    std::vector<int> ev_cls;       // class of pair i
+    std::vector<int> ev_nl;        // launches the pair brackets (the layer backward: one pair around all layers)
     size_t ev_used = 0;
 
     // hipGraph replay of the gradient evaluation: one captured graph per chain count C, over plan-owned
@@ -182,9 +185,9 @@ struct vihmc_plan {
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     }
 
-    int timing_begin(int which, hipStream_t s, hipEvent_t* stop) {
+    int timing_begin(int which, hipStream_t s, hipEvent_t* stop, int nlaunch = 1) {
         *stop = nullptr;
-        if (!timing_on || which != timing_which) return 0;
+        if (!((timing_on >> which) & 1)) return 0;
         while (ev_pool.size() < ev_used + 2) {
             hipEvent_t e;
             HIPCHK(hipEventCreate(&e));
@@ -192,6 +195,10 @@ struct vihmc_plan {
         }
         HIPCHK(hipEventRecord(ev_pool[ev_used], s));
         *stop = ev_pool[ev_used + 1];
+        ev_cls.resize(ev_used / 2 + 1);
+        ev_nl.resize(ev_used / 2 + 1);
+        ev_cls[ev_used / 2] = which;
+        ev_nl[ev_used / 2] = nlaunch;
         ev_used += 2;
         return 0;
     }
@@ -559,7 +566,13 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
     const int maxl = (int)std::max(p->nets[0].L.size(), p->nets[1].L.size());
     const bool fused = fused_forward_ok(p);
     for (int j = 0; j < maxl; ++j) {
-        if (j == 1 && fused) return launch_forward_fused(p, C, s);
+        if (j == 1 && fused) {
+            hipEvent_t stop = nullptr;
+            if (int rc = p->timing_begin(VIHMC_T_FWD, s, &stop)) return rc;
+            if (int rc = launch_forward_fused(p, C, s)) return rc;
+            if (stop) HIPCHK(hipEventRecord(stop, s));
+            return 0;
+        }
         RowdotArgs a{};
         a.C = C;
         int nt = 1;
@@ -653,8 +666,20 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
     return q;
 }
 
+int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
+                       hipStream_t s);
+
 int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out, hipStream_t s) {
     if (C < 1 || C > p->maxC) return fail("C must be in [1, max_chains]");
+    hipEvent_t stop = nullptr;
+    if (int rc = p->timing_begin(VIHMC_T_EVAL, s, &stop)) return rc;
+    if (int rc = deeponet_eval_body(p, theta, C, logp, grad, out, s)) return rc;
+    if (stop) HIPCHK(hipEventRecord(stop, s));
+    return 0;
+}
+
+int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
+                       hipStream_t s) {
     HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s));
     if (int rc = deeponet_forward_layers(p, C, s)) return rc;
     const bool want_grad = grad != nullptr && out == nullptr;
@@ -665,7 +690,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         if (a.bf16x6)
             HIPCHK(launch_split_blocks(a.Q, a.q_cs, a.ldq, p->N, p->qsplitA, p->qsplitA_cs, C, s));
         hipEvent_t stop = nullptr;
-        if (int rc = p->timing_begin(0, s, &stop)) return rc;
+        if (int rc = p->timing_begin(VIHMC_T_CONTRACT_A, s, &stop)) return rc;
         HIPCHK(launch_contract(a, C, want_grad, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
     }
@@ -709,7 +734,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         if (q.bf16x6)
             HIPCHK(launch_split_blocks(q.Q, q.q_cs, q.ldq, p->P, p->qsplitB, p->qsplitB_cs, C, s));
         hipEvent_t stop = nullptr;
-        if (int rc = p->timing_begin(1, s, &stop)) return rc;
+        if (int rc = p->timing_begin(VIHMC_T_CONTRACT_B, s, &stop)) return rc;
         HIPCHK(launch_contract(q, C, true, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
         HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s));
@@ -719,6 +744,10 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
         // grouped) computes delta_{l-1} and the dW / db partial slabs
         int cur[2] = {0, 0};
         const int maxl = (int)std::max(b.L.size(), t.L.size());
+        // one event pair around the maxl consecutive layer launches (per-launch pairs cost ~4 % of the evaluation):
+        // the recorded time includes the maxl - 1 kernel boundaries between them
+        hipEvent_t bwd_stop = nullptr;
+        if (int rc = p->timing_begin(VIHMC_T_BWD, s, &bwd_stop, maxl)) return rc;
         for (int i = 0; i < maxl; ++i) {
             BwdArgs ba{};
             ba.C = C;
@@ -760,6 +789,7 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
                 if (j >= 1) cur[net] ^= 1;
             }
         }
+        if (bwd_stop) HIPCHK(hipEventRecord(bwd_stop, s));
         HIPCHK(launch_reduce(p->jobsW, p->n_jobsW, p->max_lenW, C, s));
     }
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
@@ -889,7 +919,7 @@ int mlp_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* grad,
     a.grad = grad;
     a.out = out;
     hipEvent_t stop = nullptr;
-    if (int rc = p->timing_begin(0, s, &stop)) return rc;
+    if (int rc = p->timing_begin(VIHMC_T_MLP, s, &stop)) return rc;
     HIPCHK(launch_mlp(a, C, p->maxw, s));
     if (stop) HIPCHK(hipEventRecord(stop, s));
     return 0;
@@ -956,6 +986,26 @@ int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float
         if (grad && !p->timing_on && g_on) return eval_graph(p, theta, C, logp, grad, s);
         return p->kind == 0 ? deeponet_eval(p, theta, C, logp, grad, nullptr, s)
                             : mlp_eval(p, theta, C, logp, grad, nullptr, s);
+    });
+}
+
+int vihmc_mlp_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, const float* p_in, float* p_out,
+                         const float* g_in, float* g_out, float* logp_out, const float* eps, const float* inv_mass,
+                         int L, int C, void* stream) {
+    return guarded([&]() -> int {
+        if (!p || !theta_in || !theta_out || !p_in || !p_out || !g_in || !g_out || !logp_out || !eps)
+            return fail("null argument");
+        if (p->kind != 1) return fail("vihmc_mlp_trajectory needs a BNN (MLP) plan");
+        if (C < 1 || C > p->maxC) return fail("C must be in [1, max_chains]");
+        if (L < 1) return fail("L must be >= 1");
+        if (theta_in == theta_out) return fail("theta_out must not alias theta_in (the sampler reverts to it)");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        MlpTrajArgs t{theta_in, theta_out, p_in, p_out, g_in, g_out, logp_out, eps, inv_mass, L, 0};
+        hipEvent_t stop = nullptr;
+        if (int rc = p->timing_begin(VIHMC_T_MLP, s, &stop, L)) return rc;
+        HIPCHK(launch_mlp_traj(p->mlp, t, C, p->maxw, s));
+        if (stop) HIPCHK(hipEventRecord(stop, s));
+        return 0;
     });
 }
 
@@ -1126,24 +1176,45 @@ int64_t vihmc_plan_device_bytes(const vihmc_plan* p) { return p ? p->bytes : -1;
 
 int vihmc_timing_enable(vihmc_plan* p, int which, int on) {
     if (!p) return fail("null plan");
-    p->timing_on = on;
-    p->timing_which = which;
+    if (which < -1 || which >= VIHMC_T_COUNT) return fail("timing class out of range");
+    const int bits = which < 0 ? (1 << VIHMC_T_COUNT) - 1 : 1 << which;
+    p->timing_on = on ? (p->timing_on | bits) : (p->timing_on & ~bits);
     p->ev_used = 0;
+    p->ev_cls.clear();
+    p->ev_nl.clear();
     return 0;
 }
 
-int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches) {
+int vihmc_timing_read_class(vihmc_plan* p, int which, double* total_ms, int64_t* launches) {
     if (!p || !total_ms || !launches) return fail("null argument");
     double t = 0.0;
+    int64_t n = 0;
     for (size_t i = 0; i + 1 < p->ev_used; i += 2) {
+        if (which >= 0 && p->ev_cls[i / 2] != which) continue;
         HIPCHK(hipEventSynchronize(p->ev_pool[i + 1]));
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, p->ev_pool[i], p->ev_pool[i + 1]));
         t += ms;
+        n += p->ev_nl[i / 2];
     }
     *total_ms = t;
-    *launches = (int64_t)(p->ev_used / 2);
+    *launches = n;
+    return 0;
+}
+
+int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches) {
+    const int rc = vihmc_timing_read_class(p, -1, total_ms, launches);
+    if (p && rc == 0) {
+        p->ev_used = 0;
+        p->ev_cls.clear();
+    }
+    return rc;
+}
+
+int vihmc_timing_reset(vihmc_plan* p) {
+    if (!p) return fail("null plan");
     p->ev_used = 0;
+    p->ev_cls.clear();
     return 0;
 }
 

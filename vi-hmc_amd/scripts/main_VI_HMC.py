@@ -17,14 +17,18 @@ import torch.distributed as dist  # noqa: E402
 
 from vihmc import bnn, configs  # noqa: E402
 from vihmc.data import load_vi_artefacts, save_vi_artefacts  # noqa: E402
-from vihmc.dist import chain_block, chain_seeds, gather_pool  # noqa: E402
+from vihmc.dist import all_reduce_sum, chain_block, chain_seeds  # noqa: E402
+from vihmc.postprocess import post_burn_per_chain, predictive  # noqa: E402
 from vihmc.samplers import ChainRNG, EngineEvaluator, run_chains  # noqa: E402
 
 
 def draw_and_validate(cfg, full_hmc=False):
     rank, ws = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)))
-    uid = datetime.now().strftime("%d%m%y%H%M%S")
+    uid = [datetime.now().strftime("%d%m%y%H%M%S")]
+    if ws > 1:
+        dist.broadcast_object_list(uid, src=0)
+    uid = uid[0]
     os.makedirs(cfg.out_dir, exist_ok=True)
     x_tr, y_tr, x_val, y_val = bnn.get_data(cfg)
     torch.manual_seed(cfg.seed)
@@ -63,21 +67,19 @@ def draw_and_validate(cfg, full_hmc=False):
                      reuse_endpoint_grad=getattr(cfg, "reuse_endpoint_grad", True))
     for i, c in enumerate(chains):
         np.save(f"{cfg.out_dir}hmc_params_{uid}_{c}.npy", res.samples[i, :int(res.counts[i])].cpu().numpy())
-    pool = gather_pool(res.stacked())
+    # posterior predictive from each chain's own post-burn samples (chains that hit a LogProbError store fewer);
+    # prediction sums all-reduced over ranks, the sample pool itself never moves
+    p = predictive(fval._vihmc_engine, post_burn_per_chain(res.samples, res.counts, cfg.burn), y_val)
+    n = torch.tensor([float(p.n)], dtype=torch.float64, device=dev)
+    all_reduce_sum(p.pred_sum)
+    all_reduce_sum(n)
+    p.n = int(n.item())
     if rank == 0:
-        veng = fval._vihmc_engine
-        post = pool[:, cfg.burn:].reshape(-1, th0.numel())
-        preds, lps = [], []
-        for s in range(0, post.shape[0], veng.max_chains):
-            lp, out = veng.forward(post[s:s + veng.max_chains])
-            preds.append(out)
-            lps.append(lp)
-        preds = torch.cat(preds)
         yv = y_val.to(dev)
         print("acceptance rate per chain:", [round(float(a), 3) for a in res.accepted.float().mean(1)])
-        print("\nExpected validation log probability: {:.2f}".format(float(torch.cat(lps).mean())))
-        print("\nExpected MSE: {:.2f}".format(float(((preds.mean(0) - yv) ** 2).mean())))
-        print("\nFinal MSE: {:.2f}".format(float(((preds[-1] - yv) ** 2).mean())))
+        print("\nExpected validation log probability: {:.2f}".format(float(np.mean(p.log_prob))))
+        print("\nExpected MSE: {:.2f}".format(float(((p.mean().float() - yv) ** 2).mean())))
+        print("\nFinal MSE: {:.2f}".format(p.mse[-1]))
     return res
 
 

@@ -9,8 +9,11 @@ torch.distributed chain sharding:
 
 Data: ../Data/DeepOnet_data.mat when present, else the seeded synthetic Burgers-shaped problem;
 VI artefacts from cfg.prior_file/prior_uid when present, else synthetic ones are written there.
-Outputs (cfg.out_dir): hmc_params_{uid}_c{chain}.npy ([S_ret, K] fp32, the reference's format),
-sample_mse_{uid}.npy, and the pooled posterior-predictive mean.
+Outputs (cfg.out_dir): hmc_params_{uid}_c{chain}.npy ([S_ret, K] fp32, the reference's format), one line
+"{uid}_c{chain}" per chain appended to fnames.txt (what post_process_burgers.py pools), sample_mse_{uid}.npy,
+and the posterior-predictive mean. ``--evaluate UID`` (cfg.evaluate / cfg.eval_dt_string) re-evaluates saved
+samples instead of sampling (eval_VI_HMC, :304-349); ``--gather-pool`` also all-gathers the whole sample pool
+to every rank (RCCL over xGMI; off by default: only prediction sums are reduced).
 """
 import argparse
 import os
@@ -27,7 +30,10 @@ import torch.distributed as dist  # noqa: E402
 from vihmc import configs  # noqa: E402
 from vihmc.data import deeponet_problem, load_vi_artefacts, save_vi_artefacts  # noqa: E402
 from vihmc.dist import all_reduce_sum, chain_block, chain_seeds, gather_pool  # noqa: E402
-from vihmc.operator import DeepONet, define_model_log_prob, flatten, get_burgers_data, l2_relative_error  # noqa: E402
+from vihmc.engine import DeepONetEngine, trunk_features  # noqa: E402
+from vihmc.operator import DeepONet, define_model_log_prob, flatten, get_burgers_data  # noqa: E402
+from vihmc.postprocess import (append_fname, load_pooled_samples, post_burn_per_chain, predictive,  # noqa: E402
+                               print_summary)
 from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner, Sampler  # noqa: E402
 
 
@@ -39,10 +45,13 @@ def artefacts(cfg, net):
     return load_vi_artefacts(cfg.prior_file, cfg.prior_uid)
 
 
-def run_VI_HMC(cfg):
+def run_VI_HMC(cfg, gather=False):
     rank, ws = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)))
-    dt_string = datetime.now().strftime("%d%m%y%H%M%S") + "_" + str(os.environ.get("SLURM_JOB_ID"))
+    dt_string = [datetime.now().strftime("%d%m%y%H%M%S") + "_" + str(os.environ.get("SLURM_JOB_ID"))]
+    if ws > 1:
+        dist.broadcast_object_list(dt_string, src=0)       # one uid for the whole job's files
+    dt_string = dt_string[0]
     os.makedirs(cfg.out_dir, exist_ok=True)
     torch.manual_seed(cfg.seed)
     net = DeepONet(cfg.width_branch, cfg.width_trunk, cfg.in_branch, cfg.in_trunk, cfg.branch_depth, cfg.trunk_depth,
@@ -77,38 +86,54 @@ def run_VI_HMC(cfg):
     print(f"[rank {rank}] Time taken: {took:.2f} s, acceptance {float(res.accepted.float().mean()):.3f}")
     for i, c in enumerate(chains):
         np.save(f"{cfg.out_dir}hmc_params_{dt_string}_c{c}.npy", res.samples[i, :int(res.counts[i])].cpu().numpy())
-    pool = gather_pool(res.stacked())                      # one RCCL all-gather over xGMI
-    # posterior predictive on the validation set, this rank's chains, summed over ranks
-    from vihmc.engine import DeepONetEngine, trunk_features
-    x1, x2, yv = vld_data
-    veng = DeepONetEngine(net.spec, x1.numpy(), trunk_features(x2), yv.numpy(), mu, grad_ind,
-                          *((mu[grad_ind], sigma[grad_ind]) if cfg.load_prior else (0.0, cfg.prior_var ** 0.5)),
-                          loss=cfg.loss, tau_out=cfg.tau_out, max_chains=min(16, C * cfg.num_samples), device=dev)
-    local = res.stacked()[:, cfg.burn:].reshape(-1, params_init.numel())
-    psum = torch.zeros(yv.shape, dtype=torch.float64, device=dev)
-    mse, lps = [], []
-    y_dev = yv.to(dev)
-    with torch.no_grad():
-        for s in range(0, local.shape[0], veng.max_chains):
-            lp, out = veng.forward(local[s:s + veng.max_chains])
-            psum += out.double().sum(0)
-            mse += ((out - y_dev) ** 2).mean((1, 2)).tolist()
-            lps += lp.tolist()
-    n = torch.tensor([float(local.shape[0])], dtype=torch.float64, device=dev)
-    all_reduce_sum(psum)
-    all_reduce_sum(n)
+    if ws > 1:
+        dist.barrier()
     if rank == 0:
-        mean = (psum / n).cpu().numpy()
-        err = l2_relative_error(yv.numpy().astype(np.float64), mean)
-        print("\nExpected validation log probability: {:.2f}".format(np.mean(lps)))
-        print("\nExpected MSE: {:.4f}".format(np.mean(mse)))
-        print("\nFinal MSE: {:.4f}".format(mse[-1]))
-        print("\nMin MSE:{:.6f}".format(min(mse)))
-        print("\nMean relative L2 error of the posterior-predictive mean: {:.5f}".format(err.mean()))
-        np.save(f"{cfg.out_dir}sample_mse_{dt_string}.npy", np.asarray(mse))
-        np.save(f"{cfg.out_dir}posterior_mean_{dt_string}.npy", mean.astype(np.float32))
-        print("pooled samples:", tuple(pool.shape))
+        for c in range(cfg.num_chains):
+            append_fname(cfg.out_dir, f"{dt_string}_c{c}")
+    if gather:
+        n_min = res.counts.min().reshape(1).clone()
+        if ws > 1:
+            dist.all_reduce(n_min, op=dist.ReduceOp.MIN)
+        pool = gather_pool(res.samples[:, :int(n_min)].contiguous())   # one RCCL all-gather over xGMI
+        if rank == 0:
+            print("pooled samples:", tuple(pool.shape))
+    # posterior predictive on the validation set: this rank's chains (each its own post-burn samples),
+    # prediction sums all-reduced over ranks
+    evaluate(cfg, net.spec, mu, sigma, grad_ind, vld_data, post_burn_per_chain(res.samples, res.counts, cfg.burn),
+             dev, rank, tag=dt_string)
     return res
+
+
+def evaluate(cfg, spec, mu, sigma, grad_ind, vld_data, sample_sets, dev, rank, tag):
+    x1, x2, yv = vld_data
+    n_max = max(1, max((s.shape[0] for s in sample_sets), default=1))
+    veng = DeepONetEngine(spec, x1.numpy(), trunk_features(x2), yv.numpy(), mu, grad_ind,
+                          *((mu[grad_ind], sigma[grad_ind]) if cfg.load_prior else (0.0, cfg.prior_var ** 0.5)),
+                          loss=cfg.loss, tau_out=cfg.tau_out, max_chains=min(16, n_max), device=dev)
+    p = predictive(veng, sample_sets, yv)
+    n = torch.tensor([float(p.n)], dtype=torch.float64, device=dev)
+    all_reduce_sum(p.pred_sum)
+    all_reduce_sum(n)
+    p.n = int(n.item())
+    if rank == 0 and p.mse:
+        print_summary(p, yv)
+        np.save(f"{cfg.out_dir}sample_mse_{tag}.npy", np.asarray(p.mse))
+        np.save(f"{cfg.out_dir}posterior_mean_{tag}.npy", p.mean().cpu().numpy().astype(np.float32))
+    veng.close()
+    return p
+
+
+def eval_VI_HMC(cfg, dt_string):
+    """main_VI_HMC_burgers.py:304-349: predictive of the saved hmc_params_{dt_string}.npy[burn:] (a uid of
+    fnames.txt, e.g. '<dt>_c0')."""
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)))
+    net = DeepONet(cfg.width_branch, cfg.width_trunk, cfg.in_branch, cfg.in_trunk, cfg.branch_depth, cfg.trunk_depth,
+                   cfg.activation, cfg.output_neurons)
+    mu, sigma, grad_ind = load_vi_artefacts(cfg.prior_file, cfg.prior_uid)
+    _, vld_data = get_burgers_data(cfg)
+    sets = load_pooled_samples(cfg.out_dir.rstrip("/"), [dt_string], cfg.burn)
+    return evaluate(cfg, net.spec, mu, sigma, grad_ind, vld_data, sets, dev, 0, tag=f"eval_{dt_string}")
 
 
 def main():
@@ -116,6 +141,10 @@ def main():
     ap.add_argument("--num-samples", type=int, default=None)
     ap.add_argument("--chains", type=int, default=None)
     ap.add_argument("--n-train", type=int, default=None)
+    ap.add_argument("--evaluate", default=None, help="uid of saved samples to evaluate (cfg.evaluate)")
+    ap.add_argument("--gather-pool", action="store_true")
+    ap.add_argument("--out-dir", default=None)
+    ap.add_argument("--burn", type=int, default=None)
     args = ap.parse_args()
     over = {}
     if args.num_samples:
@@ -124,11 +153,21 @@ def main():
         over["num_chains"] = args.chains
     if args.n_train:
         over.update(N_train=args.n_train, N_valid=args.n_train)
+    if args.burn is not None:
+        over["burn"] = args.burn
+    if args.evaluate:
+        over.update(evaluate=True, eval_dt_string=args.evaluate)
+    if args.out_dir:
+        over["out_dir"] = args.out_dir.rstrip("/") + "/"
     cfg = configs.load("burgers_vi_hmc", **over)
+    if cfg.evaluate:
+        print("Evaluating...")
+        eval_VI_HMC(cfg, cfg.eval_dt_string)
+        return
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
         dist.init_process_group("nccl")
-    run_VI_HMC(cfg)
+    run_VI_HMC(cfg, gather=args.gather_pool)
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -52,6 +52,8 @@ SIGNATURES = {
                                       P_int64, P_float, P_float, c_int]),
     "vihmc_logp_grad": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "vihmc_mlp_trajectory": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "vihmc_sensitivity": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_plan_set_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "vihmc_plan_kind": (c_int, [c_void_p]),
@@ -64,6 +66,8 @@ SIGNATURES = {
     "vihmc_plan_option": (c_int, [c_void_p, c_char_p, c_int]),
     "vihmc_plan_get_option": (c_int, [c_void_p, c_char_p, ctypes.POINTER(c_int)]),
     "vihmc_timing_read": (c_int, [c_void_p, ctypes.POINTER(c_double), ctypes.POINTER(c_int64)]),
+    "vihmc_timing_read_class": (c_int, [c_void_p, c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_int64)]),
+    "vihmc_timing_reset": (c_int, [c_void_p]),
     "vihmc_plan_destroy": (None, [c_void_p]),
     "vihmc_last_error": (c_char_p, []),
     "vihmc_version": (c_char_p, []),

@@ -23,6 +23,8 @@ burn = num_samples // 2
 load_prior = False
 load_std = False
 init_prior = False
+prior_file = "Saved_models/Burgers"
+prior_uid = "020125162111"
 prior_var = 0.1 ** 2
 post_var = 0.0214 ** 2
 L = int(np.pi * post_var / (2 * step_size))

@@ -154,8 +154,23 @@ class _Engine:
         return out
 
     # ---- kernel timing hook (roofline) -----------------------------------------------------------
+    # classes of include/vihmc.h VIHMC_T_*
+    T_CONTRACT_A, T_CONTRACT_B, T_BWD, T_FWD, T_EVAL, T_MLP = range(6)
+    T_ALL = -1
+
     def timing(self, which: int = 0, on: bool = True):
+        """Enable / disable HIP-event timing of kernel class ``which`` (-1: all); discards recorded events."""
         _lib.check(self.L.vihmc_timing_enable(self._plan, which, int(on)), "vihmc_timing_enable")
+
+    def timing_class(self, which: int):
+        """(total ms, launches) recorded for one class since the last enable / reset (not discarded)."""
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        _lib.check(self.L.vihmc_timing_read_class(self._plan, which, ctypes.byref(ms), ctypes.byref(n)),
+                   "vihmc_timing_read_class")
+        return ms.value, n.value
+
+    def timing_reset(self):
+        _lib.check(self.L.vihmc_timing_reset(self._plan), "vihmc_timing_reset")
 
     def graph(self, on: bool = True):
         """hipGraph replay of the gradient evaluation (vihmc_graph_enable)."""
@@ -174,6 +189,7 @@ class _Engine:
         return v.value
 
     def timing_read(self):
+        """(total ms, launches) over every recorded class; discards the events."""
         ms, n = ctypes.c_double(), ctypes.c_int64()
         _lib.check(self.L.vihmc_timing_read(self._plan, ctypes.byref(ms), ctypes.byref(n)), "vihmc_timing_read")
         return ms.value, n.value

@@ -98,6 +98,22 @@ class DeepONetSpec:
         c = 2.0 * n * p * self.out
         return fwd + c + bwd + 2 * c
 
+    def flops_by_kernel(self, n: int, p: int) -> dict:
+        """Algorithmic FLOP per chain of each kernel class of one gradient evaluation (include/vihmc.h
+        VIHMC_T_*): input layers (row-dot), hidden + last layers (fused forward), contraction side A
+        (S = Z_b Z_t^T and dZ_t = G^T Z_b), side B (dZ_b = G Z_t), layer backward (dW every layer, dX all but
+        the input layer). They sum to flops_per_grad_eval."""
+        d = {"input": 0.0, "fwd": 0.0, "bwd": 0.0}
+        for rows, layers in ((n, self.branch), (p, self.trunk)):
+            for i, l in enumerate(layers):
+                g = 2.0 * rows * l.n_in * l.n_out
+                d["input" if i == 0 else "fwd"] += g
+                d["bwd"] += g if i == 0 else 2 * g
+        c = 2.0 * n * p * self.out
+        d["contract_a"] = 2 * c
+        d["contract_b"] = c
+        return d
+
 
 @dataclass(frozen=True)
 class MLPSpec:

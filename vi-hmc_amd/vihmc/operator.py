@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from .data import deeponet_problem, load_vi_artefacts
-from .engine import DeepONetEngine, trunk_features
+from .engine import DeepONetEngine, prior_per_tensor, trunk_features
 from .layout import DeepONetSpec
 
 
@@ -197,7 +197,7 @@ def define_model_log_prob(model, model_loss, tr_data, tau_list, tau_out, predict
 
 
 def define_split_model_log_prob(model, model_loss, train_loader, num_splits, tau_list, tau_out, predict=False,
-                                device="cpu", verbose=True, cfg=None):
+                                device="cpu", verbose=True, cfg=None, max_chains=1):
     """Operator_network/HMC/main_HMC_splitting.py:209-258: full-parameter closures over data shards,
     each with prior_scale=num_splits. ``cfg`` carries load_prior / sample_data as in the reference's
     define_model_log_prob (:115-206); the VI artefact files are never read on this path."""
@@ -206,10 +206,38 @@ def define_split_model_log_prob(model, model_loss, train_loader, num_splits, tau
         if i > num_splits - 1:
             break
         out.append(define_model_log_prob(model, model_loss, data, tau_list, tau_out, predict=predict,
-                                         prior_scale=num_splits, device=device, cfg=cfg, full=True))
+                                         prior_scale=num_splits, device=device, cfg=cfg, full=True,
+                                         max_chains=max_chains))
     if verbose:
         print("Number of splits: ", len(out), " , each of batch size ", train_loader[0][0].shape[0], "\n")
     return out
+
+
+def define_model_log_prob_nuts(model, model_loss, tr_data, params_flattened_list, params_shape_list, tau_list,
+                               tau_out, predict=False, prior_scale=1.0, device="cpu", cfg=None, max_chains=1):
+    """Operator_network/HMC/NUTS_DeepOnets.py:78-200: full-parameter DeepONet closure with a per-tensor prior.
+    Reference quirk kept: without cfg.load_prior the prior of tensor i is
+    Normal(0, tau_list[i] * 0.5) -- tau used as a std and halved (:128-132); with cfg.load_prior it is
+    Normal(tau_list[0], tau_list[1]) over all D parameters."""
+    spec = spec_of(model)
+    D = spec.n_params
+    if getattr(cfg, "load_prior", False):
+        pm = np.asarray(torch.as_tensor(tau_list[0]).cpu(), np.float32)
+        ps = np.asarray(torch.as_tensor(tau_list[1]).cpu(), np.float32)
+    else:
+        taus = [float(t) for t in torch.as_tensor(torch.stack([torch.as_tensor(t) for t in tau_list])).cpu()]
+        if len(taus) != len(params_flattened_list) or sum(params_flattened_list) != D:
+            raise ValueError("tau_list / params_flattened_list must have one entry per parameter tensor")
+        pm = 0.0
+        ps = prior_per_tensor(list(params_flattened_list), D, [0.5 * t for t in taus])
+    x1, x2, y = tr_data
+    if model_loss not in ("NLL", "regression"):
+        raise NotImplementedError(f"model_loss {model_loss!r}")
+    eng = DeepONetEngine(spec, np.asarray(torch.as_tensor(x1).cpu()).reshape(-1, spec.in_branch),
+                         trunk_features(torch.as_tensor(x2).cpu()), np.asarray(torch.as_tensor(y).cpu()),
+                         np.zeros(D, np.float32), np.arange(D), pm, ps, model_loss, tau_out, prior_scale,
+                         max_chains=max_chains, device=_device(device))
+    return make_closure(eng, predict, ())
 
 
 def predict_model(model, samples, test_loader=None, model_loss="NLL", tau_out=1., tau_list=None, cfg=None,

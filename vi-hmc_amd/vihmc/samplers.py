@@ -142,6 +142,8 @@ class ChainRNG:
         """log(torch.rand(1)) per chain on the device (hamiltorch's accept draw, computed on the CPU);
         chains with mask[c] False do not consume their stream (value -inf)."""
         if self.mode == "global":
+            if mask is not None and not mask[0]:        # hamiltorch raised LogProbError: no draw
+                return torch.full((1,), float("-inf"), device=self.device)
             return torch.log(torch.rand(1)).to(self.device)
         lu = torch.full((self.C,), float("-inf"), pin_memory=self._pin)
         for c, g in enumerate(self.gens):
@@ -401,9 +403,11 @@ def sample(log_prob_func, params_init, num_samples=10, num_steps_per_sample=10, 
         r = ChainRNG(1, K, device, mode="global")
     else:
         r = ChainRNG(1, K, device, seeds=[seed if seed is not None else torch.initial_seed()])
+    # strict_rng: a non-finite log-prob skips the accept draw exactly as hamiltorch's LogProbError does (one
+    # host sync per sample; hamiltorch syncs on every accept anyway)
     res = run_chains(evs if len(evs) > 1 else evs[0], params_init[None], num_samples, num_steps_per_sample, step_size,
                      burn=burn, inv_mass=inv_mass, sampler=sampler, integrator=integrator,
-                     desired_accept_rate=desired_accept_rate, rng=r)
+                     desired_accept_rate=desired_accept_rate, rng=r, strict_rng=True)
     out = [t.to(params_init.device) for t in res.chain(0)]
     if not verbose:
         rate = 1 - float((~res.accepted[0]).sum()) / num_samples
