@@ -79,3 +79,34 @@ def test_sharding_independence(cuda_device):
     part = run_chains(EngineEvaluator(eng), th0[None].repeat(2, 1), 8, 6, 5e-4,
                       rng=ChainRNG(2, K, cuda_device, seeds=[102, 103]))
     assert torch.equal(full.stacked()[2:], part.stacked())
+
+
+@pytest.mark.parametrize("variant", ["hmc", "inv_mass", "nuts"])
+def test_bnn_fused_trajectory_bitwise_equals_stepwise(variant, cuda_device):
+    """vihmc_mlp_trajectory (one launch per trajectory) == L separate evaluations driven by the torch
+    elementwise updates, bit for bit: positions, accept decisions, log-probs and step sizes."""
+    from vihmc.engine import MLPEngine
+    from vihmc.samplers import ChainRNG, EngineEvaluator, Sampler, run_chains
+    c = bnn_case("bnn_vi_hmc")
+    g = c.g
+    C = 5
+    th0 = torch.tensor(c.thetas[0])
+    kw = dict(burn=3)
+    if variant == "inv_mass":
+        kw["inv_mass"] = torch.linspace(0.5, 1.5, th0.numel())
+    if variant == "nuts":
+        kw.update(sampler=Sampler.HMC_NUTS, burn=5)
+    out = []
+    for fused in (True, False):
+        eng = MLPEngine(c.spec, c.data["x_train"], c.data["y_train"], g["mu"], c.idx, c.prior_mu, c.prior_sd, c.loss,
+                        c.tau_out, max_chains=C, device=cuda_device)
+        eng.fused_trajectory = fused
+        out.append(run_chains(EngineEvaluator(eng), th0[None].repeat(C, 1), 12, 25, 1e-3,
+                              rng=ChainRNG(C, th0.numel(), cuda_device, seeds=[7 + i for i in range(C)]), **kw))
+    a, b = out
+    assert torch.equal(a.accepted, b.accepted)
+    assert torch.equal(a.counts, b.counts)
+    assert torch.equal(a.samples[:, :int(a.counts.max())], b.samples[:, :int(b.counts.max())])
+    assert torch.equal(a.logp_trace, b.logp_trace)
+    assert a.step_size == b.step_size
+    assert 0 < float(a.accepted.float().mean()) < 1 or variant != "hmc"

@@ -221,6 +221,9 @@ constexpr int MLP_SLD = 65;
 template <class ThetaAt, class GradOut>
 __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* sm, int c, ThetaAt theta_at,
                                                 GradOut grad_out, bool want_grad, float* out) {
+    // no implicit contraction into fma: the two kernels that inline this body (k_mlp, k_mlp_traj) must round
+    // identically (explicit fmaf calls stay fused)
+#pragma clang fp contract(off)
     constexpr int SLD = MLP_SLD;
     const int NL = a.n_layers;
     float* w = sm;
@@ -276,18 +279,20 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
             }
             __syncthreads();
             // dW[j][i] = sum_rows d[j] h[i], db[j] = sum_rows d[j]: every lane owns distinct entries and
-            // sums the 64 staged rows in a fixed order (masked rows carry d = 0).
+            // sums the staged rows in a fixed order. Rows past N carry d = 0 and are skipped (fmaf(0, h, s) = s:
+            // the same sums, 64 / N times fewer dependent steps -- 20 of 64 rows on the shipped BNN data).
             const int nw = L.n_out * L.n_in;
             const int ne = nw + (L.b_off >= 0 ? L.n_out : 0);
+            const int nrow = min(64, a.N - r0);
             for (int e = lane; e < ne; e += 64) {
                 float s = 0.f;
                 if (e < nw) {
                     const int j = e / L.n_in, i = e - j * L.n_in;
-                    for (int m = 0; m < 64; ++m) s = fmaf(ds[j * SLD + m], hin[i * SLD + m], s);
+                    for (int m = 0; m < nrow; ++m) s = fmaf(ds[j * SLD + m], hin[i * SLD + m], s);
                     gw[L.w_off + e] += s;
                 } else {
                     const int j = e - nw;
-                    for (int m = 0; m < 64; ++m) s += ds[j * SLD + m];
+                    for (int m = 0; m < nrow; ++m) s += ds[j * SLD + m];
                     gw[L.b_off + j] += s;
                 }
             }
@@ -336,10 +341,13 @@ __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
 
 // A leapfrog trajectory per chain (hamiltorch leapfrog, Sampler.HMC, non-splitting integrator):
 //   p += (eps/2) g(th0);  L x { th += eps p  [eps inv_mass p];  g = grad log p(th);  p += eps g };  p -= (eps/2) g
-// every product and sum rounded separately (__fmul_rn / __fadd_rn: no contraction into fma), as the torch
+// every product and sum rounded separately (fp contract off: no fma), as the torch
 // elementwise ops round them, so the result is bitwise the step-by-step path. theta / momentum / gradient of
 // the chain live in LDS after the evaluation's workspace; one wave per chain, no host round trip per step.
 __global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t) {
+    // products and sums written here are rounded separately (the HIP __fmul_rn / __fadd_rn helpers are plain * and
+    // + defined in a header, outside this pragma's reach: the compiler fused them into fma)
+#pragma clang fp contract(off)
     extern __shared__ float sm[];
     const int c = blockIdx.x, lane = threadIdx.x, K = a.K;
     float* w = sm;
@@ -352,25 +360,25 @@ __global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t
     for (int k = lane; k < K; k += 64) {
         th[k] = t.th_in[off + k];
         gk[k] = t.g_in[off + k];
-        pm[k] = __fadd_rn(t.p_in[off + k], __fmul_rn(he, gk[k]));
+        pm[k] = t.p_in[off + k] + he * gk[k];
     }
     double lp = 0.0;
     for (int s = 0; s < t.L; ++s) {
         for (int k = lane; k < K; k += 64) {
-            const float step = t.inv_mass ? __fmul_rn(__fmul_rn(e, t.inv_mass[k]), pm[k]) : __fmul_rn(e, pm[k]);
-            th[k] = __fadd_rn(th[k], step);
+            const float step = t.inv_mass ? (e * t.inv_mass[k]) * pm[k] : e * pm[k];
+            th[k] = th[k] + step;
         }
         __syncthreads();
         for (int k = lane; k < K; k += 64) w[a.idx[k]] = th[k];
         __syncthreads();
         lp = mlp_eval_core(
             a, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gk[k] = g; }, true, nullptr);
-        for (int k = lane; k < K; k += 64) pm[k] = __fadd_rn(pm[k], __fmul_rn(e, gk[k]));
+        for (int k = lane; k < K; k += 64) pm[k] = pm[k] + e * gk[k];
     }
     for (int k = lane; k < K; k += 64) {
         t.th_out[off + k] = th[k];
         t.g_out[off + k] = gk[k];
-        t.p_out[off + k] = __fsub_rn(pm[k], __fmul_rn(he, gk[k]));
+        t.p_out[off + k] = pm[k] - he * gk[k];
     }
     if (lane == 0) t.lp_out[c] = (float)lp;
 }

@@ -72,6 +72,15 @@ class EngineEvaluator:
         self.n_value += theta.shape[0]
         return self.engine.logp(theta)
 
+    @property
+    def fused_trajectory(self) -> bool:
+        """BNN engines run a whole leapfrog trajectory in one launch (MLPEngine.trajectory)."""
+        return hasattr(self.engine, "trajectory") and getattr(self.engine, "fused_trajectory", True)
+
+    def trajectory(self, theta, p, g, eps, L, inv_mass=None):
+        self.n_grad += theta.shape[0] * L
+        return self.engine.trajectory(theta, p, g, eps, L, inv_mass)
+
 
 class AutogradEvaluator:
     """Any scalar torch closure ``f(params[K]) -> logp`` (the reference's own contract), one chain
@@ -281,6 +290,11 @@ class HMCRunner:
 
     def _trajectory(self, th, g, p, eps):
         evs, L, M, inv_mass = self.evs, self.L, self.M, self.inv_mass
+        if not self.splitting and getattr(evs[0], "fused_trajectory", False):
+            g_open = g if self.reuse else evs[0].logp_grad(th)[1]
+            th, p, lp_new, g_new = evs[0].trajectory(th, p, g_open, eps if not torch.is_tensor(eps) else eps[:, 0],
+                                                     L, inv_mass)
+            return th, p, lp_new, g_new
         if not self.splitting:
             g_open = g if self.reuse else evs[0].logp_grad(th)[1]
             p = p + (0.5 * eps) * g_open
