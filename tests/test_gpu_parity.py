@@ -248,3 +248,34 @@ def test_bnn_engine_matches_golden(name, cuda_device):
     for t in range(2):
         check_logp(float(lpv[t]), float(g[f"val_logp{t}"]))
         np.testing.assert_allclose(pred[t].cpu().numpy(), g[f"val_pred{t}"], rtol=1e-4, atol=1e-4)
+
+
+def test_split_shards_small_rows_on_concurrent_streams(cuda_device):
+    """Round-1 record (profiles/README.md): a variant that built side B's pre-split trunk image on a second
+    stream faulted in the N = 4-per-shard split test. The shipped kernels take the caller's stream; here the
+    two shard engines (N = 4 rows: below one 32-row chunk and one 256-row side-B owner tile) run on two torch
+    streams at once, interleaved over many evaluations, and every result must equal the single-stream one
+    bit for bit -- no fault, no cross-talk between plans on concurrent streams."""
+    from vihmc.engine import DeepONetEngine, trunk_features
+    g = load("deeponet_split")
+    spec = spec_of(g)
+    th = torch.tensor(g["theta"], device=cuda_device)[None].repeat(3, 1)
+    th[1:] += 1e-3 * torch.arange(1, 3, device=cuda_device, dtype=th.dtype)[:, None]
+    engs = [DeepONetEngine(spec, g["branch_in"][4 * m:4 * m + 4], trunk_features(g["trunk_in"]), g["y"][4 * m:4 * m + 4],
+                           g["theta"], np.arange(spec.n_params), 0.0, float(np.sqrt(g["prior_var"])), str(g["loss"]),
+                           float(g["tau_out"]), prior_scale=2.0, max_chains=3, device=cuda_device) for m in range(2)]
+    ref = [e.logp_grad(th) for e in engs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(device=cuda_device) for _ in range(2)]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream())
+    outs = [[], []]
+    for _ in range(20):
+        for m in range(2):
+            with torch.cuda.stream(streams[m]):
+                outs[m].append(engs[m].logp_grad(th))
+    torch.cuda.synchronize()
+    for m in range(2):
+        for lp, gr in outs[m]:
+            assert torch.equal(lp, ref[m][0]) and torch.equal(gr, ref[m][1])
+        check_logp(float(ref[m][0][0]), float(g[f"logp_shard{m}"]))

@@ -20,6 +20,7 @@
 //       in a fixed order at the end. Deterministic: every partial slab has exactly one writer.
 #include "vihmc_internal.h"
 #include "vihmc_bf16x6.h"
+#include <cstdlib>
 
 #ifndef BB_ABL
 #define BB_ABL 0    // timing-only ablations (wrong results): 1 no loads after the first sub-tile, 2 no dX
@@ -409,6 +410,243 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
 #endif
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_bwd_bf2: the same contract with a third role. 16 waves = 8 dX + 4 dW + 4 staging waves (one of each of the
+// latter two per SIMD). In k_bwd_bf every thread stages (global load + three-way split + LDS plane stores) before
+// its MFMAs, so the split VALU sits in the MFMA waves' instruction streams and the dW role (younger, lower
+// priority) reaches its MFMAs ~2,000 cycles into a ~5,000-cycle sub-tile period (stamps, profiles/README.md).
+// Here the staging waves alone move sub-tile i+1 into the free LDS buffer (and keep i+2 in flight in registers)
+// while the dX and dW waves compute sub-tile i; their VALU issues in the MFMA issue gaps of the other waves on
+// the SIMD. dW: wave q owns output row tiles {q, q + 4} (q + 4 < 7) x every column tile.
+// ---------------------------------------------------------------------------------------------------------
+constexpr int B2_SLOTS = 7;                            // staged float4 per staging thread (<= 800 D + 896 H)
+constexpr int B2_DCOL = 4;                             // of them D slots (idx < 800 = 3.125 x 256)
+
+__global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
+    int b = blockIdx.x;
+    const int per0 = args.C * args.p[0].n_wg;
+    const bool second = b >= per0;
+    const BwdProb P = second ? args.p[1] : args.p[0];
+    if (second) b -= per0;
+    const int c = b / P.n_wg;
+    const int wg = b - c * P.n_wg;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int NI4 = (P.n_in + 3) & ~3;
+    const int hq4 = NI4 >> 2;                          // H float4 per row (<= 28)
+    const float* D = P.D + c * P.d_cs;
+    const float* H = P.H + c * P.h_cs;
+    const int r0 = wg * P.rows_per_wg;
+    const int r1 = min(P.M, r0 + P.rows_per_wg);
+    const int nsub = r1 > r0 ? (r1 - r0 + BB_SUB - 1) / BB_SUB : 0;
+
+    // ---- W^T planes (once per workgroup): rows i < n_in, features k < 100 ----
+    if (P.has_dx) {
+        const float* WT = P.WT + c * P.wt_cs;
+        for (int idx = tid; idx < P.n_in * 25; idx += BB_THREADS) {
+            const int r = idx / 25, c4 = idx - r * 25;
+            const f32x4 x = *reinterpret_cast<const f32x4*>(WT + (int64_t)r * P.ldw + 4 * c4);
+            bf16x4 p0, p1, p2;
+            split4(x, p0, p1, p2);
+            unsigned char* o = smw + BB_W + r * BB_WPITCH + 8 * c4;
+            *reinterpret_cast<bf16x4*>(o) = p0;
+            *reinterpret_cast<bf16x4*>(o + BB_WPLANE) = p1;
+            *reinterpret_cast<bf16x4*>(o + 2 * BB_WPLANE) = p2;
+            if (c4 == 24) *reinterpret_cast<f32x4*>(smw + BB_WT + r * 16) = x;
+        }
+    }
+
+    if (wave >= 12) {
+        // ---------------- staging role: item idx = t + 256 v -> D (row, c4) for idx < 800, else H ----------------
+        const int t = tid - 768;
+        const int nd = BB_SUB * 25, ntot = nd + BB_SUB * hq4;
+        int st[B2_SLOTS];
+#pragma unroll
+        for (int v = 0; v < B2_SLOTS; ++v) {
+            const int idx = t + 256 * v;
+            const bool isd = idx < nd;
+            const int e = isd ? idx : idx - nd;
+            const int q = isd ? 25 : hq4;
+            const int r = e / q, c4 = e - r * q;
+            st[v] = idx < ntot ? (r << 8) | c4 : -1;
+        }
+        f32x4 pf[B2_SLOTS];
+        f32x4 dcol[B2_DCOL];
+#pragma unroll
+        for (int v = 0; v < B2_DCOL; ++v) dcol[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto load = [&](int sub) {
+#pragma unroll
+            for (int v = 0; v < B2_SLOTS; ++v) {
+                const int row = min(sub + (max(st[v], 0) >> 8), P.M - 1);
+                const int c4 = max(st[v], 0) & 255;      // idle slots read column 0 of a valid row: in bounds
+                pf[v] = (t + 256 * v < nd) ? reinterpret_cast<const f32x4*>(D + (int64_t)row * P.ldd)[c4]
+                                           : reinterpret_cast<const f32x4*>(H + (int64_t)row * P.ldh)[c4];
+            }
+        };
+        auto store = [&](int sub, int buf) {
+#pragma unroll
+            for (int v = 0; v < B2_SLOTS; ++v) {
+                if (st[v] < 0) continue;
+                const int r = st[v] >> 8, c4 = st[v] & 255;
+                const f32x4 x = (sub + r < r1) ? pf[v] : f32x4{0.f, 0.f, 0.f, 0.f};
+                const bool isd = t + 256 * v < nd;
+                unsigned char* base = smw + buf * BB_BUF + (isd ? BB_DP : BB_HP) + r * BB_PITCH + 8 * c4;
+                bf16x4 p0, p1, p2;
+                split4(x, p0, p1, p2);
+                *reinterpret_cast<bf16x4*>(base) = p0;
+                *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;
+                *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;
+                if (isd) {
+                    if (v < B2_DCOL) dcol[v < B2_DCOL ? v : 0] += x;
+                    if (c4 == 24) *reinterpret_cast<f32x4*>(smw + buf * BB_BUF + BB_DT + r * 16) = x;
+                }
+            }
+        };
+        if (nsub > 0) {
+            load(r0);
+            store(r0, 0);
+            if (nsub > 1) load(r0 + BB_SUB);
+        }
+        for (int i = 0; i < nsub; ++i) {
+            __syncthreads();                           // buffer i&1 holds sub-tile i, (i+1)&1 is free
+            if (i + 1 < nsub) {
+                store(r0 + (i + 1) * BB_SUB, (i + 1) & 1);
+                if (i + 2 < nsub) load(r0 + (i + 2) * BB_SUB);
+            }
+        }
+        // db: per-slot column partials -> LDS [32 rows][25 float4] -> fixed-order sum over rows (below)
+        __syncthreads();
+        f32x4* red = reinterpret_cast<f32x4*>(smw);
+#pragma unroll
+        for (int v = 0; v < B2_DCOL; ++v)
+            if (st[v] >= 0 && t + 256 * v < nd) red[(st[v] >> 8) * 25 + (st[v] & 255)] = dcol[v];
+    } else if (wave < 8) {
+        // ---------------- dX role: i-tiles {2p, 2p+1} x row half h (as k_bwd_bf) ----------------
+        const int h = wave & 1, p2 = wave >> 1;
+        const int t0 = 2 * p2;
+        const bool two = t0 + 1 < 7;
+        const unsigned char* wrow0 = smw + BB_W + min(16 * t0 + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
+        const unsigned char* wrow1 = smw + BB_W + min(16 * (t0 + 1) + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
+        const float* wtl = reinterpret_cast<const float*>(smw + BB_WT);
+        const int wr0 = min(16 * t0 + lr, P.n_in - 1), wr1 = min(16 * (t0 + 1) + lr, P.n_in - 1);
+        bf16x8 wra[3][3], wrb[3][3];
+        float wta = 0.f, wtb = 0.f;
+        for (int i = 0; i < nsub; ++i) {
+            const int sub = r0 + i * BB_SUB;
+            __syncthreads();
+            if (!P.has_dx) continue;
+            if (i == 0) {
+#pragma unroll
+                for (int kb = 0; kb < 3; ++kb)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) wra[kb][p] = *reinterpret_cast<const bf16x8*>(wrow0 + p * BB_WPLANE + 64 * kb);
+                wta = wtl[wr0 * 4 + lg];
+                wtb = wtl[wr1 * 4 + lg];
+            }
+            const unsigned char* buf = smw + (i & 1) * BB_BUF;
+            const unsigned char* drow = buf + BB_DP + (16 * h + lr) * BB_PITCH + 16 * lg;
+            const float dtl = reinterpret_cast<const float*>(buf + BB_DT)[(16 * h + lr) * 4 + lg];
+            f32x4 acc[2];
+            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wta, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            acc[1] = two ? __builtin_amdgcn_mfma_f32_16x16x4f32(wtb, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kb = 0; kb < 3; ++kb) {
+                bf16x8 db[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) db[p] = *reinterpret_cast<const bf16x8*>(drow + p * BB_PLANE + 64 * kb);
+                acc[0] = six(wra[kb], db, acc[0]);
+#pragma unroll
+                for (int p = 0; p < 3; ++p) wrb[kb][p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
+                if (two) acc[1] = six(wrb[kb], db, acc[1]);
+            }
+            const int m = sub + 16 * h + lr;
+            if (m < r1) {
+                const unsigned char* hrow = buf + BB_HP + (16 * h + lr) * BB_PITCH;
+                float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int col = 16 * (t0 + u) + 4 * lg;
+                    if ((u == 1 && !two) || col >= NI4) continue;
+                    const bf16x4 h0 = *reinterpret_cast<const bf16x4*>(hrow + 2 * col);
+                    const bf16x4 h1 = *reinterpret_cast<const bf16x4*>(hrow + BB_PLANE + 2 * col);
+                    const bf16x4 h2 = *reinterpret_cast<const bf16x4*>(hrow + 2 * BB_PLANE + 2 * col);
+                    f32x4 o;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float hv = ((float)h2[r] + (float)h1[r]) + (float)h0[r];
+                        o[r] = (col + r < P.n_in) ? acc[u][r] * act_grad_bf(P.act, hv) : 0.f;
+                    }
+                    *reinterpret_cast<f32x4*>(orow + col) = o;
+                }
+            }
+        }
+        __syncthreads();
+    } else {
+        // ---------------- dW role: row tiles {q, q + 4} x every column tile ----------------
+        // q = 3 (one row tile) on the SIMD whose dX waves carry four tiles (wave w runs on SIMD w % 4)
+        const int q = (wave - 8 + 3) & 3;
+        const bool two = __builtin_amdgcn_readfirstlane(q) + 4 < 7;
+        const int ntj = __builtin_amdgcn_readfirstlane((NI4 + 15) >> 4);
+        f32x4 acc[2][7];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) acc[s2][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int tro = bf6::tr_lane_off(lr, lg);
+        for (int i = 0; i < nsub; ++i) {
+            __syncthreads();
+            const unsigned char* buf = smw + (i & 1) * BB_BUF;
+            bf16x8 da[2][3], hb[2][3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                da[0][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * q);
+                da[1][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * (two ? q + 4 : q));
+                hb[0][p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 0);
+            }
+            // software pipeline: column tile t + 1's H fragments are read while tile t's MFMAs run
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                if (t >= ntj) break;                   // wave-uniform: column tiles past n_in (trunk layer 0)
+                if (t + 1 < ntj) {
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 16 * (t + 1));
+                }
+                acc[0][t] = six(da[0], hb[t & 1], acc[0][t]);
+                if (two) acc[1][t] = six(da[1], hb[t & 1], acc[1][t]);
+            }
+        }
+        float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            if (s2 == 1 && !two) continue;
+            const int tn = s2 == 0 ? q : q + 4;
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                const int j = 16 * t + lr;
+                if (t >= ntj || j >= NI4) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = 16 * tn + 4 * lg + r;
+                    if (n < P.n_out) part[(int64_t)n * NI4 + j] = (j < P.n_in) ? acc[s2][t][r] : 0.f;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // ---- db: fixed-order sum over the 32 staged rows of the per-slot column partials (written above) ----
+    __syncthreads();
+    if (tid < 25) {
+        const f32x4* red = reinterpret_cast<const f32x4*>(smw);
+        f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < BB_SUB; ++r) sacc += red[r * 25 + tid];
+        float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride + (int64_t)P.n_out * NI4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (4 * tid + e < P.n_out) part[4 * tid + e] = sacc[e];
+    }
+}
+
 bool bwd_bf_ok(const BwdArgs& a) {
     for (int i = 0; i < a.nprob; ++i) {
         const BwdProb& p = a.p[i];
@@ -427,10 +665,20 @@ extern "C" int vihmc_debug_bb_stamps(void* stamps, size_t stamp_bytes, void* rea
 }
 #endif
 
+// k_bwd_bf2 (dedicated staging waves) unless VIHMC_BWD_V2=0 (read once per process)
+static bool bwd_v2() {
+    static const bool on = [] {
+        const char* e = std::getenv("VIHMC_BWD_V2");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s) {
     if (!bwd_bf_ok(a)) return hipErrorInvalidValue;
     const int blocks = a.C * a.p[0].n_wg + (a.nprob > 1 ? a.C * a.p[1].n_wg : 0);
-    hipLaunchKernelGGL(k_bwd_bf, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
+    if (bwd_v2()) hipLaunchKernelGGL(k_bwd_bf2, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
+    else hipLaunchKernelGGL(k_bwd_bf, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
     return hipGetLastError();
 }
 

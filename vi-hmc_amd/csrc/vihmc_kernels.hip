@@ -218,7 +218,15 @@ constexpr int MLP_SLD = 65;
 // One log-posterior (+ gradient) evaluation of chain c by one wave. On entry w[] holds the chain's full weight
 // vector (frozen values with its sampled entries written); theta_at(k) is its k-th sampled value (prior term).
 // grad_out(k, value) receives the gradient at the sampled indices; returns logp (lane 0's value is the result).
-template <class ThetaAt, class GradOut>
+// Loops over layer widths / staged rows, optionally with a compile-time bound (MAXW > 0: fully unrolled with a
+// guard; the iteration order -- and so every rounding -- is that of the plain loop). Measured on the shipped BNN
+// (widths 10): MAXW = 16 took 34 us per leapfrog step against 21-23 us for the plain loops (MAXW = 0, shipped).
+#define VIHMC_MLP_FOR(v, n) \
+    _Pragma("unroll") for (int v = 0; v < (MAXW > 0 ? MAXW : (n)); ++v) if (MAXW == 0 || v < (n))
+#define VIHMC_MLP_ROWS(v, n) \
+    _Pragma("unroll") for (int v = 0; v < (MAXW > 0 ? 64 : (n)); ++v) if (MAXW == 0 || v < (n))
+
+template <int MAXW, class ThetaAt, class GradOut>
 __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* sm, int c, ThetaAt theta_at,
                                                 GradOut grad_out, bool want_grad, float* out) {
     // no implicit contraction into fma: the two kernels that inline this body (k_mlp, k_mlp_traj) must round
@@ -247,9 +255,9 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
         for (int l = 0; l < NL; ++l) {
             const MlpLayer L = a.L[l];
             const float* hin = hs + l * W * SLD;
-            for (int j = 0; j < L.n_out; ++j) {
+            VIHMC_MLP_FOR(j, L.n_out) {
                 float s = 0.f;
-                for (int i = 0; i < L.n_in; ++i) s = fmaf(w[L.w_off + j * L.n_in + i], hin[i * SLD + lane], s);
+                VIHMC_MLP_FOR(i, L.n_in) s = fmaf(w[L.w_off + j * L.n_in + i], hin[i * SLD + lane], s);
                 if (L.b_off >= 0) s += w[L.b_off + j];
                 zs[(l * W + j) * SLD + lane] = s;
                 hs[((l + 1) * W + j) * SLD + lane] = act_apply(L.act, s);
@@ -272,7 +280,7 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
         for (int l = NL - 1; l >= 0; --l) {
             const MlpLayer L = a.L[l];
             const float* hin = hs + l * W * SLD;
-            for (int j = 0; j < L.n_out; ++j) {
+            VIHMC_MLP_FOR(j, L.n_out) {
                 const float z = zs[(l * W + j) * SLD + lane];
                 const float h = hs[((l + 1) * W + j) * SLD + lane];
                 ds[j * SLD + lane] = gs[j * SLD + lane] * act_grad_z(L.act, z, h);
@@ -288,18 +296,18 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
                 float s = 0.f;
                 if (e < nw) {
                     const int j = e / L.n_in, i = e - j * L.n_in;
-                    for (int m = 0; m < nrow; ++m) s = fmaf(ds[j * SLD + m], hin[i * SLD + m], s);
+                    VIHMC_MLP_ROWS(m, nrow) s = fmaf(ds[j * SLD + m], hin[i * SLD + m], s);
                     gw[L.w_off + e] += s;
                 } else {
                     const int j = e - nw;
-                    for (int m = 0; m < nrow; ++m) s += ds[j * SLD + m];
+                    VIHMC_MLP_ROWS(m, nrow) s += ds[j * SLD + m];
                     gw[L.b_off + j] += s;
                 }
             }
             if (l > 0) {
-                for (int i = 0; i < L.n_in; ++i) {
+                VIHMC_MLP_FOR(i, L.n_in) {
                     float s = 0.f;
-                    for (int j = 0; j < L.n_out; ++j) s = fmaf(ds[j * SLD + lane], w[L.w_off + j * L.n_in + i], s);
+                    VIHMC_MLP_FOR(j, L.n_out) s = fmaf(ds[j * SLD + lane], w[L.w_off + j * L.n_in + i], s);
                     gs[i * SLD + lane] = s;
                 }
             }
@@ -324,6 +332,7 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
     return ll + (lp + a.prior_const) / (double)a.prior_scale;
 }
 
+template <int MAXW>
 __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
     extern __shared__ float sm[];
     float* w = sm;
@@ -334,7 +343,7 @@ __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
     __syncthreads();
     const float* th = a.theta + (int64_t)c * a.K;
     float* gr = a.grad ? a.grad + (int64_t)c * a.K : nullptr;
-    const double lp = mlp_eval_core(
+    const double lp = mlp_eval_core<MAXW>(
         a, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gr[k] = g; }, gr != nullptr, a.out);
     if (lane == 0) a.logp[c] = (float)lp;
 }
@@ -344,6 +353,7 @@ __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
 // every product and sum rounded separately (fp contract off: no fma), as the torch
 // elementwise ops round them, so the result is bitwise the step-by-step path. theta / momentum / gradient of
 // the chain live in LDS after the evaluation's workspace; one wave per chain, no host round trip per step.
+template <int MAXW>
 __global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t) {
     // products and sums written here are rounded separately (the HIP __fmul_rn / __fadd_rn helpers are plain * and
     // + defined in a header, outside this pragma's reach: the compiler fused them into fma)
@@ -371,7 +381,7 @@ __global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t
         __syncthreads();
         for (int k = lane; k < K; k += 64) w[a.idx[k]] = th[k];
         __syncthreads();
-        lp = mlp_eval_core(
+        lp = mlp_eval_core<MAXW>(
             a, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gk[k] = g; }, true, nullptr);
         for (int k = lane; k < K; k += 64) pm[k] = pm[k] + e * gk[k];
     }
@@ -433,7 +443,7 @@ size_t mlp_lds_bytes(int D, int n_layers, int maxw) {
 hipError_t launch_mlp(const MlpArgs& a, int C, int maxw, hipStream_t s) {
     const size_t shm = mlp_lds_bytes(a.D, a.n_layers, maxw);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
-    VIHMC_LAUNCH(k_mlp, dim3(C), dim3(64), shm, s, a, maxw);
+    VIHMC_LAUNCH(k_mlp<0>, dim3(C), dim3(64), shm, s, a, maxw);
 }
 
 hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int maxw, hipStream_t s) {
@@ -442,7 +452,7 @@ hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int ma
     if (shm > 160 * 1024 || t.L < 1) return hipErrorInvalidValue;
     MlpTrajArgs tt = t;
     tt.ws_floats = (int32_t)(ws / sizeof(float));
-    VIHMC_LAUNCH(k_mlp_traj, dim3(C), dim3(64), shm, s, a, maxw, tt);
+    VIHMC_LAUNCH(k_mlp_traj<0>, dim3(C), dim3(64), shm, s, a, maxw, tt);
 }
 
 }  // namespace vihmc

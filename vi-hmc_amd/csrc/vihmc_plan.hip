@@ -44,8 +44,8 @@ inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 struct LayerPk {
     int n_out, n_in, ldi, ldo, act;
     int64_t wp, bias, wt;
-    // dW partials
-    int n_chunks;
+    // dW partials: one slab per row chunk of rows_per_chunk rows
+    int n_chunks, rows_per_chunk;
     int64_t part_off, part_stride;
 };
 
@@ -396,8 +396,19 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             n.rows_per_chunk = (int)R;
         }
         int64_t po = 0;
-        for (auto& L : n.L) {
-            L.n_chunks = cdiv(n.rows, n.rows_per_chunk);
+        for (size_t j = 0; j < n.L.size(); ++j) {
+            LayerPk& L = n.L[j];
+            // the input layer has no dX: its launch is dW only, and the branch input layer (K = 101: all seven
+            // column tiles) is ~7x the work per row of the trunk one (K = 5: one tile) -- with the common chunk
+            // the branch workgroups alone set that launch (41 us of 64-us-class launches at C = 16). Its chunks
+            // are cut to VIHMC_BWD_L0_ROWS rows (default 128: 4 sub-tiles) so they fit beside the trunk ones.
+            L.rows_per_chunk = n.rows_per_chunk;
+            if (j == 0 && L.n_in >= 64) {
+                int r0 = 128;
+                if (const char* e = std::getenv("VIHMC_BWD_L0_ROWS")) r0 = std::max(32, std::atoi(e) / 32 * 32);
+                L.rows_per_chunk = std::min(n.rows_per_chunk, r0);
+            }
+            L.n_chunks = cdiv(n.rows, L.rows_per_chunk);
             L.part_stride = r4((int64_t)L.n_out * L.ldi + L.n_out);
             L.part_off = po;
             po += L.part_stride * L.n_chunks;
@@ -777,7 +788,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
                 q.n_in = L.n_in;
                 q.act = j >= 1 ? n.L[j - 1].act : 0;
                 q.has_dx = j >= 1;
-                q.rows_per_wg = n.rows_per_chunk;
+                q.rows_per_wg = L.rows_per_chunk;
                 q.n_wg = L.n_chunks;
                 nti = std::max(nti, nt_of(L.n_in));
             }
