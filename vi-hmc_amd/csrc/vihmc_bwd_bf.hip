@@ -439,6 +439,14 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
     const int r0 = wg * P.rows_per_wg;
     const int r1 = min(P.M, r0 + P.rows_per_wg);
     const int nsub = r1 > r0 ? (r1 - r0 + BB_SUB - 1) / BB_SUB : 0;
+#if BB_STAMP
+    const bool samp = second && P.has_dx && (b % 16) == 0 && b / 16 < BBS_WG;
+    const int sidx = b / 16;
+    if (samp && tid == 0) {
+        bb_real[sidx][0][0] = __builtin_amdgcn_s_memtime();
+        bb_real[sidx][0][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 
     // ---- W^T planes (once per workgroup): rows i < n_in, features k < 100 ----
     if (P.has_dx) {
@@ -456,6 +464,12 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         }
     }
 
+#ifndef B2_PRIO
+#define B2_PRIO 1       // static wave priority: 1 = staging waves at 1 (the youngest waves, and the critical path
+                        // of the sub-tile period without it: stamps, profiles/r02p_stamps.log); 2 = staging 2, dW 1
+#endif
+    if (B2_PRIO >= 1 && wave >= 12) __builtin_amdgcn_s_setprio(B2_PRIO);
+    if (B2_PRIO == 2 && wave >= 8 && wave < 12) __builtin_amdgcn_s_setprio(1);
     if (wave >= 12) {
         // ---------------- staging role: item idx = t + 256 v -> D (row, c4) for idx < 800, else H ----------------
         const int t = tid - 768;
@@ -507,12 +521,17 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             store(r0, 0);
             if (nsub > 1) load(r0 + BB_SUB);
         }
+        // (issuing each slot's next load right after that slot's store instead measured 2x slower: the compiler's
+        // conservative vmcnt waits then serialised every slot on the HBM latency, profiles/r02s_stamps.log)
         for (int i = 0; i < nsub; ++i) {
             __syncthreads();                           // buffer i&1 holds sub-tile i, (i+1)&1 is free
+            VIHMC_BB_STAMP(i, 0)
             if (i + 1 < nsub) {
                 store(r0 + (i + 1) * BB_SUB, (i + 1) & 1);
                 if (i + 2 < nsub) load(r0 + (i + 2) * BB_SUB);
             }
+            VIHMC_BB_STAMP(i, 1)
+            VIHMC_BB_STAMP(i, 2)
         }
         // db: per-slot column partials -> LDS [32 rows][25 float4] -> fixed-order sum over rows (below)
         __syncthreads();
@@ -534,6 +553,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         for (int i = 0; i < nsub; ++i) {
             const int sub = r0 + i * BB_SUB;
             __syncthreads();
+            VIHMC_BB_STAMP(i, 0)
             if (!P.has_dx) continue;
             if (i == 0) {
 #pragma unroll
@@ -560,6 +580,10 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 for (int p = 0; p < 3; ++p) wrb[kb][p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
                 if (two) acc[1] = six(wrb[kb], db, acc[1]);
             }
+#if BB_STAMP
+            asm volatile("" :: "v"(acc[0]), "v"(acc[1]));
+            VIHMC_BB_STAMP(i, 1)
+#endif
             const int m = sub + 16 * h + lr;
             if (m < r1) {
                 const unsigned char* hrow = buf + BB_HP + (16 * h + lr) * BB_PITCH;
@@ -580,6 +604,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                     *reinterpret_cast<f32x4*>(orow + col) = o;
                 }
             }
+            VIHMC_BB_STAMP(i, 2)
         }
         __syncthreads();
     } else {
@@ -596,6 +621,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         const int tro = bf6::tr_lane_off(lr, lg);
         for (int i = 0; i < nsub; ++i) {
             __syncthreads();
+            VIHMC_BB_STAMP(i, 0)
             const unsigned char* buf = smw + (i & 1) * BB_BUF;
             bf16x8 da[2][3], hb[2][3];
 #pragma unroll
@@ -615,6 +641,11 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 acc[0][t] = six(da[0], hb[t & 1], acc[0][t]);
                 if (two) acc[1][t] = six(da[1], hb[t & 1], acc[1][t]);
             }
+#if BB_STAMP
+            asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][6]));
+            VIHMC_BB_STAMP(i, 1)
+            VIHMC_BB_STAMP(i, 2)
+#endif
         }
         float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride;
 #pragma unroll
@@ -645,6 +676,12 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         for (int e = 0; e < 4; ++e)
             if (4 * tid + e < P.n_out) part[4 * tid + e] = sacc[e];
     }
+#if BB_STAMP
+    if (samp && tid == 0) {
+        bb_real[sidx][1][0] = __builtin_amdgcn_s_memtime();
+        bb_real[sidx][1][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 bool bwd_bf_ok(const BwdArgs& a) {
@@ -665,19 +702,19 @@ extern "C" int vihmc_debug_bb_stamps(void* stamps, size_t stamp_bytes, void* rea
 }
 #endif
 
-// k_bwd_bf2 (dedicated staging waves) unless VIHMC_BWD_V2=0 (read once per process)
-static bool bwd_v2() {
-    static const bool on = [] {
+// layer-backward kernel: VIHMC_BWD_V2 = 0 k_bwd_bf, otherwise (default) k_bwd_bf2 (read once per process)
+static int bwd_v2() {
+    static const int v = [] {
         const char* e = std::getenv("VIHMC_BWD_V2");
-        return !(e && e[0] == '0');
+        return e ? std::atoi(e) : 2;
     }();
-    return on;
+    return v;
 }
 
 hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s) {
     if (!bwd_bf_ok(a)) return hipErrorInvalidValue;
     const int blocks = a.C * a.p[0].n_wg + (a.nprob > 1 ? a.C * a.p[1].n_wg : 0);
-    if (bwd_v2()) hipLaunchKernelGGL(k_bwd_bf2, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
+    if (bwd_v2() != 0) hipLaunchKernelGGL(k_bwd_bf2, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
     else hipLaunchKernelGGL(k_bwd_bf, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
     return hipGetLastError();
 }

@@ -75,9 +75,14 @@ def main():
     g0 = int(np.nonzero(ok)[0][0])
     print("workgroup", g0, "sub-tile 5, per wave: barrier exit / staging done / MFMAs done, from the first exit")
     t0 = st[g0, :, 5, 0].min()
+    v2 = os.environ.get("VIHMC_BWD_V2", "1") != "0"
     for w in range(16):
-        print(f"  wave {w:2d} {'dX' if w < 8 else 'dW'} SIMD {w % 4}  {st[g0, w, 5, 0] - t0:6.0f} "
+        role = ("dX" if w < 8 else "dW" if w < 12 else "stg") if v2 else ("dX" if w < 8 else "dW")
+        print(f"  wave {w:2d} {role:3s} SIMD {w % 4}  {st[g0, w, 5, 0] - t0:6.0f} "
               f"{st[g0, w, 5, 1] - t0:6.0f} {st[g0, w, 5, 2] - t0:6.0f}")
+    if v2:
+        print("k_bwd_bf2 stamps: dX [1] = MFMAs done, [2] = epilogue stored; dW [1] = [2] = MFMAs done; "
+              "staging [1] = [2] = next sub-tile staged (the 'staging done' rows above mix roles)")
     eng.close()
 
 
