@@ -128,6 +128,16 @@ int vihmc_mlp_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out,
                          const float* g_in, float* g_out, float* logp_out, const float* eps, const float* inv_mass,
                          int L, int C, void* stream);
 
+/* Any plan: one whole leapfrog trajectory, the contract of vihmc_mlp_trajectory (which it calls for BNN plans).
+ * DeepONet plans: one opening kernel (p = p_in + (eps/2) g_in; theta = theta_in + eps p) and L evaluations
+ * whose gradient gather applies the momentum step and the next position step in place (theta_out and p_out
+ * hold the running state; no torch elementwise kernels per step). Same rounding as the step-by-step path,
+ * so the result is bitwise that path. Replaces hamiltorch's leapfrog loop over params_grad
+ *  for every config's Sampler.HMC / HMC_NUTS trajectory. */
+int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, const float* p_in, float* p_out,
+                     const float* g_in, float* g_out, float* logp_out, const float* eps, const float* inv_mass,
+                     int L, int C, void* stream);
+
 /* Plan introspection: 0 = DeepONet, 1 = MLP; D; K; max_chains; device bytes owned. */
 /* Sensitivity scores of every parameter at theta (chain 0 of the plan, [K] device):
  *   out[d] = sigma[d]^2 * mean over outputs of (d f / d theta_d)^2,  d < D, flat (named_parameters) order.

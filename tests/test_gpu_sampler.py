@@ -82,6 +82,37 @@ def test_sharding_independence(cuda_device):
 
 
 @pytest.mark.parametrize("variant", ["hmc", "inv_mass", "nuts"])
+def test_deeponet_fused_trajectory_bitwise_equals_stepwise(variant, cuda_device):
+    """vihmc_trajectory on a DeepONet plan (leapfrog updates fused into the gradient gather) == L separate
+    evaluations driven by the torch elementwise updates, bit for bit: positions, accepts, log-probs, step sizes."""
+    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.samplers import ChainRNG, EngineEvaluator, Sampler, run_chains
+    c = deeponet_case("deeponet_small")
+    p = c.prob
+    C = 3
+    th0 = torch.tensor(c.thetas[0])
+    kw = dict(burn=2)
+    if variant == "inv_mass":
+        kw["inv_mass"] = torch.linspace(0.5, 1.5, th0.numel())
+    if variant == "nuts":
+        kw.update(sampler=Sampler.HMC_NUTS, burn=4)
+    out = []
+    for fused in (True, False):
+        eng = DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
+                             c.prior_sd, c.loss, c.tau_out, max_chains=C, device=cuda_device)
+        eng.fused_trajectory = fused
+        out.append(run_chains(EngineEvaluator(eng), th0[None].repeat(C, 1), 8, 7, 2e-3,
+                              rng=ChainRNG(C, th0.numel(), cuda_device, seeds=[20 + i for i in range(C)]), **kw))
+    a, b = out
+    assert torch.equal(a.accepted, b.accepted)
+    assert torch.equal(a.counts, b.counts)
+    assert torch.equal(a.samples[:, :int(a.counts.max())], b.samples[:, :int(b.counts.max())])
+    assert torch.equal(a.logp_trace, b.logp_trace)
+    assert a.step_size == b.step_size
+    assert a.n_grad_evals == b.n_grad_evals
+
+
+@pytest.mark.parametrize("variant", ["hmc", "inv_mass", "nuts"])
 def test_bnn_fused_trajectory_bitwise_equals_stepwise(variant, cuda_device):
     """vihmc_mlp_trajectory (one launch per trajectory) == L separate evaluations driven by the torch
     elementwise updates, bit for bit: positions, accept decisions, log-probs and step sizes."""

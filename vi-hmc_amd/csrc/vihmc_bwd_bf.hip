@@ -21,6 +21,7 @@
 #include "vihmc_internal.h"
 #include "vihmc_bf16x6.h"
 #include <cstdlib>
+#include <type_traits>
 
 #ifndef BB_ABL
 #define BB_ABL 0    // timing-only ablations (wrong results): 1 no loads after the first sub-tile, 2 no dX
@@ -420,7 +421,6 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf(BwdArgs args) {
 // the SIMD. dW: wave q owns output row tiles {q, q + 4} (q + 4 < 7) x every column tile.
 // ---------------------------------------------------------------------------------------------------------
 constexpr int B2_SLOTS = 7;                            // staged float4 per staging thread (<= 800 D + 896 H)
-constexpr int B2_DCOL = 4;                             // of them D slots (idx < 800 = 3.125 x 256)
 
 __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
@@ -484,197 +484,240 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             const int r = e / q, c4 = e - r * q;
             st[v] = idx < ntot ? (r << 8) | c4 : -1;
         }
-        f32x4 pf[B2_SLOTS];
-        f32x4 dcol[B2_DCOL];
-#pragma unroll
-        for (int v = 0; v < B2_DCOL; ++v) dcol[v] = f32x4{0.f, 0.f, 0.f, 0.f};
-        auto load = [&](int sub) {
+        // db column: H column NI4 of both buffers is the constant 1 (planes 1, 0, 0), never overwritten by the
+        // H stores (columns < NI4), so the dW MFMAs produce part[n][NI4] = sum_m D[m][n] = db[n] exactly
+        // (the products D x 1 are exact; fp32 accumulation) in the column tile that already covers it
+        if (t < 2 * BB_SUB) {
+            unsigned char* o = smw + (t >> 5) * BB_BUF + BB_HP + (t & 31) * BB_PITCH + 2 * NI4;
+            *reinterpret_cast<unsigned short*>(o) = 0x3F80;
+            *reinterpret_cast<unsigned short*>(o + BB_PLANE) = 0;
+            *reinterpret_cast<unsigned short*>(o + 2 * BB_PLANE) = 0;
+        }
+        // two register sets: sub-tile s is loaded into set s & 1 two sub-tiles before its store, so a load has
+        // a whole sub-tile period plus the store phase to land (one set: issued ~500 cycles before its use,
+        // the staging waves waited out the HBM latency every period -- profiles/r02_bwd/v2_stamps.log)
+        f32x4 pfa[B2_SLOTS], pfb[B2_SLOTS];
+        // slots 0-2 are D items, slot 3 D for t < 32, slots 4-6 H: per slot a 32-bit byte offset from the
+        // sub-tile's (uniform) row base, so the loads take the SGPR-base form and no 64-bit addresses stay live
+        static_assert(3 * 256 < BB_SUB * 25 && BB_SUB * 25 <= 3 * 256 + 32, "D slots");
+        auto load = [&](int sub, f32x4 (&pf)[B2_SLOTS]) __attribute__((always_inline)) {
+            const int rmax = P.M - 1 - sub;
+            const char* db = reinterpret_cast<const char*>(D + (int64_t)sub * P.ldd);
+            const char* hb = reinterpret_cast<const char*>(H + (int64_t)sub * P.ldh);
 #pragma unroll
             for (int v = 0; v < B2_SLOTS; ++v) {
-                const int row = min(sub + (max(st[v], 0) >> 8), P.M - 1);
-                const int c4 = max(st[v], 0) & 255;      // idle slots read column 0 of a valid row: in bounds
-                pf[v] = (t + 256 * v < nd) ? reinterpret_cast<const f32x4*>(D + (int64_t)row * P.ldd)[c4]
-                                           : reinterpret_cast<const f32x4*>(H + (int64_t)row * P.ldh)[c4];
+                const int sv = max(st[v], 0);            // idle slots read column 0 of a valid row: in bounds
+                const int r = min(sv >> 8, rmax), c4 = sv & 255;
+                const bool isd = v < 3 || (v == 3 && t < 32);
+                const unsigned off = 4u * (unsigned)(r * (isd ? P.ldd : P.ldh) + 4 * c4);
+                pf[v] = *reinterpret_cast<const f32x4*>((isd ? db : hb) + off);
             }
         };
-        auto store = [&](int sub, int buf) {
+        auto store = [&](int sub, int buf, const f32x4 (&pf)[B2_SLOTS]) __attribute__((always_inline)) {
 #pragma unroll
             for (int v = 0; v < B2_SLOTS; ++v) {
                 if (st[v] < 0) continue;
                 const int r = st[v] >> 8, c4 = st[v] & 255;
                 const f32x4 x = (sub + r < r1) ? pf[v] : f32x4{0.f, 0.f, 0.f, 0.f};
-                const bool isd = t + 256 * v < nd;
+                const bool isd = v < 3 || (v == 3 && t < 32);
                 unsigned char* base = smw + buf * BB_BUF + (isd ? BB_DP : BB_HP) + r * BB_PITCH + 8 * c4;
                 bf16x4 p0, p1, p2;
                 split4(x, p0, p1, p2);
                 *reinterpret_cast<bf16x4*>(base) = p0;
                 *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;
                 *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;
-                if (isd) {
-                    if (v < B2_DCOL) dcol[v < B2_DCOL ? v : 0] += x;
-                    if (c4 == 24) *reinterpret_cast<f32x4*>(smw + buf * BB_BUF + BB_DT + r * 16) = x;
-                }
+                if (isd && c4 == 24) *reinterpret_cast<f32x4*>(smw + buf * BB_BUF + BB_DT + r * 16) = x;
             }
         };
+        // Loop unrolled by two so set A is always the newest in flight at the loop head, and every load issued
+        // unconditionally (rows past the chunk read its last sub-tile again, an L2 hit): with a conditional load or
+        // a set index that alternates at run time, the compiler's merged wait state treated both sets as newest
+        // and waited for the sub-tile two ahead (vmcnt(0)) before every store.
+        const int slast = r0 + max(nsub - 1, 0) * BB_SUB;
+        auto sub_at = [&](int k) { return min(r0 + k * BB_SUB, slast); };
         if (nsub > 0) {
-            load(r0);
-            store(r0, 0);
-            if (nsub > 1) load(r0 + BB_SUB);
+            load(sub_at(0), pfa);
+            load(sub_at(1), pfb);
+            store(r0, 0, pfa);
+            load(sub_at(2), pfa);
         }
-        // (issuing each slot's next load right after that slot's store instead measured 2x slower: the compiler's
-        // conservative vmcnt waits then serialised every slot on the HBM latency, profiles/r02s_stamps.log)
-        for (int i = 0; i < nsub; ++i) {
-            __syncthreads();                           // buffer i&1 holds sub-tile i, (i+1)&1 is free
+        int i = 0;
+        for (; i + 1 < nsub; i += 2) {
+            __syncthreads();                           // buffer 0 holds sub-tile i, buffer 1 is free
             VIHMC_BB_STAMP(i, 0)
-            if (i + 1 < nsub) {
-                store(r0 + (i + 1) * BB_SUB, (i + 1) & 1);
-                if (i + 2 < nsub) load(r0 + (i + 2) * BB_SUB);
-            }
+            store(r0 + (i + 1) * BB_SUB, 1, pfb);
+            load(sub_at(i + 3), pfb);
+            VIHMC_BB_STAMP(i, 1)
+            VIHMC_BB_STAMP(i, 2)
+            __syncthreads();                           // buffer 1 holds sub-tile i + 1, buffer 0 is free
+            VIHMC_BB_STAMP(i + 1, 0)
+            if (i + 2 < nsub) store(r0 + (i + 2) * BB_SUB, 0, pfa);
+            load(sub_at(i + 4), pfa);
+            VIHMC_BB_STAMP(i + 1, 1)
+            VIHMC_BB_STAMP(i + 1, 2)
+        }
+        if (i < nsub) {
+            __syncthreads();                           // the last sub-tile (odd count): nothing left to stage
+            VIHMC_BB_STAMP(i, 0)
             VIHMC_BB_STAMP(i, 1)
             VIHMC_BB_STAMP(i, 2)
         }
-        // db: per-slot column partials -> LDS [32 rows][25 float4] -> fixed-order sum over rows (below)
-        __syncthreads();
-        f32x4* red = reinterpret_cast<f32x4*>(smw);
-#pragma unroll
-        for (int v = 0; v < B2_DCOL; ++v)
-            if (st[v] >= 0 && t + 256 * v < nd) red[(st[v] >> 8) * 25 + (st[v] & 255)] = dcol[v];
     } else if (wave < 8) {
         // ---------------- dX role: i-tiles {2p, 2p+1} x row half h (as k_bwd_bf) ----------------
+        // The role body is instantiated per tile count (TWO) and the epilogue per activation (tanh or the rest),
+        // so no exec-masked branch splits the LDS reads from the MFMAs that consume them: hipcc then issues
+        // the nine D fragment reads of a sub-tile ahead with counted lgkmcnt waits (with `if (two)` regions
+        // between them every read was waited for right before its MFMA).
         const int h = wave & 1, p2 = wave >> 1;
-        const int t0 = 2 * p2;
-        const bool two = t0 + 1 < 7;
+        const int t0 = 2 * __builtin_amdgcn_readfirstlane(p2);
         const unsigned char* wrow0 = smw + BB_W + min(16 * t0 + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
         const unsigned char* wrow1 = smw + BB_W + min(16 * (t0 + 1) + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
         const float* wtl = reinterpret_cast<const float*>(smw + BB_WT);
         const int wr0 = min(16 * t0 + lr, P.n_in - 1), wr1 = min(16 * (t0 + 1) + lr, P.n_in - 1);
-        bf16x8 wra[3][3], wrb[3][3];
-        float wta = 0.f, wtb = 0.f;
-        for (int i = 0; i < nsub; ++i) {
-            const int sub = r0 + i * BB_SUB;
-            __syncthreads();
-            VIHMC_BB_STAMP(i, 0)
-            if (!P.has_dx) continue;
-            if (i == 0) {
+        auto dx_run = [&](auto two_c) __attribute__((always_inline)) {
+            constexpr bool TWO = decltype(two_c)::value;
+            bf16x8 wra[3][3];
+            float wta = 0.f, wtb = 0.f;
+            for (int i = 0; i < nsub; ++i) {
+                const int sub = r0 + i * BB_SUB;
+                __syncthreads();
+                VIHMC_BB_STAMP(i, 0)
+                if (!P.has_dx) continue;
+                if (i == 0) {
+#pragma unroll
+                    for (int kb = 0; kb < 3; ++kb)
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            wra[kb][p] = *reinterpret_cast<const bf16x8*>(wrow0 + p * BB_WPLANE + 64 * kb);
+                    wta = wtl[wr0 * 4 + lg];
+                    if (TWO) wtb = wtl[wr1 * 4 + lg];
+                }
+                const unsigned char* buf = smw + (i & 1) * BB_BUF;
+                const unsigned char* drow = buf + BB_DP + (16 * h + lr) * BB_PITCH + 16 * lg;
+                bf16x8 db[3][3];
 #pragma unroll
                 for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-                    for (int p = 0; p < 3; ++p) wra[kb][p] = *reinterpret_cast<const bf16x8*>(wrow0 + p * BB_WPLANE + 64 * kb);
-                wta = wtl[wr0 * 4 + lg];
-                wtb = wtl[wr1 * 4 + lg];
-            }
-            const unsigned char* buf = smw + (i & 1) * BB_BUF;
-            const unsigned char* drow = buf + BB_DP + (16 * h + lr) * BB_PITCH + 16 * lg;
-            const float dtl = reinterpret_cast<const float*>(buf + BB_DT)[(16 * h + lr) * 4 + lg];
-            f32x4 acc[2];
-            acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wta, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            acc[1] = two ? __builtin_amdgcn_mfma_f32_16x16x4f32(wtb, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0)
-                         : f32x4{0.f, 0.f, 0.f, 0.f};
+                    for (int p = 0; p < 3; ++p) db[kb][p] = *reinterpret_cast<const bf16x8*>(drow + p * BB_PLANE + 64 * kb);
+                const float dtl = reinterpret_cast<const float*>(buf + BB_DT)[(16 * h + lr) * 4 + lg];
+                f32x4 acc[2];
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wta, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                acc[1] = TWO ? __builtin_amdgcn_mfma_f32_16x16x4f32(wtb, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0)
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int kb = 0; kb < 3; ++kb) {
-                bf16x8 db[3];
+                for (int kb = 0; kb < 3; ++kb) {
+                    acc[0] = six(wra[kb], db[kb], acc[0]);
+                    if (TWO) {
+                        bf16x8 wb[3];
 #pragma unroll
-                for (int p = 0; p < 3; ++p) db[p] = *reinterpret_cast<const bf16x8*>(drow + p * BB_PLANE + 64 * kb);
-                acc[0] = six(wra[kb], db, acc[0]);
-#pragma unroll
-                for (int p = 0; p < 3; ++p) wrb[kb][p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
-                if (two) acc[1] = six(wrb[kb], db, acc[1]);
-            }
+                        for (int p = 0; p < 3; ++p) wb[p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
+                        acc[1] = six(wb, db[kb], acc[1]);
+                    }
+                }
 #if BB_STAMP
-            asm volatile("" :: "v"(acc[0]), "v"(acc[1]));
-            VIHMC_BB_STAMP(i, 1)
+                asm volatile("" :: "v"(acc[0]), "v"(acc[1]));
+                VIHMC_BB_STAMP(i, 1)
 #endif
-            const int m = sub + 16 * h + lr;
-            if (m < r1) {
+                const int m = sub + 16 * h + lr;
                 const unsigned char* hrow = buf + BB_HP + (16 * h + lr) * BB_PITCH;
                 float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
+                auto epi = [&](auto tanh_c) __attribute__((always_inline)) {
+                    constexpr bool TANH = decltype(tanh_c)::value;
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int col = 16 * (t0 + u) + 4 * lg;
-                    if ((u == 1 && !two) || col >= NI4) continue;
-                    const bf16x4 h0 = *reinterpret_cast<const bf16x4*>(hrow + 2 * col);
-                    const bf16x4 h1 = *reinterpret_cast<const bf16x4*>(hrow + BB_PLANE + 2 * col);
-                    const bf16x4 h2 = *reinterpret_cast<const bf16x4*>(hrow + 2 * BB_PLANE + 2 * col);
-                    f32x4 o;
+                    for (int u = 0; u < (TWO ? 2 : 1); ++u) {
+                        const int col = 16 * (t0 + u) + 4 * lg;
+                        if (m >= r1 || col >= NI4) continue;
+                        const bf16x4 h0 = *reinterpret_cast<const bf16x4*>(hrow + 2 * col);
+                        const bf16x4 h1 = *reinterpret_cast<const bf16x4*>(hrow + BB_PLANE + 2 * col);
+                        const bf16x4 h2 = *reinterpret_cast<const bf16x4*>(hrow + 2 * BB_PLANE + 2 * col);
+                        f32x4 o;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float hv = ((float)h2[r] + (float)h1[r]) + (float)h0[r];
-                        o[r] = (col + r < P.n_in) ? acc[u][r] * act_grad_bf(P.act, hv) : 0.f;
+                        for (int r = 0; r < 4; ++r) {
+                            const float hv = ((float)h2[r] + (float)h1[r]) + (float)h0[r];
+                            const float gd = TANH ? 1.f - hv * hv : act_grad_bf(P.act, hv);
+                            o[r] = (col + r < P.n_in) ? acc[u][r] * gd : 0.f;
+                        }
+                        *reinterpret_cast<f32x4*>(orow + col) = o;
                     }
-                    *reinterpret_cast<f32x4*>(orow + col) = o;
-                }
+                };
+                if (P.act == ACT_TANH) epi(std::true_type{});
+                else epi(std::false_type{});
+                VIHMC_BB_STAMP(i, 2)
             }
-            VIHMC_BB_STAMP(i, 2)
-        }
-        __syncthreads();
+        };
+        if (t0 + 1 < 7) dx_run(std::true_type{});
+        else dx_run(std::false_type{});
     } else {
-        // ---------------- dW role: row tiles {q, q + 4} x every column tile ----------------
-        // q = 3 (one row tile) on the SIMD whose dX waves carry four tiles (wave w runs on SIMD w % 4)
-        const int q = (wave - 8 + 3) & 3;
-        const bool two = __builtin_amdgcn_readfirstlane(q) + 4 < 7;
-        const int ntj = __builtin_amdgcn_readfirstlane((NI4 + 15) >> 4);
+        // ---------------- dW role: two row tiles per wave, the second over a column range ----------------
+        // Waves w, w + 4, w + 8, w + 12 share a SIMD. The dX waves of SIMD groups 0 and 1 (waves 0/4, 1/5) carry
+        // four tile-jobs of 20 MFMA-equivalents, those of groups 2 and 3 three; a dW (row, column) tile-job is 6
+        // MFMAs. Groups 2 and 3 (waves 10, 11) take row tiles {0, 1} and {2, 3} whole (14 jobs), groups 0 and 1
+        // (waves 8, 9) row tile 4 or 5 whole plus row tile 6 (rows 96..99 of n_out) over columns 0..3 or 4..6:
+        // at most 146 MFMA-equivalents per SIMD (row tiles {q, q + 4} per wave: 164 on one SIMD).
+        const int g = __builtin_amdgcn_readfirstlane(wave - 8);
+        const int rta = g == 2 ? 0 : g == 3 ? 2 : 4 + g;               // first row tile, all column tiles
+        const int rtb = g == 2 ? 1 : g == 3 ? 3 : 6;                   // second row tile over [cb0, cb1)
+        const int cb0 = g == 1 ? 4 : 0, cb1 = g == 0 ? 4 : 7;
+        const int ntj = __builtin_amdgcn_readfirstlane((NI4 + 16) >> 4);   // through the db column NI4
         f32x4 acc[2][7];
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
             for (int t = 0; t < 7; ++t) acc[s2][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int tro = bf6::tr_lane_off(lr, lg);
-        for (int i = 0; i < nsub; ++i) {
-            __syncthreads();
-            VIHMC_BB_STAMP(i, 0)
-            const unsigned char* buf = smw + (i & 1) * BB_BUF;
-            bf16x8 da[2][3], hb[2][3];
+        // instantiated for 7 column tiles (every layer but the trunk input layer) with the tile loop's reads
+        // unconditional, so the next tile's H reads stay in flight under this tile's MFMAs (a run-time tile count
+        // made them conditional, and hipcc then waited lgkmcnt(0) -- for the prefetch too -- before each tile)
+        auto dw_run = [&](auto nt_c) __attribute__((always_inline)) {
+            constexpr int NT = decltype(nt_c)::value;                  // 0: ntj at run time
+            const int nt = NT ? NT : ntj;
+            for (int i = 0; i < nsub; ++i) {
+                __syncthreads();
+                VIHMC_BB_STAMP(i, 0)
+                const unsigned char* buf = smw + (i & 1) * BB_BUF;
+                bf16x8 da[2][3], hb[2][3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) {
-                da[0][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * q);
-                da[1][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * (two ? q + 4 : q));
-                hb[0][p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 0);
-            }
-            // software pipeline: column tile t + 1's H fragments are read while tile t's MFMAs run
-#pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                if (t >= ntj) break;                   // wave-uniform: column tiles past n_in (trunk layer 0)
-                if (t + 1 < ntj) {
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 16 * (t + 1));
+                for (int p = 0; p < 3; ++p) {
+                    da[0][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * rta);
+                    da[1][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * rtb);
+                    hb[0][p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 0);
                 }
-                acc[0][t] = six(da[0], hb[t & 1], acc[0][t]);
-                if (two) acc[1][t] = six(da[1], hb[t & 1], acc[1][t]);
-            }
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    if (t >= nt) break;                    // wave-uniform (NT = 0 only)
+                    if (t + 1 < nt) {
+#pragma unroll
+                        for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 16 * (t + 1));
+                    }
+                    acc[0][t] = six(da[0], hb[t & 1], acc[0][t]);
+                    if (t >= cb0 && t < cb1) acc[1][t] = six(da[1], hb[t & 1], acc[1][t]);
+                }
 #if BB_STAMP
-            asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][6]));
-            VIHMC_BB_STAMP(i, 1)
-            VIHMC_BB_STAMP(i, 2)
+                asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][6]));
+                VIHMC_BB_STAMP(i, 1)
+                VIHMC_BB_STAMP(i, 2)
 #endif
-        }
+            }
+        };
+        if (ntj == 7) dw_run(std::integral_constant<int, 7>{});
+        else dw_run(std::integral_constant<int, 0>{});
         float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-            if (s2 == 1 && !two) continue;
-            const int tn = s2 == 0 ? q : q + 4;
+            const int tn = s2 == 0 ? rta : rtb;
 #pragma unroll
             for (int t = 0; t < 7; ++t) {
                 const int j = 16 * t + lr;
-                if (t >= ntj || j >= NI4) continue;
+                if (t >= ntj || j > NI4 || (s2 == 1 && (t < cb0 || t >= cb1))) continue;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int n = 16 * tn + 4 * lg + r;
-                    if (n < P.n_out) part[(int64_t)n * NI4 + j] = (j < P.n_in) ? acc[s2][t][r] : 0.f;
+                    if (n >= P.n_out) continue;
+                    if (j == NI4) part[(int64_t)P.n_out * NI4 + n] = acc[s2][t][r];     // db
+                    else part[(int64_t)n * NI4 + j] = (j < P.n_in) ? acc[s2][t][r] : 0.f;
                 }
             }
         }
-        __syncthreads();
-    }
-    // ---- db: fixed-order sum over the 32 staged rows of the per-slot column partials (written above) ----
-    __syncthreads();
-    if (tid < 25) {
-        const f32x4* red = reinterpret_cast<const f32x4*>(smw);
-        f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
-        for (int r = 0; r < BB_SUB; ++r) sacc += red[r * 25 + tid];
-        float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride + (int64_t)P.n_out * NI4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (4 * tid + e < P.n_out) part[4 * tid + e] = sacc[e];
     }
 #if BB_STAMP
     if (samp && tid == 0) {
@@ -714,7 +757,10 @@ static int bwd_v2() {
 hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s) {
     if (!bwd_bf_ok(a)) return hipErrorInvalidValue;
     const int blocks = a.C * a.p[0].n_wg + (a.nprob > 1 ? a.C * a.p[1].n_wg : 0);
-    if (bwd_v2() != 0) hipLaunchKernelGGL(k_bwd_bf2, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
+    // k_bwd_bf2 keeps its db column at H column NI4 inside the last column tile: NI4 < 112
+    bool v2 = bwd_v2() != 0;
+    for (int i = 0; i < a.nprob; ++i) v2 = v2 && ((a.p[i].n_in + 3) & ~3) < 112;
+    if (v2) hipLaunchKernelGGL(k_bwd_bf2, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
     else hipLaunchKernelGGL(k_bwd_bf, dim3(blocks), dim3(BB_THREADS), BB_LDS, s, a);
     return hipGetLastError();
 }

@@ -128,10 +128,25 @@ struct ReduceJob {
 hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s);
 hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_waves, int C, float* lik,
                                  float* gp, int64_t gp_cs, double count, int loss, float tau_out, hipStream_t s);
+// Leapfrog update fused into the gradient gather (vihmc_trajectory on DeepONet plans), hamiltorch's order with
+// every product and sum rounded separately: p += eps g; then on the last step p -= (eps / 2) g, otherwise
+// theta += eps p (eps inv_mass p with a diagonal mass). p and theta are updated in place (theta is the
+// evaluation's own input, read by the same thread first).
+struct LeapArgs {
+    float* p;               // [C, K]
+    float* th;              // [C, K]
+    const float* eps;       // [C]
+    const float* inv_mass;  // [K] or null
+    int32_t last;
+};
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
                                const float* prior_mu, const float* prior_inv_var, double prior_const,
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
-                               double* lp_part, hipStream_t s);
+                               double* lp_part, hipStream_t s, const LeapArgs* leap = nullptr);
+// the opening half step and first position step of a trajectory: p_out = p_in + (eps / 2) g_in,
+// th_out = th_in + eps p_out (eps inv_mass p_out)
+hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out, const float* g_in,
+                            const float* eps, const float* inv_mass, int K, int C, hipStream_t s);
 
 // Fused hidden-layer forward (width 100 -> 100 layers of both nets, one launch): every wave keeps 16 rows
 // of activations in registers through all fused layers; per layer the weights + bias of the next layer

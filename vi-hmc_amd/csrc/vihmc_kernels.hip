@@ -168,10 +168,11 @@ __global__ __launch_bounds__(256) void k_contract_stats(const double* stats, int
 constexpr int GATHER_SPLIT = GATHER_SPLIT_N;
 static_assert(GATHER_SPLIT <= GATHER_SPLIT_MAX, "lp_part slots");
 
+template <bool LEAP>
 __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap,
                                                       const float* theta, int K, const float* prior_mu,
                                                       const float* prior_inv_var, float prior_scale,
-                                                      float* grad, double* lp_part) {
+                                                      float* grad, double* lp_part, LeapArgs lf) {
     __shared__ double sh[8];
     const int c = blockIdx.y;
     const int per = (K + gridDim.x - 1) / gridDim.x;
@@ -179,14 +180,42 @@ __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t g
     const float inv_scale = 1.f / prior_scale;
     double lp = 0.0;
     for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
-        const float th = theta[(int64_t)c * K + k];
+        const int64_t o = (int64_t)c * K + k;
+        const float th = theta[o];
         const float d = th - prior_mu[k];
         const float iv = prior_inv_var[k];
         lp += -0.5 * (double)d * (double)d * (double)iv;
-        if (grad) grad[(int64_t)c * K + k] = gp[c * gp_cs + smap[k]] - d * iv * inv_scale;
+        const float g = gp[c * gp_cs + smap[k]] - d * iv * inv_scale;
+        if (grad) grad[o] = g;
+        if (LEAP) {
+#pragma clang fp contract(off)
+            const float e = lf.eps[c];
+            float pn = lf.p[o] + e * g;
+            if (lf.last) {
+                pn = pn - (0.5f * e) * g;
+            } else {
+                const float step = lf.inv_mass ? (e * lf.inv_mass[k]) * pn : e * pn;
+                lf.th[o] = th + step;
+            }
+            lf.p[o] = pn;
+        }
     }
     lp = block_sum_256(lp, sh);
     if (threadIdx.x == 0) lp_part[c * gridDim.x + blockIdx.x] = lp;
+}
+
+__global__ __launch_bounds__(256) void k_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out,
+                                                   const float* g_in, const float* eps, const float* inv_mass, int K) {
+#pragma clang fp contract(off)
+    const int c = blockIdx.y;
+    const float e = eps[c], he = 0.5f * e;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
+        const int64_t o = (int64_t)c * K + k;
+        const float pn = p_in[o] + he * g_in[o];
+        const float step = inv_mass ? (e * inv_mass[k]) * pn : e * pn;
+        p_out[o] = pn;
+        th_out[o] = th_in[o] + step;
+    }
 }
 
 // One wave per chain: lane i holds partial i (nparts <= 64), summed by a fixed xor butterfly (deterministic).
@@ -426,14 +455,24 @@ hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_wa
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
                                const float* prior_mu, const float* prior_inv_var, double prior_const,
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
-                               double* lp_part, hipStream_t s) {
-    hipLaunchKernelGGL(k_gather_prior, dim3(GATHER_SPLIT, C), dim3(256), 0, s, gp, gp_cs, smap, theta, K, prior_mu,
-                       prior_inv_var, prior_scale, grad, lp_part);
+                               double* lp_part, hipStream_t s, const LeapArgs* leap) {
+    if (leap)
+        hipLaunchKernelGGL(k_gather_prior<true>, dim3(GATHER_SPLIT, C), dim3(256), 0, s, gp, gp_cs, smap, theta, K,
+                           prior_mu, prior_inv_var, prior_scale, grad, lp_part, *leap);
+    else
+        hipLaunchKernelGGL(k_gather_prior<false>, dim3(GATHER_SPLIT, C), dim3(256), 0, s, gp, gp_cs, smap, theta, K,
+                           prior_mu, prior_inv_var, prior_scale, grad, lp_part, LeapArgs{});
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     static_assert(GATHER_SPLIT <= 64, "one lane per partial");
     VIHMC_LAUNCH(k_logp_finalize, dim3(C), dim3(64), 0, s, lp_part, GATHER_SPLIT, lik, prior_const, prior_scale,
                  logp);
+}
+
+hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out, const float* g_in,
+                            const float* eps, const float* inv_mass, int K, int C, hipStream_t s) {
+    VIHMC_LAUNCH(k_leap_open, dim3((K + 1023) / 1024, C), dim3(256), 0, s, th_in, th_out, p_in, p_out, g_in, eps,
+                 inv_mass, K);
 }
 
 size_t mlp_lds_bytes(int D, int n_layers, int maxw) {

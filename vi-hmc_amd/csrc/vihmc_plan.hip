@@ -678,19 +678,20 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
 }
 
 int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
-                       hipStream_t s);
+                       hipStream_t s, const LeapArgs* leap);
 
-int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out, hipStream_t s) {
+int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out, hipStream_t s,
+                  const LeapArgs* leap = nullptr) {
     if (C < 1 || C > p->maxC) return fail("C must be in [1, max_chains]");
     hipEvent_t stop = nullptr;
     if (int rc = p->timing_begin(VIHMC_T_EVAL, s, &stop)) return rc;
-    if (int rc = deeponet_eval_body(p, theta, C, logp, grad, out, s)) return rc;
+    if (int rc = deeponet_eval_body(p, theta, C, logp, grad, out, s, leap)) return rc;
     if (stop) HIPCHK(hipEventRecord(stop, s));
     return 0;
 }
 
 int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
-                       hipStream_t s) {
+                       hipStream_t s, const LeapArgs* leap) {
     HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s));
     if (int rc = deeponet_forward_layers(p, C, s)) return rc;
     const bool want_grad = grad != nullptr && out == nullptr;
@@ -804,7 +805,8 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         HIPCHK(launch_reduce(p->jobsW, p->n_jobsW, p->max_lenW, C, s));
     }
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
-                               p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, s));
+                               p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, s,
+                               want_grad ? leap : nullptr));
     return 0;
 }
 
@@ -1016,6 +1018,31 @@ int vihmc_mlp_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out,
         if (int rc = p->timing_begin(VIHMC_T_MLP, s, &stop, L)) return rc;
         HIPCHK(launch_mlp_traj(p->mlp, t, C, p->maxw, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
+        return 0;
+    });
+}
+
+int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, const float* p_in, float* p_out,
+                     const float* g_in, float* g_out, float* logp_out, const float* eps, const float* inv_mass, int L,
+                     int C, void* stream) {
+    if (p && p->kind == 1)
+        return vihmc_mlp_trajectory(p, theta_in, theta_out, p_in, p_out, g_in, g_out, logp_out, eps, inv_mass, L, C,
+                                    stream);
+    return guarded([&]() -> int {
+        if (!p || !theta_in || !theta_out || !p_in || !p_out || !g_in || !g_out || !logp_out || !eps)
+            return fail("null argument");
+        if (C < 1 || C > p->maxC) return fail("C must be in [1, max_chains]");
+        if (L < 1) return fail("L must be >= 1");
+        if (theta_in == theta_out) return fail("theta_out must not alias theta_in (the sampler reverts to it)");
+        if (p_in == p_out) return fail("p_out must not alias p_in");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        // opening half step + first position step, then L evaluations whose gradient gather applies the
+        // momentum step and the next position step in place (theta_out / p_out are the running state)
+        HIPCHK(launch_leap_open(theta_in, theta_out, p_in, p_out, g_in, eps, inv_mass, p->K, C, s));
+        for (int st = 0; st < L; ++st) {
+            LeapArgs lf{p_out, theta_out, eps, inv_mass, st == L - 1 ? 1 : 0};
+            if (int rc = deeponet_eval(p, theta_out, C, logp_out, g_out, nullptr, s, &lf)) return rc;
+        }
         return 0;
     });
 }

@@ -54,6 +54,8 @@ SIGNATURES = {
     "vihmc_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_mlp_trajectory": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "vihmc_trajectory": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "vihmc_sensitivity": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_plan_set_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "vihmc_plan_kind": (c_int, [c_void_p]),

@@ -116,6 +116,32 @@ class _Engine:
         _lib.check(rc, "vihmc_forward")
         return logp, out
 
+    def trajectory(self, theta: torch.Tensor, momentum: torch.Tensor, grad: torch.Tensor, eps, L: int,
+                   inv_mass: Optional[torch.Tensor] = None):
+        """One whole leapfrog trajectory of every chain (vihmc_trajectory: one launch for BNN plans; for DeepONet
+        plans L evaluations with the momentum / position steps fused into their gradient gather): from theta
+        [C, K], the fresh momentum and the gradient at theta, L steps of size eps (python float or per-chain [C])
+        -> (theta_L, p_L, logp_L, grad_L), bitwise the step-by-step path."""
+        th = self._theta(theta)
+        C = th.shape[0]
+        p = momentum.to(self.device, torch.float32).contiguous()
+        g = grad.to(self.device, torch.float32).contiguous()
+        if p.shape != th.shape or g.shape != th.shape:
+            raise ValueError("momentum and grad must match theta [C, K]")
+        e = (torch.full((C,), float(eps), dtype=torch.float32, device=self.device) if not torch.is_tensor(eps)
+             else eps.to(self.device, torch.float32).reshape(-1).expand(C).contiguous())
+        im = None if inv_mass is None else inv_mass.to(self.device, torch.float32).reshape(-1).contiguous()
+        if im is not None and im.numel() != self.K:
+            raise ValueError(f"inv_mass must be [{self.K}]")
+        th_out, p_out, g_out = torch.empty_like(th), torch.empty_like(th), torch.empty_like(th)
+        lp = torch.empty(C, device=self.device, dtype=torch.float32)
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_trajectory(self._plan, th.data_ptr(), th_out.data_ptr(), p.data_ptr(), p_out.data_ptr(),
+                                         g.data_ptr(), g_out.data_ptr(), lp.data_ptr(), e.data_ptr(),
+                                         None if im is None else im.data_ptr(), int(L), C, self._stream())
+        _lib.check(rc, "vihmc_trajectory")
+        return th_out, p_out, lp, g_out
+
     def set_data(self, x_branch: torch.Tensor, y: torch.Tensor):
         """vihmc_plan_set_data (DeepONet): new branch rows [N, in_branch] and targets [N, P], same N / P."""
         xb = torch.as_tensor(x_branch).to(device=self.device, dtype=torch.float32).contiguous()
@@ -263,32 +289,6 @@ class MLPEngine(_Engine):
                                               _lib.fptr(fz), _lib.iptr(idx), _lib.fptr(pm), _lib.fptr(ps),
                                               self.device.index)
         self._created(rc, "vihmc_mlp_plan_create")
-
-
-    def trajectory(self, theta: torch.Tensor, momentum: torch.Tensor, grad: torch.Tensor, eps, L: int,
-                   inv_mass: Optional[torch.Tensor] = None):
-        """One whole leapfrog trajectory of every chain in one launch (vihmc_mlp_trajectory): from theta [C, K],
-        the fresh momentum and the gradient at theta, L steps of size eps (python float or per-chain [C]) ->
-        (theta_L, p_L, logp_L, grad_L), bitwise the step-by-step path."""
-        th = self._theta(theta)
-        C = th.shape[0]
-        p = momentum.to(self.device, torch.float32).contiguous()
-        g = grad.to(self.device, torch.float32).contiguous()
-        if p.shape != th.shape or g.shape != th.shape:
-            raise ValueError("momentum and grad must match theta [C, K]")
-        e = (torch.full((C,), float(eps), dtype=torch.float32, device=self.device) if not torch.is_tensor(eps)
-             else eps.to(self.device, torch.float32).reshape(-1).expand(C).contiguous())
-        im = None if inv_mass is None else inv_mass.to(self.device, torch.float32).reshape(-1).contiguous()
-        if im is not None and im.numel() != self.K:
-            raise ValueError(f"inv_mass must be [{self.K}]")
-        th_out, p_out, g_out = torch.empty_like(th), torch.empty_like(th), torch.empty_like(th)
-        lp = torch.empty(C, device=self.device, dtype=torch.float32)
-        with torch.cuda.device(self.device):
-            rc = self.L.vihmc_mlp_trajectory(self._plan, th.data_ptr(), th_out.data_ptr(), p.data_ptr(), p_out.data_ptr(),
-                                             g.data_ptr(), g_out.data_ptr(), lp.data_ptr(), e.data_ptr(),
-                                             None if im is None else im.data_ptr(), int(L), C, self._stream())
-        _lib.check(rc, "vihmc_mlp_trajectory")
-        return th_out, p_out, lp, g_out
 
 
 def trunk_features(trunk_in) -> np.ndarray:

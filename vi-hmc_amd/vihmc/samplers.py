@@ -74,7 +74,8 @@ class EngineEvaluator:
 
     @property
     def fused_trajectory(self) -> bool:
-        """BNN engines run a whole leapfrog trajectory in one launch (MLPEngine.trajectory)."""
+        """Engines run a whole leapfrog trajectory per call (_Engine.trajectory / vihmc_trajectory: one launch for
+        BNN plans, the updates fused into the gradient gather for DeepONet plans); False = step-by-step path."""
         return hasattr(self.engine, "trajectory") and getattr(self.engine, "fused_trajectory", True)
 
     def trajectory(self, theta, p, g, eps, L, inv_mass=None):
