@@ -102,7 +102,7 @@ def cpu_throughput(procs, seconds, L, step_size):
 # ------------------------------------------------------------------------------------------------
 KCLASS = {0: ("contract_a", "k_contract_bf", "side-A contraction: S = Z_b Z_t^T + b, Gaussian NLL, G, dZ_trunk"),
           1: ("contract_b", "k_contract_bf_b", "side-B contraction: dZ_branch = G Z_trunk"),
-          2: ("bwd", "k_bwd_bf", "layer backward (dX and dW of both MLPs), one launch per layer"),
+          2: ("bwd", "k_bwd_bf2", "layer backward (dX and dW of both MLPs), one launch per layer"),
           3: ("fwd", "k_fwd_fused_bf", "fused hidden-layer forward of both MLPs (layers 1..8)")}
 T_EVAL = 4
 CAL_STEPS = 2          # untimed HMC iterations with every kernel class under HIP events
@@ -243,18 +243,20 @@ def leg_bnn(dev, C, steps=10, L=196, eps=5e-4):
     dt = _timed_steps(r, 2, steps)
     ms, n = eng.timing_class(eng.T_MLP)
     eng.timing(-1, False)
-    avg = ms / max(n, 1)
-    # algorithmic bytes per launch: theta in + grad out per chain, x / y / frozen weights / index map once
-    byts = C * 2 * 4 * K + 2 * 4 * x.size + 4 * D + 4 * K
+    avg = ms / max(n, 1)                                   # in-kernel ms per leapfrog step (L counted per launch)
+    # one k_mlp_traj launch per HMC iteration runs the whole trajectory; algorithmic bytes per launch: theta, p,
+    # g in and out per chain, x / y / frozen weights / index map once
+    byts = C * 6 * 4 * K + 2 * 4 * x.size + 4 * D + 4 * K
     lf = C * L * steps / dt
     eng.close()
     return {"workload": f"BNN VI-HMC (configs 2-3), {C} chain(s) per GPU, L = {L}", "chains": C,
             "leapfrog_steps_per_s": lf, "us_per_leapfrog_step": 1e6 * dt / (L * steps),
-            "kernel_avg_us": avg * 1e3, "kernel_share_of_wall": ms / 1e3 / dt,
+            "kernel_us_per_leapfrog_step": avg * 1e3,
+            "kernel_share_of_wall": avg * L * steps / 1e3 / dt,
             "algorithmic_bytes_per_launch": byts,
-            "hbm_frac": byts / (avg / 1e3) / 1e9 / HBM_PEAK_GBS,
-            "note": "latency-bound: one k_mlp launch per leapfrog step (one wave per chain) plus the torch "
-                    "elementwise updates; the HBM fraction is from algorithmic bytes"}
+            "hbm_frac": byts / (avg * L / 1e3) / 1e9 / HBM_PEAK_GBS,
+            "note": "latency-bound: one k_mlp_traj launch per HMC iteration (one wave per chain, the whole "
+                    "leapfrog trajectory in LDS); the HBM fraction is from algorithmic bytes"}
 
 
 def ess_phase(args, ev, runner, K, dev, chains, world):

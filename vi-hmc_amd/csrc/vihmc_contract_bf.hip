@@ -149,23 +149,6 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
             reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
             (__attribute__((address_space(3))) void*)(smc + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
 #endif
-    // DMA pieces per D wave and chunk: k = d, d + 8, d + 16 < 22 (scalar: the counted waits are immediates)
-    const int dpieces = __builtin_amdgcn_readfirstlane(wave - 8) < CB_GLDS - 16 ? 3 : 2;
-    if (wave >= 8 && nchunks > 0) {
-        VIHMC_CB_GLDS(0, 0)
-        if (CBA_PIPE) {
-            if (nchunks > 1) {
-                VIHMC_CB_GLDS(1, 1)
-                if (dpieces == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");   // chunk 0 landed
-                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            } else {
-                bf6::wait_vmcnt0();
-            }
-        } else if (CBA_ASM_DMA) {
-            bf6::wait_vmcnt0();                      // chunk 0 published by the first barrier
-        }
-    }
-
     if (wave < 8) {
         // ---------------- S role ----------------
         if (CBA_PRIO == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) < 512) __builtin_amdgcn_s_setprio(1);
@@ -216,11 +199,13 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                 YN[sub][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(              \
                     yrs, yoff, (uint32_t)(q_lo + (CI) * CB_QC + 16 * sub + r) * ystep, 0));
         VIHMC_CB_YLOAD(ya, 0)
+        // chunk i < nchunks, called with no condition around its loads or stores (below): hipcc's wait counts
+        // stay exact (a conditional chunk body or a store count that depends on the path made it wait vmcnt(0)
+        // -- for this wave's own G^T stores -- at the head of every other chunk)
         auto s_chunk = [&](int i, float (&yv)[2][4], float (&yn)[2][4]) __attribute__((always_inline)) {
-            if (i > nchunks) return;                // same barrier count as the D role
             VIHMC_CB_BAR()
             VIHMC_CB_STAMP(i, 0)
-            if (i < nchunks) {
+            {
                 const int q0 = q_lo + i * CB_QC;
                 const bool full = q0 + CB_QC <= q_hi;
                 const unsigned char* img = smc + (i % CB_NQBUF) * CB_QIMG;
@@ -287,22 +272,11 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                     const f32x4 X = lo ? gs[0] : recv;
                     const f32x4 Y = lo ? recv : gs[1];
                     const uint32_t cofs = (uint32_t)i * (uint32_t)P.ldg * (CB_QC * 4u);
-                    if (full) {
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, X), grs, gx_off + cofs, 0, 0);
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, Y), grs, gy_off + cofs, 0, 0);
-                    } else {
-                        const int qq = q0 + (lo ? 0 : 16) + 4 * lg;
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            // copy the element out first: __builtin_bit_cast of an ext-vector element
-                            // subscript compiled to element 0 for every r (hipcc, ROCm 7.2)
-                            const float xv = X[r], yv2 = Y[r];
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xv), grs,
-                                qq + r < q_hi ? gx_off + cofs + 4u * r : OOB_C, 0, 0);
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(yv2), grs,
-                                qq + r < q_hi ? gy_off + cofs + 4u * r : OOB_C, 0, 0);
-                        }
-                    }
+                    // whole lines in a partial chunk too: its q >= q_hi elements are G = 0 (rv zeroed above)
+                    // and land in the padding of the chunk-blocked layout (q_hi < Mq only at chunk boundaries,
+                    // qperA being a multiple of 32), which no workgroup owns
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, X), grs, gx_off + cofs, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, Y), grs, gy_off + cofs, 0, 0);
                 }
                 // sum r^2 (no cancellation): per-chunk fp32 partial of 8 terms per lane, then fp64
                 ssq += (double)ps;
@@ -312,10 +286,13 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
 #endif
             }
         };
-        for (int i = 0; i <= nchunks; i += 2) {
+        int i = 0;
+        for (; i + 1 < nchunks; i += 2) {
             s_chunk(i, ya, yb);
             s_chunk(i + 1, yb, ya);
         }
+        if (i < nchunks) s_chunk(i, ya, yb);
+        VIHMC_CB_BAR()                                 // the D role's last barrier (it runs one chunk behind)
         if (P.with_stats) {
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
@@ -332,6 +309,25 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
     }
 
     // ---------------- D role ----------------
+    // The chunk-0 DMA is issued here, on the D waves' own path: issued before the role split, hipcc's wait
+    // analysis (one per kernel, not per role) carried a pending LDS-DMA into the S role's loop head and waited
+    // vmcnt -- i.e. for the S waves' own G^T stores and target loads -- before their LDS reads of every chunk.
+    // DMA pieces per D wave and chunk: k = d, d + 8, d + 16 < 22 (scalar: the counted waits are immediates)
+    const int dpieces = __builtin_amdgcn_readfirstlane(wave - 8) < CB_GLDS - 16 ? 3 : 2;
+    if (nchunks > 0) {
+        VIHMC_CB_GLDS(0, 0)
+        if (CBA_PIPE) {
+            if (nchunks > 1) {
+                VIHMC_CB_GLDS(1, 1)
+                if (dpieces == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");   // chunk 0 landed
+                else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            } else {
+                bf6::wait_vmcnt0();
+            }
+        } else if (CBA_ASM_DMA) {
+            bf6::wait_vmcnt0();                      // chunk 0 published by the first barrier
+        }
+    }
     if (CBA_PRIO == 1 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 512) __builtin_amdgcn_s_setprio(1);
     f32x4 dacc[7];
 #pragma unroll

@@ -375,6 +375,14 @@ __device__ __forceinline__ void bf_split_operand(const float4 (&h)[7], bf16x8 (&
 #define FWD_TF_SCHED 0     // 1: sched_barrier between tile pairs (fewer spills, 257-262 vs 256 us: not kept)
 #endif
 constexpr int FWD_WTAIL = 3 * BPLANE * 2 + 112 * 4;   // byte offset of the fp32 W tail [100][4] in an image
+constexpr int QI_PITCH = 224;                           // contraction block image (vihmc_contract_bf.hip): plane
+constexpr int QI_PLANE = CONTRACT_SPLIT_ROWS * QI_PITCH;  // rows of 112 bf16, 3 planes, then the fp32 tail [32][4]
+static_assert(3 * QI_PLANE + CONTRACT_SPLIT_ROWS * 16 <= CONTRACT_SPLIT_BLOCK, "block image");
+constexpr int QI_HALF = 16 * QI_PITCH;                  // a wave's 16 rows of one plane (3584 B)
+constexpr int QI_WAVE = 3 * QI_HALF + 16 * 16;          // + its tail rows: 11008 B of LDS per wave
+#ifndef FWD_IMG_LDS
+#define FWD_IMG_LDS 1   // 0: the image written straight from registers (8-B stores per lane and tile)
+#endif
 
 __device__ __forceinline__ int tf_row(int t, int lr) { return t < 6 ? 16 * t + lr : 96 + (lr >> 2); }
 
@@ -556,6 +564,92 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         if (!dma) {
             VIHMC_FB_STORE((j + 1) & 1)
         }
+    }
+    // the output layer's rows as the contraction's pre-split image (bit-identical to k_split_blocks on the fp32
+    // rows just stored: same conversions), which saves that kernel's re-read of the outputs and its launch
+    if (N.qimg != nullptr) {
+        auto split_tile = [&](int t, bf16x4& a, bf16x4& b, bf16x4& cc) __attribute__((always_inline)) {
+            const float v[4] = {h[t].x, h[t].y, h[t].z, h[t].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                __bf16 x0, x1, x2;
+                split3(v[e], x0, x1, x2);
+                a[e] = x0;
+                b[e] = x1;
+                cc[e] = x2;
+            }
+        };
+        __bf16 y0, y1, y2;
+        split3(h[6].x, y0, y1, y2);                       // column 96 + lg: its planes and the fp32 tail
+        unsigned char* blk = N.qimg + c * N.qimg_cs + (int64_t)(min(row, N.rows - 1) / CONTRACT_SPLIT_ROWS) *
+                                                          CONTRACT_SPLIT_BLOCK;
+#if FWD_IMG_LDS
+        // through LDS (the weight buffers are free after the last layer): each wave lays its 16 rows out as in
+        // the image -- three 16-row plane slices and the tail slice, 11,008 B -- then copies them out in whole
+        // 1-KB wave stores (direct 8-B stores per lane and tile measured slower)
+        __syncthreads();
+        unsigned char* reg = fsmb + wave * QI_WAVE;
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            bf16x4 a, b, cc;
+            split_tile(t, a, b, cc);
+            unsigned char* o = reg + lr * QI_PITCH + 2 * (16 * t + 4 * lg);
+            *reinterpret_cast<bf16x4*>(o) = a;
+            *reinterpret_cast<bf16x4*>(o + QI_HALF) = b;
+            *reinterpret_cast<bf16x4*>(o + 2 * QI_HALF) = cc;
+        }
+        {
+            unsigned char* o = reg + lr * QI_PITCH + 2 * (96 + lg);
+            *reinterpret_cast<__bf16*>(o) = y0;
+            *reinterpret_cast<__bf16*>(o + QI_HALF) = y1;
+            *reinterpret_cast<__bf16*>(o + 2 * QI_HALF) = y2;
+            if (lg < 3) {                                  // zero columns 100..111 of plane lg (8-B aligned)
+                uint64_t* z = reinterpret_cast<uint64_t*>(reg + lg * QI_HALF + lr * QI_PITCH + 200);
+                z[0] = 0;
+                z[1] = 0;
+                z[2] = 0;
+            }
+            reinterpret_cast<float*>(reg + 3 * QI_HALF + lr * 16)[lg] = h[6].x;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);               // lgkmcnt(0): this wave's LDS writes done
+        __builtin_amdgcn_wave_barrier();
+        const int row0 = row - lr;                         // the wave's first row (16-row aligned)
+        const int hb = (row0 % CONTRACT_SPLIT_ROWS) / 16;  // which half of the 32-row block
+#pragma unroll
+        for (int k = 0; k < (QI_WAVE / 16 + 63) / 64; ++k) {
+            const int i = k * 64 + lane;                   // 16-B piece of the wave's region
+            if (i >= QI_WAVE / 16) break;
+            int r, off;
+            if (i < 3 * QI_HALF / 16) {
+                const int pl = i / (QI_HALF / 16), w16 = i % (QI_HALF / 16);
+                r = w16 / (QI_PITCH / 16);
+                off = pl * QI_PLANE + hb * QI_HALF + w16 * 16;
+            } else {
+                r = i - 3 * QI_HALF / 16;
+                off = 3 * QI_PLANE + (hb * 16 + r) * 16;
+            }
+            if (row0 + r < N.rows)
+                *reinterpret_cast<u32x4*>(blk + off) = *reinterpret_cast<const u32x4*>(reg + i * 16);
+        }
+#else
+        if (rok) {
+            unsigned char* rp = blk + (row % CONTRACT_SPLIT_ROWS) * QI_PITCH;
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                bf16x4 a, b, cc;
+                split_tile(t, a, b, cc);
+                unsigned char* o = rp + 2 * (16 * t + 4 * lg);
+                *reinterpret_cast<bf16x4*>(o) = a;
+                *reinterpret_cast<bf16x4*>(o + QI_PLANE) = b;
+                *reinterpret_cast<bf16x4*>(o + 2 * QI_PLANE) = cc;
+            }
+            unsigned char* o = rp + 2 * (96 + lg);
+            *reinterpret_cast<__bf16*>(o) = y0;
+            *reinterpret_cast<__bf16*>(o + QI_PLANE) = y1;
+            *reinterpret_cast<__bf16*>(o + 2 * QI_PLANE) = y2;
+            reinterpret_cast<float*>(blk + 3 * QI_PLANE + (row % CONTRACT_SPLIT_ROWS) * 16)[lg] = h[6].x;
+        }
+#endif
     }
 #undef VIHMC_FB_LOAD
 #undef VIHMC_FB_STORE

@@ -162,6 +162,9 @@ struct FusedNet {
     int32_t nl, rows, nblk;                         // nblk = ceil(rows / (16 * waves per workgroup))
     const unsigned char* wimg; int64_t wimg_cs;     // bf16x6: pre-split [W_j | bias] LDS images of layers
                                                     // 1..nl, FWD_WIMG bytes each (k_split_wimg), or null
+    unsigned char* qimg; int64_t qimg_cs;           // or null: the last layer's output also written as the
+                                                    // contraction's pre-split block image (k_split_blocks'
+                                                    // layout; padding pre-zeroed by the plan)
 };
 struct FusedArgs {
     FusedNet net[2];

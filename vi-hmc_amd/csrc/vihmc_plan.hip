@@ -97,6 +97,7 @@ struct vihmc_plan {
     int64_t qsplitA_cs = 0;             // bytes per chain
     unsigned char* qsplitB = nullptr;   // per chain: trunk outputs pre-split for k_contract_bf_b
     int64_t qsplitB_cs = 0;
+    bool img_by_fwd = false;            // this evaluation's fused forward wrote qsplitA / qsplitB
     float* partB = nullptr;
     int64_t partB_cs = 0;
     int qchunksB = 1, qperB = 32;
@@ -525,7 +526,16 @@ bool fused_forward_ok(const vihmc_plan* p) {
     return true;
 }
 
-int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s) {
+// VIHMC_FWD_IMG=0: the contraction images come from k_split_blocks instead of the forward (A/B timing)
+bool fwd_writes_img() {
+    static const bool on = [] {
+        const char* e = std::getenv("VIHMC_FWD_IMG");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
     FusedArgs a{};
     a.C = C;
     a.packed = p->packed;
@@ -556,6 +566,14 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s) {
     }
     if (p->fwd_bf16x6 && nw == 12 && (!fwd_fused_bf_needs_wimg() || (p->fwd_wimg && p->wimg))) {
         for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * fwd_fused_bf_waves());
+        if (img && fwd_writes_img()) {
+            // the contraction's pre-split images of the branch (side A) and trunk (side B) outputs
+            a.net[0].qimg = p->qsplitA;
+            a.net[0].qimg_cs = p->qsplitA_cs;
+            a.net[1].qimg = p->qsplitB;
+            a.net[1].qimg_cs = p->qsplitB_cs;
+            p->img_by_fwd = true;
+        }
         if (p->fwd_wimg && p->wimg) {
             // pre-split weight images, DMA-staged by the forward (FWD_WIMG bytes per fused layer)
             a.net[0].wimg = p->wimg;
@@ -573,14 +591,14 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s) {
 
 // Forward through both MLPs (grouped launches: branch + trunk layer j together); the hidden 100 -> 100
 // stack goes through the fused kernel when its shape allows.
-int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s) {
+int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img) {
     const int maxl = (int)std::max(p->nets[0].L.size(), p->nets[1].L.size());
     const bool fused = fused_forward_ok(p);
     for (int j = 0; j < maxl; ++j) {
         if (j == 1 && fused) {
             hipEvent_t stop = nullptr;
             if (int rc = p->timing_begin(VIHMC_T_FWD, s, &stop)) return rc;
-            if (int rc = launch_forward_fused(p, C, s)) return rc;
+            if (int rc = launch_forward_fused(p, C, s, img)) return rc;
             if (stop) HIPCHK(hipEventRecord(stop, s));
             return 0;
         }
@@ -693,13 +711,16 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
 int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
                        hipStream_t s, const LeapArgs* leap) {
     HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s));
-    if (int rc = deeponet_forward_layers(p, C, s)) return rc;
     const bool want_grad = grad != nullptr && out == nullptr;
+    // the pre-split contraction images (bf16x6 sides, gradient evaluations) are written by the fused forward
+    // when it runs; otherwise k_split_blocks makes them below
+    p->img_by_fwd = false;
+    if (int rc = deeponet_forward_layers(p, C, s, want_grad && p->contract_bf16x6 && p->W == 100)) return rc;
     int stats_waves = 0;
     {
         ContractProb a = side_a(p, C, want_grad, out);
         stats_waves = p->qchunksA * cdiv(p->P, CONTRACT_OWN_PER_WG) * (a.bf16x6 ? 8 : 4);
-        if (a.bf16x6)
+        if (a.bf16x6 && !p->img_by_fwd)
             HIPCHK(launch_split_blocks(a.Q, a.q_cs, a.ldq, p->N, p->qsplitA, p->qsplitA_cs, C, s));
         hipEvent_t stop = nullptr;
         if (int rc = p->timing_begin(VIHMC_T_CONTRACT_A, s, &stop)) return rc;
@@ -743,7 +764,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         q.with_stats = 0;
         const float v = std::max(p->lik.tau_out, 1e-6f);
         q.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
-        if (q.bf16x6)
+        if (q.bf16x6 && !p->img_by_fwd)
             HIPCHK(launch_split_blocks(q.Q, q.q_cs, q.ldq, p->P, p->qsplitB, p->qsplitB_cs, C, s));
         hipEvent_t stop = nullptr;
         if (int rc = p->timing_begin(VIHMC_T_CONTRACT_B, s, &stop)) return rc;
@@ -1156,7 +1177,7 @@ int deeponet_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, 
     a.ldw = ld_residue(128, 4);       // W image [128][132]: b32 reads of rows 4 apart hit distinct bank groups
     a.count = (float)((double)N * npts);
     e = launch_scatter(p->packed, p->dp, 1, theta, p->K, p->smap_w, p->smap_wt, s);
-    int rc = e == hipSuccess ? deeponet_forward_layers(p, 1, s) : 0;
+    int rc = e == hipSuccess ? deeponet_forward_layers(p, 1, s, false) : 0;
     SensArgs* dev_a = nullptr;
     if (e == hipSuccess && rc == 0) e = talloc((void**)&dev_a, sizeof(SensArgs));
     if (e == hipSuccess && rc == 0) e = hipMemcpyAsync(dev_a, &a, sizeof(SensArgs), hipMemcpyHostToDevice, s);
