@@ -17,6 +17,7 @@
 // Blocks are chain-fastest (c = blockIdx % C) so, with C a multiple of 8, all blocks of one chain run on
 // one XCD and share its L2 copy of that chain's weights.
 #include "vihmc_internal.h"
+#include "vihmc_bf16x6.h"
 
 namespace vihmc {
 
@@ -308,13 +309,16 @@ __device__ __forceinline__ float4 bf_epi(const float* bias, int t, int lg, const
     h.y = n + 1 < FW ? act_t<ACT>(acc[1] + bv.y) : 0.f;
     h.z = n + 2 < FW ? act_t<ACT>(acc[2] + bv.z) : 0.f;
     h.w = n + 3 < FW ? act_t<ACT>(acc[3] + bv.w) : 0.f;
-    const uint32_t off = (t < 6 || lg == 0) ? ooff + 4u * n : OOB;
+    // one per-lane offset (row + 16 lg bytes) for every tile, the tile's 64 t bytes as the scalar offset: with
+    // per-tile lane offsets hipcc hoisted seven of them out of the layer loop and spilled them at 168 VGPRs, and
+    // each reload's vmcnt(0) then also waited for this wave's earlier h stores (OOB + 64 t stays out of range)
+    const uint32_t off = (t < 6 || lg == 0) ? ooff + 16u * lg : OOB;
 #if FWD_ABL == 1
     asm volatile("" :: "v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w));
     (void)off;
     (void)orsrc;
 #else
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), orsrc, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), orsrc, off, 64 * t, 0);
 #endif
     return h;
 }
@@ -429,7 +433,7 @@ __device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, co
 #if FWD_ABL == 1
     asm volatile("" :: "v"(v));
 #else
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, ooff == OOB ? OOB : ooff + 4u * (96 + lg), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, ooff + 4u * lg, 4 * 96, 0);
 #endif
     hn[6].x = v;
 }
@@ -505,11 +509,23 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
     // (global_load_lds, 1 KB per wave-instruction, no VGPRs / VALU); the barrier drains it (vmcnt(0))
     const bool dma = FWD_TAILF32 || FWD_DMA_ONLY || N.wimg != nullptr;  // FWD_TAILF32: images only (host-checked)
     const unsigned char* wimgc = dma ? N.wimg + c * N.wimg_cs : nullptr;
+#ifndef FWD_ASM_DMA
+#define FWD_ASM_DMA 1   // 1: the weight-image DMA from inline asm (hipcc does not track it): with the builtin, hipcc
+                        // waited vmcnt(0) -- this wave's h stores included -- before the bias reads of every tile
+                        // pair, not knowing the DMA target disjoint; the wave then waits for the DMA itself at the
+                        // end of the layer, before the barrier that publishes it
+#endif
+#if FWD_ASM_DMA
+#define VIHMC_FB_DMA(J, BUF)                                                                          \
+    for (int k = wave; k < FWD_WIMG / 1024; k += NW)                                                  \
+        bf6::glds16_asm(wimgc + (int64_t)(J) * FWD_WIMG + k * 1024 + lane * 16, fsmb + (BUF) * FWD_WIMG + k * 1024);
+#else
 #define VIHMC_FB_DMA(J, BUF)                                                                          \
     for (int k = wave; k < FWD_WIMG / 1024; k += NW)                                                  \
         __builtin_amdgcn_global_load_lds(                                                             \
             reinterpret_cast<const void*>(wimgc + (int64_t)(J) * FWD_WIMG + k * 1024 + lane * 16),   \
             (__attribute__((address_space(3))) void*)(fsmb + (BUF) * FWD_WIMG + k * 1024), 16, 0, 0);
+#endif
     if (dma) {
         VIHMC_FB_DMA(0, 0)
     } else {
@@ -564,6 +580,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         if (!dma) {
             VIHMC_FB_STORE((j + 1) & 1)
         }
+        if (FWD_ASM_DMA && dma) bf6::wait_vmcnt0();       // layer j+1's image landed before the next barrier
     }
     // the output layer's rows as the contraction's pre-split image (bit-identical to k_split_blocks on the fp32
     // rows just stored: same conversions), which saves that kernel's re-read of the outputs and its launch
