@@ -574,10 +574,39 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         const unsigned char* wrow1 = smw + BB_W + min(16 * (t0 + 1) + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
         const float* wtl = reinterpret_cast<const float*>(smw + BB_WT);
         const int wr0 = min(16 * t0 + lr, P.n_in - 1), wr1 = min(16 * (t0 + 1) + lr, P.n_in - 1);
-        auto dx_run = [&](auto two_c) __attribute__((always_inline)) {
+#ifndef B2_DEFER
+#define B2_DEFER 0      // 1: the dX epilogue of sub-tile i runs after sub-tile i+1's MFMAs are issued (branch-free, in
+                        // their basic block, so its VALU fills their issue gaps); 0: right after its own MFMAs
+#endif
+        // Dout through a buffer resource: rows past r1 (another workgroup's) and columns past NI4 get an out-of-range
+        // offset instead of a branch around the store
+        const __amdgpu_buffer_rsrc_t drs =
+            bf6::make_rsrc(P.Dout + c * P.o_cs, (uint32_t)((int64_t)P.M * P.ldh * 4));
+        auto dx_run = [&](auto two_c, auto tanh_c) __attribute__((always_inline)) {
             constexpr bool TWO = decltype(two_c)::value;
+            constexpr bool TANH = decltype(tanh_c)::value;
+            constexpr int NU = TWO ? 2 : 1;
             bf16x8 wra[3][3];
             float wta = 0.f, wtb = 0.f;
+            // the pending epilogue: accumulators, the H planes of its rows (read before the buffer is reused) and the
+            // store offsets (OOB: nothing pending / not this workgroup's row / past NI4)
+            f32x4 accp[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+            bf16x4 hq[2][3] = {};
+            uint32_t offp[2] = {bf6::OOB, bf6::OOB};
+            auto epilogue = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int u = 0; u < NU; ++u) {
+                    const int col = 16 * (t0 + u) + 4 * lg;
+                    f32x4 o;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float hv = ((float)hq[u][2][r] + (float)hq[u][1][r]) + (float)hq[u][0][r];
+                        const float gd = TANH ? 1.f - hv * hv : act_grad_bf(P.act, hv);
+                        o[r] = (col + r < P.n_in) ? accp[u][r] * gd : 0.f;
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bf6::u32x4, o), drs, offp[u], 0, 0);
+                }
+            };
             for (int i = 0; i < nsub; ++i) {
                 const int sub = r0 + i * BB_SUB;
                 __syncthreads();
@@ -614,39 +643,34 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                         acc[1] = six(wb, db[kb], acc[1]);
                     }
                 }
+                if (B2_DEFER) epilogue();                  // sub-tile i-1 (nothing stored when i = 0)
 #if BB_STAMP
                 asm volatile("" :: "v"(acc[0]), "v"(acc[1]));
                 VIHMC_BB_STAMP(i, 1)
 #endif
                 const int m = sub + 16 * h + lr;
                 const unsigned char* hrow = buf + BB_HP + (16 * h + lr) * BB_PITCH;
-                float* orow = P.Dout + c * P.o_cs + (int64_t)m * P.ldh;
-                auto epi = [&](auto tanh_c) __attribute__((always_inline)) {
-                    constexpr bool TANH = decltype(tanh_c)::value;
 #pragma unroll
-                    for (int u = 0; u < (TWO ? 2 : 1); ++u) {
-                        const int col = 16 * (t0 + u) + 4 * lg;
-                        if (m >= r1 || col >= NI4) continue;
-                        const bf16x4 h0 = *reinterpret_cast<const bf16x4*>(hrow + 2 * col);
-                        const bf16x4 h1 = *reinterpret_cast<const bf16x4*>(hrow + BB_PLANE + 2 * col);
-                        const bf16x4 h2 = *reinterpret_cast<const bf16x4*>(hrow + 2 * BB_PLANE + 2 * col);
-                        f32x4 o;
+                for (int u = 0; u < NU; ++u) {
+                    const int col = 16 * (t0 + u) + 4 * lg;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float hv = ((float)h2[r] + (float)h1[r]) + (float)h0[r];
-                            const float gd = TANH ? 1.f - hv * hv : act_grad_bf(P.act, hv);
-                            o[r] = (col + r < P.n_in) ? acc[u][r] * gd : 0.f;
-                        }
-                        *reinterpret_cast<f32x4*>(orow + col) = o;
-                    }
-                };
-                if (P.act == ACT_TANH) epi(std::true_type{});
-                else epi(std::false_type{});
+                    for (int p = 0; p < 3; ++p) hq[u][p] = *reinterpret_cast<const bf16x4*>(hrow + p * BB_PLANE + 2 * col);
+                    offp[u] = (m < r1 && col < NI4) ? (uint32_t)(m * P.ldh + col) * 4u : bf6::OOB;
+                    accp[u] = acc[u];
+                }
+                if (!B2_DEFER) epilogue();
                 VIHMC_BB_STAMP(i, 2)
             }
+            if (B2_DEFER && P.has_dx && nsub > 0) epilogue();
         };
-        if (t0 + 1 < 7) dx_run(std::true_type{});
-        else dx_run(std::false_type{});
+        const bool tanh_act = P.act == ACT_TANH;
+        if (t0 + 1 < 7) {
+            if (tanh_act) dx_run(std::true_type{}, std::true_type{});
+            else dx_run(std::true_type{}, std::false_type{});
+        } else {
+            if (tanh_act) dx_run(std::false_type{}, std::true_type{});
+            else dx_run(std::false_type{}, std::false_type{});
+        }
     } else {
         // ---------------- dW role: two row tiles per wave, the second over a column range ----------------
         // Waves w, w + 4, w + 8, w + 12 share a SIMD. The dX waves of SIMD groups 0 and 1 (waves 0/4, 1/5) carry
