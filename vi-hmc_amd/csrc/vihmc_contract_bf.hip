@@ -545,15 +545,16 @@ __global__ __launch_bounds__(CBB_THREADS, 1) void k_contract_bf_b(ContractProb P
         }                                                                                                   \
     }
 
-    // G two chunks ahead in three register sets (named, rotated by a 3x unrolled loop), the image one chunk
-    // ahead by asm DMA, and every wave drains its own loads (vmcnt(0)) at the end of each chunk: the counted
-    // wait hipcc puts before the split of G(i) (its 32 newer loads) then never waits on this chunk's loads
-    float gc_[CBB_NS][8];
+    // G one chunk ahead in two register sets (rotated by a 2x unrolled loop), the image one chunk ahead by asm
+    // LDS-DMA. Per chunk the DMA is issued before the G loads, so the chunk ends with a counted vmcnt(8 NS) -- the
+    // image (invisible to hipcc) landed, G(i+1) left in flight for the next chunk's split -- instead of vmcnt(0),
+    // which made every chunk wait out the HBM latency of the G loads it had just issued (the previous design
+    // loaded G two chunks ahead in three sets to survive that drain). The G loads are unconditional (clamped
+    // chunk index) and the loop runs whole pairs, so hipcc's own counted wait before the split of G(i) is exact.
     if (nchunks > 0) {
         VIHMC_CBB_GLDS(0, 0)
         VIHMC_CBB_GLOAD(ga_, 0)
-        if (nchunks > 1) VIHMC_CBB_GLOAD(gb_, 1)
-        if (CB_ASM_DMA) bf6::wait_vmcnt0();          // chunk 0 published by the first barrier
+        bf6::wait_vmcnt0();                          // chunk 0 published by the first barrier
     }
     f32x4 dacc[CBB_NS][7];
 #pragma unroll
@@ -562,13 +563,9 @@ __global__ __launch_bounds__(CBB_THREADS, 1) void k_contract_bf_b(ContractProb P
         for (int t = 0; t < 7; ++t) dacc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int tr_off = (4 * lg + (lr >> 2)) * CB_PITCH + 8 * (lr & 3);
     auto chunk = [&](int i, float (&gv)[CBB_NS][8], float (&gn)[CBB_NS][8]) __attribute__((always_inline)) {
-        if (i >= nchunks) return;
         __syncthreads();                      // chunk i landed; buffer (i+1)%3 free
-        if (i + 2 < nchunks) VIHMC_CBB_GLOAD(gn, i + 2)
-        if (i + 1 < nchunks) {
-            VIHMC_CBB_GLDS(i + 1, (i + 1) % 3)
-        }
-        const unsigned char* img = smb + (i % 3) * CB_QIMG;
+        // split G(i) first: hipcc's wait for its loads then sits before this chunk's DMA (which it cannot see and
+        // would otherwise wait for too); the empty asm pins the split ahead of the DMA's asm
         bf16x8 ga[CBB_NS][3];
 #pragma unroll
         for (int s = 0; s < CBB_NS; ++s) {
@@ -578,7 +575,13 @@ __global__ __launch_bounds__(CBB_THREADS, 1) void k_contract_bf_b(ContractProb P
             ga[s][0] = cat8(l0, h0);
             ga[s][1] = cat8(l1, h1);
             ga[s][2] = cat8(l2, h2);
+            asm volatile("" :: "v"(ga[s][0]), "v"(ga[s][1]), "v"(ga[s][2]));
         }
+        if (i + 1 < nchunks) {
+            VIHMC_CBB_GLDS(i + 1, (i + 1) % 3)
+        }
+        VIHMC_CBB_GLOAD(gn, min(i + 1, nchunks - 1))
+        const unsigned char* img = smb + (i % 3) * CB_QIMG;
 #pragma unroll
         for (int t = 0; t < 7; ++t) {
             bf16x8 qb[3];
@@ -592,13 +595,17 @@ __global__ __launch_bounds__(CBB_THREADS, 1) void k_contract_bf_b(ContractProb P
 #pragma unroll
             for (int s = 0; s < CBB_NS; ++s) dacc[s][t] = six(ga[s], qb, dacc[s][t]);
         }
-        if (CB_ASM_DMA) bf6::wait_vmcnt0();   // this chunk's DMA (i+1) and G loads (i+2) done
+        // the image of chunk i+1 landed before the next barrier; G(i+1) may stay in flight
+        if (CBB_NS == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     };
-    for (int i = 0; i < nchunks; i += 3) {
-        chunk(i, ga_, gc_);
+    int i = 0;
+    for (; i + 1 < nchunks; i += 2) {
+        chunk(i, ga_, gb_);
         chunk(i + 1, gb_, ga_);
-        chunk(i + 2, gc_, gb_);
     }
+    if (i < nchunks) chunk(i, ga_, gb_);
+    bf6::wait_vmcnt0();                              // the clamped tail loads retired
     float* out = P.out + c * P.out_cs + (int64_t)qc * P.out_chunk_stride;
 #pragma unroll
     for (int s = 0; s < CBB_NS; ++s)
