@@ -515,6 +515,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
                         // pair, not knowing the DMA target disjoint; the wave then waits for the DMA itself at the
                         // end of the layer, before the barrier that publishes it
 #endif
+#ifndef FWD_DMA_CNT0
+#define FWD_DMA_CNT0 0  // 1: drain vmcnt(0) at the end of each layer (A/B)
+#endif
 #if FWD_ASM_DMA
 #define VIHMC_FB_DMA(J, BUF)                                                                          \
     for (int k = wave; k < FWD_WIMG / 1024; k += NW)                                                  \
@@ -580,7 +583,12 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         if (!dma) {
             VIHMC_FB_STORE((j + 1) & 1)
         }
-        if (FWD_ASM_DMA && dma) bf6::wait_vmcnt0();       // layer j+1's image landed before the next barrier
+        // layer j+1's image landed before the next barrier. The DMA was issued ahead of this layer's seven h stores
+        // (six b128 + the tile-6 b32), so a counted wait leaves those stores in flight (vmcnt(0) waited for them)
+        if (FWD_ASM_DMA && dma) {
+            if (FWD_TAILF32 && !FWD_DMA_CNT0) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+            else bf6::wait_vmcnt0();
+        }
     }
     // the output layer's rows as the contraction's pre-split image (bit-identical to k_split_blocks on the fp32
     // rows just stored: same conversions), which saves that kernel's re-read of the outputs and its launch
