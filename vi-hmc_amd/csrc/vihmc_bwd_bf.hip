@@ -449,18 +449,32 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
 #endif
 
     // ---- W^T planes (once per workgroup): rows i < n_in, features k < 100 ----
-    if (P.has_dx) {
+    if (P.has_dx && wave < 12) {
+        // by the dX and dW waves only (the staging waves start their first sub-tiles' loads meanwhile), all of a
+        // thread's W^T loads (n_in * 25 <= 2800 float4 over 768 threads: <= 4) issued before the first split, so
+        // the prologue waits out one HBM latency instead of one per iteration
         const float* WT = P.WT + c * P.wt_cs;
-        for (int idx = tid; idx < P.n_in * 25; idx += BB_THREADS) {
+        constexpr int WTH = 768;
+        constexpr int WSL = (112 * 25 + WTH - 1) / WTH;
+        f32x4 wx[WSL];
+#pragma unroll
+        for (int v = 0; v < WSL; ++v) {
+            const int idx = min(tid + WTH * v, P.n_in * 25 - 1);
             const int r = idx / 25, c4 = idx - r * 25;
-            const f32x4 x = *reinterpret_cast<const f32x4*>(WT + (int64_t)r * P.ldw + 4 * c4);
+            wx[v] = *reinterpret_cast<const f32x4*>(WT + (int64_t)r * P.ldw + 4 * c4);
+        }
+#pragma unroll
+        for (int v = 0; v < WSL; ++v) {
+            const int idx = tid + WTH * v;
+            if (idx >= P.n_in * 25) break;
+            const int r = idx / 25, c4 = idx - r * 25;
             bf16x4 p0, p1, p2;
-            split4(x, p0, p1, p2);
+            split4(wx[v], p0, p1, p2);
             unsigned char* o = smw + BB_W + r * BB_WPITCH + 8 * c4;
             *reinterpret_cast<bf16x4*>(o) = p0;
             *reinterpret_cast<bf16x4*>(o + BB_WPLANE) = p1;
             *reinterpret_cast<bf16x4*>(o + 2 * BB_WPLANE) = p2;
-            if (c4 == 24) *reinterpret_cast<f32x4*>(smw + BB_WT + r * 16) = x;
+            if (c4 == 24) *reinterpret_cast<f32x4*>(smw + BB_WT + r * 16) = wx[v];
         }
     }
 
