@@ -69,6 +69,11 @@ constexpr int CBA_THREADS = 1024;
 #endif
 // G image per buffer: 8 S waves x 64 lanes x (3 bf16x8 planes = 48 B, or 2 f32x4 = 32 B)
 constexpr int CB_GIMG = CBA_GSPLIT ? 8 * 3 * 64 * 16 : 8 * 2 * 64 * 16;
+#ifndef CBA_GSUM32
+#define CBA_GSUM32 1    // sum G: per chunk an fp32 partial of the lane's 8 terms, then fp64 (as sum r^2); its rounding,
+                        // ~1e-6 of the b gradient, is below the reference's own fp32 sum over N x P terms. 0: every term
+                        // in fp64 (8 conversions and fp64 adds per lane and chunk on the S waves' issue path)
+#endif
 #ifndef CBA_PIPE
 #define CBA_PIPE 0      // 1: 4 Q buffers, asm LDS-DMA two chunks ahead kept in flight across raw barriers
                         // (counted vmcnt, no vmcnt(0) at every __syncthreads)
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                 const unsigned char* img = smc + (i % CB_NQBUF) * CB_QIMG;
                 VIHMC_CB_YLOAD(yn, min(i + 1, nchunks - 1))
                 unsigned char* gimg = smc + CB_NQBUF * CB_QIMG + (i & 1) * CB_GIMG + w * (CB_GIMG / 8);
-                float ps = 0.f;
+                float ps = 0.f, gp = 0.f;
                 f32x4 gs[2];
 #pragma unroll
                 for (int sub = 0; sub < 2; ++sub) {
@@ -237,7 +242,10 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                         rv = ok ? rv : 0.f;
                         g[r] = P.gscale * rv;
                         ps = fmaf(rv, rv, ps);
-                        if (CB_ABL != 4) gsum += (double)g[r];  // G terms cancel: exact-order fp64, not fp32 partials
+                        if (CB_ABL != 4) {
+                            if (CBA_GSUM32) gp += g[r];
+                            else gsum += (double)g[r];
+                        }
                     }
                     if (!CBA_GSPLIT) reinterpret_cast<f32x4*>(gimg)[sub * 64 + lane] = g;
                     gs[sub] = g;
@@ -280,6 +288,7 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                 }
                 // sum r^2 (no cancellation): per-chunk fp32 partial of 8 terms per lane, then fp64
                 ssq += (double)ps;
+                if (CBA_GSUM32) gsum += (double)gp;
 #if CB_STAMP
                 asm volatile("" :: "v"(ps));
                 VIHMC_CB_STAMP(i, 1)
