@@ -206,6 +206,7 @@ struct MlpTrajArgs {
     const float* th_in; float* th_out; const float* p_in; float* p_out; const float* g_in; float* g_out;
     float* lp_out; const float* eps; const float* inv_mass; int32_t L;
     int32_t ws_floats;             // set by launch_mlp_traj: the evaluation workspace (mlp_lds_bytes) in floats
+    int32_t cache;                 // set by launch_mlp_traj: 1 = data rows / index map / prior / mass cached in LDS
 };
 hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int maxw, hipStream_t s);
 

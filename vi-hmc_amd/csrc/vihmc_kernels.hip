@@ -15,6 +15,7 @@
 //   Functional_Net.functional_model       Neural_network/VI_HMC/my_make_func.py:52-73
 // and torch.autograd.grad through them (hamiltorch params_grad).
 #include "vihmc_internal.h"
+#include <cstdlib>
 
 namespace vihmc {
 
@@ -252,17 +253,45 @@ constexpr int MLP_SLD = 65;
 // (widths 10): MAXW = 16 took 34 us per leapfrog step against 21-23 us for the plain loops (MAXW = 0, shipped).
 #define VIHMC_MLP_FOR(v, n) \
     _Pragma("unroll") for (int v = 0; v < (MAXW > 0 ? MAXW : (n)); ++v) if (MAXW == 0 || v < (n))
+// the row sums (run-time count: the data rows of one 64-row pass) unrolled by 4 so each group's LDS reads are issued
+// together; the accumulation order, and so the rounding, is that of the plain loop
 #define VIHMC_MLP_ROWS(v, n) \
-    _Pragma("unroll") for (int v = 0; v < (MAXW > 0 ? 64 : (n)); ++v) if (MAXW == 0 || v < (n))
+    _Pragma("unroll 4") for (int v = 0; v < (MAXW > 0 ? 64 : (n)); ++v) if (MAXW == 0 || v < (n))
 
-template <int MAXW, class ThetaAt, class GradOut>
-__device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* sm, int c, ThetaAt theta_at,
-                                                GradOut grad_out, bool want_grad, float* out) {
+// Layer widths: MlpDyn reads them from the plan at run time; MlpFix<in, w1, ..., out> fixes them at compile time,
+// so every width loop (and the layer loop) unrolls completely and the LDS reads of a layer are issued ahead of its
+// FMA chains. Same loops, same order: the rounding is that of the run-time form.
+struct MlpDyn {
+    static constexpr int NL = 0;
+    static constexpr int dim(int) { return 0; }
+};
+template <int... Ds>
+struct MlpFix {
+    static constexpr int NL = (int)sizeof...(Ds) - 1;
+    static constexpr int dim(int i) {
+        constexpr int d[] = {Ds...};
+        return d[i];
+    }
+};
+using MlpBnn = MlpFix<1, 10, 10, 1>;     // the reference's BNN (Neural_network/*: 1 -> 10 -> 10 -> 1, D = 141)
+
+// the per-step read-only operands, from the plan (global) or from an LDS copy (k_mlp_traj); passed beside the
+// kernel arguments rather than in a modified copy of them (a private MlpArgs went to scratch memory)
+struct MlpRead {
+    const float* x; const float* y; const int32_t* idx; const float* prior_mu; const float* prior_inv_var;
+};
+
+template <int MAXW, class SH = MlpDyn, class ThetaAt, class GradOut>
+__device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, MlpRead rd, int W, float* sm, int c,
+                                                ThetaAt theta_at, GradOut grad_out, bool want_grad, float* out) {
     // no implicit contraction into fma: the two kernels that inline this body (k_mlp, k_mlp_traj) must round
     // identically (explicit fmaf calls stay fused)
 #pragma clang fp contract(off)
     constexpr int SLD = MLP_SLD;
-    const int NL = a.n_layers;
+    constexpr bool FIX = SH::NL > 0;
+    const int NL = FIX ? SH::NL : a.n_layers;
+    const int in_dim = FIX ? SH::dim(0) : a.in_dim;
+    const int out_dim = FIX ? SH::dim(FIX ? SH::NL : 0) : a.out_dim;
     float* w = sm;
     float* gw = w + a.D;
     float* hs = gw + a.D;
@@ -280,36 +309,42 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
         const int row = r0 + lane;
         const bool ok = row < a.N;
         const int rr = ok ? row : 0;
-        for (int i = 0; i < a.in_dim; ++i) hs[i * SLD + lane] = a.x[(int64_t)rr * a.in_dim + i];
+#pragma unroll
+        for (int i = 0; i < in_dim; ++i) hs[i * SLD + lane] = rd.x[(int64_t)rr * in_dim + i];
+#pragma unroll
         for (int l = 0; l < NL; ++l) {
             const MlpLayer L = a.L[l];
+            const int nin = FIX ? SH::dim(l) : L.n_in, nout = FIX ? SH::dim(l + 1) : L.n_out;
             const float* hin = hs + l * W * SLD;
-            VIHMC_MLP_FOR(j, L.n_out) {
+            VIHMC_MLP_FOR(j, nout) {
                 float s = 0.f;
-                VIHMC_MLP_FOR(i, L.n_in) s = fmaf(w[L.w_off + j * L.n_in + i], hin[i * SLD + lane], s);
+                VIHMC_MLP_FOR(i, nin) s = fmaf(w[L.w_off + j * nin + i], hin[i * SLD + lane], s);
                 if (L.b_off >= 0) s += w[L.b_off + j];
                 zs[(l * W + j) * SLD + lane] = s;
                 hs[((l + 1) * W + j) * SLD + lane] = act_apply(L.act, s);
             }
         }
         const float* hout = hs + NL * W * SLD;
-        for (int o = 0; o < a.out_dim; ++o) {
-            const float yv = a.y[(int64_t)rr * a.out_dim + o];
+#pragma unroll
+        for (int o = 0; o < out_dim; ++o) {
+            const float yv = rd.y[(int64_t)rr * out_dim + o];
             const float pred = hout[o * SLD + lane];
             const float rv = pred - yv;
             float g = 0.f;
             if (ok) {
                 ssq += (double)rv * (double)rv;
                 g = gscale * rv;
-                if (out) out[((int64_t)c * a.N + row) * a.out_dim + o] = pred;
+                if (out) out[((int64_t)c * a.N + row) * out_dim + o] = pred;
             }
             gs[o * SLD + lane] = g;
         }
         if (!want_grad) continue;
+#pragma unroll
         for (int l = NL - 1; l >= 0; --l) {
             const MlpLayer L = a.L[l];
+            const int nin = FIX ? SH::dim(l) : L.n_in, nout = FIX ? SH::dim(l + 1) : L.n_out;
             const float* hin = hs + l * W * SLD;
-            VIHMC_MLP_FOR(j, L.n_out) {
+            VIHMC_MLP_FOR(j, nout) {
                 const float z = zs[(l * W + j) * SLD + lane];
                 const float h = hs[((l + 1) * W + j) * SLD + lane];
                 ds[j * SLD + lane] = gs[j * SLD + lane] * act_grad_z(L.act, z, h);
@@ -318,13 +353,13 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
             // dW[j][i] = sum_rows d[j] h[i], db[j] = sum_rows d[j]: every lane owns distinct entries and
             // sums the staged rows in a fixed order. Rows past N carry d = 0 and are skipped (fmaf(0, h, s) = s:
             // the same sums, 64 / N times fewer dependent steps -- 20 of 64 rows on the shipped BNN data).
-            const int nw = L.n_out * L.n_in;
-            const int ne = nw + (L.b_off >= 0 ? L.n_out : 0);
+            const int nw = nout * nin;
+            const int ne = nw + (L.b_off >= 0 ? nout : 0);
             const int nrow = min(64, a.N - r0);
             for (int e = lane; e < ne; e += 64) {
                 float s = 0.f;
                 if (e < nw) {
-                    const int j = e / L.n_in, i = e - j * L.n_in;
+                    const int j = e / nin, i = e - j * nin;
                     VIHMC_MLP_ROWS(m, nrow) s = fmaf(ds[j * SLD + m], hin[i * SLD + m], s);
                     gw[L.w_off + e] += s;
                 } else {
@@ -334,9 +369,9 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
                 }
             }
             if (l > 0) {
-                VIHMC_MLP_FOR(i, L.n_in) {
+                VIHMC_MLP_FOR(i, nin) {
                     float s = 0.f;
-                    VIHMC_MLP_FOR(j, L.n_out) s = fmaf(ds[j * SLD + lane], w[L.w_off + j * L.n_in + i], s);
+                    VIHMC_MLP_FOR(j, nout) s = fmaf(ds[j * SLD + lane], w[L.w_off + j * nin + i], s);
                     gs[i * SLD + lane] = s;
                 }
             }
@@ -352,16 +387,16 @@ __device__ __forceinline__ double mlp_eval_core(const MlpArgs& a, int W, float* 
     double lp = 0.0;
     for (int k = lane; k < a.K; k += 64) {
         const float th = theta_at(k);
-        const float dd = th - a.prior_mu[k];
-        const float iv = a.prior_inv_var[k];
+        const float dd = th - rd.prior_mu[k];
+        const float iv = rd.prior_inv_var[k];
         lp += -0.5 * (double)dd * (double)dd * (double)iv;
-        if (want_grad) grad_out(k, gw[a.idx[k]] - dd * iv * inv_scale);
+        if (want_grad) grad_out(k, gw[rd.idx[k]] - dd * iv * inv_scale);
     }
     lp = wave_sum(lp);
     return ll + (lp + a.prior_const) / (double)a.prior_scale;
 }
 
-template <int MAXW>
+template <int MAXW, class SH = MlpDyn>
 __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
     extern __shared__ float sm[];
     float* w = sm;
@@ -372,8 +407,9 @@ __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
     __syncthreads();
     const float* th = a.theta + (int64_t)c * a.K;
     float* gr = a.grad ? a.grad + (int64_t)c * a.K : nullptr;
-    const double lp = mlp_eval_core<MAXW>(
-        a, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gr[k] = g; }, gr != nullptr, a.out);
+    const MlpRead rd{a.x, a.y, a.idx, a.prior_mu, a.prior_inv_var};
+    const double lp = mlp_eval_core<MAXW, SH>(
+        a, rd, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gr[k] = g; }, gr != nullptr, a.out);
     if (lane == 0) a.logp[c] = (float)lp;
 }
 
@@ -382,7 +418,7 @@ __global__ __launch_bounds__(64) void k_mlp(MlpArgs a, int W) {
 // every product and sum rounded separately (fp contract off: no fma), as the torch
 // elementwise ops round them, so the result is bitwise the step-by-step path. theta / momentum / gradient of
 // the chain live in LDS after the evaluation's workspace; one wave per chain, no host round trip per step.
-template <int MAXW>
+template <int MAXW, class SH = MlpDyn>
 __global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t) {
     // products and sums written here are rounded separately (the HIP __fmul_rn / __fadd_rn helpers are plain * and
     // + defined in a header, outside this pragma's reach: the compiler fused them into fma)
@@ -393,6 +429,28 @@ __global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t
     float* th = sm + t.ws_floats;
     float* pm = th + K;
     float* gk = pm + K;
+    // t.cache: the per-step read-only operands (data rows, sampled-index map, prior, mass) copied into LDS once per
+    // trajectory, so a leapfrog step issues no global loads (each was an L2 round trip per step before)
+    MlpRead rd{a.x, a.y, a.idx, a.prior_mu, a.prior_inv_var};
+    const float* im = t.inv_mass;
+    if (t.cache) {
+        float* xs = gk + K;
+        float* ys = xs + a.N * a.in_dim;
+        float* pmu = ys + a.N * a.out_dim;
+        float* piv = pmu + K;
+        float* ims = piv + K;
+        int32_t* ids = reinterpret_cast<int32_t*>(ims + K);
+        for (int i = lane; i < a.N * a.in_dim; i += 64) xs[i] = a.x[i];
+        for (int i = lane; i < a.N * a.out_dim; i += 64) ys[i] = a.y[i];
+        for (int k = lane; k < K; k += 64) {
+            pmu[k] = a.prior_mu[k];
+            piv[k] = a.prior_inv_var[k];
+            ids[k] = a.idx[k];
+            if (im) ims[k] = im[k];
+        }
+        rd = MlpRead{xs, ys, ids, pmu, piv};
+        if (im) im = ims;
+    }
     for (int i = lane; i < a.D; i += 64) w[i] = a.frozen[i];
     const float e = t.eps[c], he = 0.5f * e;
     const int64_t off = (int64_t)c * K;
@@ -404,14 +462,14 @@ __global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t
     double lp = 0.0;
     for (int s = 0; s < t.L; ++s) {
         for (int k = lane; k < K; k += 64) {
-            const float step = t.inv_mass ? (e * t.inv_mass[k]) * pm[k] : e * pm[k];
+            const float step = im ? (e * im[k]) * pm[k] : e * pm[k];
             th[k] = th[k] + step;
         }
         __syncthreads();
-        for (int k = lane; k < K; k += 64) w[a.idx[k]] = th[k];
+        for (int k = lane; k < K; k += 64) w[rd.idx[k]] = th[k];
         __syncthreads();
-        lp = mlp_eval_core<MAXW>(
-            a, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gk[k] = g; }, true, nullptr);
+        lp = mlp_eval_core<MAXW, SH>(
+            a, rd, W, sm, c, [&](int k) { return th[k]; }, [&](int k, float g) { gk[k] = g; }, true, nullptr);
         for (int k = lane; k < K; k += 64) pm[k] = pm[k] + e * gk[k];
     }
     for (int k = lane; k < K; k += 64) {
@@ -475,6 +533,20 @@ hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in
                  inv_mass, K);
 }
 
+// the plan's layers are exactly MlpBnn's widths (then the compile-time form runs); VIHMC_MLP_FIX=0: never
+static bool mlp_is_bnn(const MlpArgs& a, int maxw) {
+    static const bool on = [] {
+        const char* e = std::getenv("VIHMC_MLP_FIX");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (!on || a.n_layers != MlpBnn::NL || maxw != 10 || a.in_dim != MlpBnn::dim(0) ||
+        a.out_dim != MlpBnn::dim(MlpBnn::NL))
+        return false;
+    for (int l = 0; l < MlpBnn::NL; ++l)
+        if (a.L[l].n_in != MlpBnn::dim(l) || a.L[l].n_out != MlpBnn::dim(l + 1)) return false;
+    return true;
+}
+
 size_t mlp_lds_bytes(int D, int n_layers, int maxw) {
     return sizeof(float) * (2 * (size_t)D + (size_t)(2 * n_layers + 3) * maxw * MLP_SLD);
 }
@@ -482,15 +554,24 @@ size_t mlp_lds_bytes(int D, int n_layers, int maxw) {
 hipError_t launch_mlp(const MlpArgs& a, int C, int maxw, hipStream_t s) {
     const size_t shm = mlp_lds_bytes(a.D, a.n_layers, maxw);
     if (shm > 160 * 1024) return hipErrorInvalidValue;
+    if (mlp_is_bnn(a, maxw)) VIHMC_LAUNCH((k_mlp<0, MlpBnn>), dim3(C), dim3(64), shm, s, a, maxw);
     VIHMC_LAUNCH(k_mlp<0>, dim3(C), dim3(64), shm, s, a, maxw);
 }
 
 hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int maxw, hipStream_t s) {
     const size_t ws = mlp_lds_bytes(a.D, a.n_layers, maxw);
-    const size_t shm = ws + 3 * sizeof(float) * (size_t)a.K;
+    size_t shm = ws + 3 * sizeof(float) * (size_t)a.K;
     if (shm > 160 * 1024 || t.L < 1) return hipErrorInvalidValue;
     MlpTrajArgs tt = t;
     tt.ws_floats = (int32_t)(ws / sizeof(float));
+    const size_t cache = sizeof(float) * ((size_t)a.N * (a.in_dim + a.out_dim) + 4 * (size_t)a.K);
+    static const bool cache_on = [] {
+        const char* e = std::getenv("VIHMC_MLP_CACHE");
+        return !e || std::atoi(e) != 0;
+    }();
+    tt.cache = cache_on && shm + cache <= 160 * 1024 ? 1 : 0;
+    if (tt.cache) shm += cache;
+    if (mlp_is_bnn(a, maxw)) VIHMC_LAUNCH((k_mlp_traj<0, MlpBnn>), dim3(C), dim3(64), shm, s, a, maxw, tt);
     VIHMC_LAUNCH(k_mlp_traj<0>, dim3(C), dim3(64), shm, s, a, maxw, tt);
 }
 
