@@ -740,9 +740,12 @@ static_assert(BBUF <= FWD_WIMG && FWD_WTAIL + FW * 16 <= FWD_WIMG && FWD_WIMG % 
 bool fwd_fused_bf_needs_wimg() { return FWD_TAILF32 != 0; }
 int fwd_fused_bf_waves() { return FWD_BF_NW; }
 
-hipError_t launch_fwd_fused_bf(const FusedArgs& a, hipStream_t s) {
+hipError_t launch_fwd_fused_bf(const FusedArgs& a, int nw, hipStream_t s) {
     dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk));
-    hipLaunchKernelGGL(k_fwd_fused_bf<FWD_BF_NW>, g, dim3(FWD_BF_NW * 64), fwd_fused_bf_lds_bytes(), s, a);
+    // 4 waves (64 rows per workgroup) for chain counts whose 12-wave grid would leave most CUs idle (single chain:
+    // 176 workgroups instead of 60)
+    if (nw == 4) hipLaunchKernelGGL(k_fwd_fused_bf<4>, g, dim3(4 * 64), fwd_fused_bf_lds_bytes(), s, a);
+    else hipLaunchKernelGGL(k_fwd_fused_bf<FWD_BF_NW>, g, dim3(FWD_BF_NW * 64), fwd_fused_bf_lds_bytes(), s, a);
     return hipGetLastError();
 }
 

@@ -564,8 +564,14 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
         const int v = std::atoi(e);
         if (v == 4 || v == 12 || v == 16) nw = v;
     }
-    if (p->fwd_bf16x6 && nw == 12 && (!fwd_fused_bf_needs_wimg() || (p->fwd_wimg && p->wimg))) {
-        for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * fwd_fused_bf_waves());
+    // bf16x6 at 12 waves, or at 4 for small chain counts (VIHMC_FWD_BF4=0: the fp32 4-wave kernel there instead)
+    static const bool bf4 = [] {
+        const char* e = std::getenv("VIHMC_FWD_BF4");
+        return !e || std::atoi(e) != 0;
+    }();
+    const int nwb = nw == 12 ? fwd_fused_bf_waves() : 4;
+    if (p->fwd_bf16x6 && (nw == 12 || (nw == 4 && bf4)) && (!fwd_fused_bf_needs_wimg() || (p->fwd_wimg && p->wimg))) {
+        for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * nwb);
         if (img && fwd_writes_img()) {
             // the contraction's pre-split images of the branch (side A) and trunk (side B) outputs
             a.net[0].qimg = p->qsplitA;
@@ -581,7 +587,7 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
             a.net[0].wimg_cs = a.net[1].wimg_cs = p->wimg_cs;
             HIPCHK(launch_split_wimg(a, s));
         }
-        HIPCHK(launch_fwd_fused_bf(a, s));
+        HIPCHK(launch_fwd_fused_bf(a, nwb, s));
         return 0;
     }
     for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * nw);
