@@ -734,6 +734,16 @@ hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+int fwd_img_plane_off(int n, int col) {
+    // inverse of k_split_wimg's position -> column map (VIHMC_FB_STORE's permuted column order)
+    const int t = col >> 4, g = (col >> 2) & 3, e = col & 3;
+    const int pos = t < 6 ? (t >> 1) * 32 + g * 8 + (t & 1) * 4 + e : 96 + g * 4 + e;
+    return 2 * (n * BROW + pos);
+}
+int fwd_img_plane_stride() { return 2 * BPLANE; }
+int fwd_img_bias_off(int n) { return 3 * BPLANE * 2 + 4 * n; }
+int fwd_img_tail_off(int n, int col) { return FWD_WTAIL + 4 * (n * 4 + (col - 96)); }
+
 size_t fwd_fused_bf_lds_bytes() { return 2 * (size_t)FWD_WIMG; }
 static_assert(BBUF <= FWD_WIMG && FWD_WTAIL + FW * 16 <= FWD_WIMG && FWD_WIMG % 1024 == 0 &&
               2 * FWD_WIMG <= 160 * 1024, "weight image");

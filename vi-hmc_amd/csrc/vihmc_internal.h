@@ -117,8 +117,15 @@ hipError_t launch_split_blocks(const float* src, int64_t src_cs, int ld, int row
 size_t contract_lds_bytes(int W);
 hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* frozen, const int32_t* map_w,
                               const int32_t* map_wt, int64_t D, hipStream_t s);
+// Optional: the bf16x6 forward's pre-split weight images kept current by the scatter itself (plane triple and the
+// fp32 copies -- k tail or bias -- of every sampled weight of a fused layer), so they are split from the full
+// weights only once per plan instead of once per evaluation (k_split_wimg). img_w / img_f: byte offsets inside a
+// chain's image region, -1 = none; null maps: packed only.
+struct ScatterImg {
+    unsigned char* img; int64_t img_cs; const int32_t* img_w; const int32_t* img_f; int32_t plane;  // plane stride (B)
+};
 hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, int K, const int32_t* smap_w,
-                          const int32_t* smap_wt, hipStream_t s);
+                          const int32_t* smap_wt, hipStream_t s, const ScatterImg* si = nullptr);
 // Sum `n_parts` partial slabs of `len` floats (slab stride `part_stride`, chain stride `in_cs`) into
 // dst[c*dst_cs + e] (e < len), fixed order.
 struct ReduceJob {
@@ -174,6 +181,12 @@ struct FusedArgs {
 constexpr int FWD_WIMG = 69632;                     // one pre-split weight image: 3 x [100][112] bf16 + fp32
                                                     // bias [112], zero padded to 68 KB (whole 1-KB DMA pieces)
 hipError_t launch_split_wimg(const FusedArgs& a, hipStream_t s);
+// byte offsets inside one layer image (k_split_wimg's layout): plane-0 bf16 of W[n][col], the plane stride, the
+// fp32 bias[n], and the fp32 k-tail copy of W[n][col] for col in 96..99
+int fwd_img_plane_off(int n, int col);
+int fwd_img_plane_stride();
+int fwd_img_bias_off(int n);
+int fwd_img_tail_off(int n, int col);
 bool fwd_fused_bf_needs_wimg();                     // the bf16x6 forward reads the fp32 k tail of the image
 int fwd_fused_bf_waves();                           // its waves per workgroup (16 rows each)
 // Nonzero when a translation unit was built with a timing-only ablation (FWD_ABL, CB_ABL, BB_ABL: wrong

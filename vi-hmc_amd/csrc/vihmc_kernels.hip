@@ -62,13 +62,29 @@ __global__ void k_init_packed(float* packed, int64_t dp, const float* frozen, co
 }
 
 __global__ void k_scatter(float* packed, int64_t dp, const float* theta, int K, const int32_t* smap_w,
-                          const int32_t* smap_wt) {
+                          const int32_t* smap_wt, ScatterImg si) {
     const int c = blockIdx.y;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
         const float v = theta[(int64_t)c * K + k];
         packed[c * dp + smap_w[k]] = v;
         const int32_t t = smap_wt[k];
         if (t >= 0) packed[c * dp + t] = v;
+        if (si.img_w != nullptr) {
+            unsigned char* img = si.img + c * si.img_cs;
+            const int32_t o = si.img_w[k];
+            if (o >= 0) {
+                // the three planes exactly as k_split_wimg splits them
+                const __bf16 a = (__bf16)v;
+                const float r = v - (float)a;
+                const __bf16 b = (__bf16)r;
+                const __bf16 cc = (__bf16)(r - (float)b);
+                *reinterpret_cast<__bf16*>(img + o) = a;
+                *reinterpret_cast<__bf16*>(img + o + si.plane) = b;
+                *reinterpret_cast<__bf16*>(img + o + 2 * si.plane) = cc;
+            }
+            const int32_t f = si.img_f[k];
+            if (f >= 0) *reinterpret_cast<float*>(img + f) = v;
+        }
     }
 }
 
@@ -493,9 +509,9 @@ hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* fro
 }
 
 hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, int K, const int32_t* smap_w,
-                          const int32_t* smap_wt, hipStream_t s) {
+                          const int32_t* smap_wt, hipStream_t s, const ScatterImg* si) {
     dim3 g((unsigned)std::min((K + 255) / 256, 256), C), blk(256);
-    VIHMC_LAUNCH(k_scatter, g, blk, 0, s, packed, dp, theta, K, smap_w, smap_wt);
+    VIHMC_LAUNCH(k_scatter, g, blk, 0, s, packed, dp, theta, K, smap_w, smap_wt, si ? *si : ScatterImg{});
 }
 
 hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s) {

@@ -76,6 +76,9 @@ struct vihmc_plan {
 
     int32_t* smap_w = nullptr;
     int32_t* smap_wt = nullptr;
+    int32_t* smap_img = nullptr;    // per sampled index: byte offset of its weight-image plane element, or -1
+    int32_t* smap_imgf = nullptr;   // ... of its fp32 image copy (k tail / bias), or -1
+    bool img_by_scatter = false;    // the weight images are split once and kept current by k_scatter
     float* prior_mu = nullptr;
     float* prior_iv = nullptr;
     double prior_const = 0.0;
@@ -237,6 +240,53 @@ int check_lik(const vihmc_lik_desc& l) {
     if (l.loss != VIHMC_LOSS_NLL && l.loss != VIHMC_LOSS_REGRESSION) return fail("unsupported loss kind");
     if (!(l.prior_scale > 0.f)) return fail("prior_scale must be > 0");
     return 0;
+}
+
+bool fused_forward_ok(const vihmc_plan* p);
+void fused_args(vihmc_plan* p, int C, FusedArgs& a);
+
+// Weight images kept current by the scatter (ScatterImg): per sampled index the byte offsets of its plane element
+// and of its fp32 copy (k tail / bias) inside a chain's images; then every chain's images are split once from the
+// initial packed weights. Only when the fused forward owns layers 1.. of both nets (otherwise k_split_wimg per
+// evaluation, or no images).
+int image_maps(vihmc_plan* p, const vihmc_deeponet_desc* d, const int64_t* idx) {
+    if (!fused_forward_ok(p)) return 0;
+    if (const char* e = std::getenv("VIHMC_IMG_SCATTER"))      // 0: split per evaluation (A/B)
+        if (std::atoi(e) == 0) return 0;
+    std::vector<int32_t> fw(p->D, -1), ff(p->D, -1);
+    int img = 0;
+    const vihmc_linear* tabs[2] = {d->branch, d->trunk};
+    const int nl[2] = {d->n_branch_layers, d->n_trunk_layers};
+    for (int net = 0; net < 2; ++net)
+        for (int j = 1; j < nl[net]; ++j, ++img) {
+            const vihmc_linear& l = tabs[net][j];
+            const int64_t base = (int64_t)img * FWD_WIMG;
+            for (int r = 0; r < l.n_out; ++r) {
+                for (int c = 0; c < l.n_in; ++c) {
+                    const int64_t f = l.w_off + (int64_t)r * l.n_in + c;
+                    fw[f] = (int32_t)(base + fwd_img_plane_off(r, c));
+                    if (c >= 96) ff[f] = (int32_t)(base + fwd_img_tail_off(r, c));
+                }
+                ff[l.b_off + r] = (int32_t)(base + fwd_img_bias_off(r));
+            }
+        }
+    std::vector<int32_t> sw(p->K), sf(p->K);
+    for (int k = 0; k < p->K; ++k) {
+        sw[k] = fw[idx[k]];
+        sf[k] = ff[idx[k]];
+    }
+    if (int rc = p->upload(&p->smap_img, sw.data(), p->K)) return rc;
+    if (int rc = p->upload(&p->smap_imgf, sf.data(), p->K)) return rc;
+    FusedArgs a{};
+    fused_args(p, p->maxC, a);
+    HIPCHK(launch_split_wimg(a, nullptr));
+    HIPCHK(hipDeviceSynchronize());
+    p->img_by_scatter = true;
+    return 0;
+}
+
+ScatterImg scatter_img(const vihmc_plan* p) {
+    return ScatterImg{p->wimg, p->wimg_cs, p->smap_img, p->smap_imgf, fwd_img_plane_stride()};
 }
 
 int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb, const float* tf, const float* y,
@@ -493,6 +543,9 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         p->n_jobsW = (int)jw.size();
         if (int rc = p->upload(&p->jobsW, jw.data(), (int64_t)jw.size())) return rc;
     }
+    // weight images maintained by the scatter (after the activation layout, which fused_args reads)
+    if (p->wimg)
+        if (int rc = image_maps(p, d, idx)) return rc;
     return 0;
 }
 
@@ -535,8 +588,7 @@ bool fwd_writes_img() {
     return on;
 }
 
-int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
-    FusedArgs a{};
+void fused_args(vihmc_plan* p, int C, FusedArgs& a) {
     a.C = C;
     a.packed = p->packed;
     a.dp = p->dp;
@@ -557,6 +609,15 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
         }
         f.rows = n.rows;
     }
+    a.net[0].wimg = p->wimg;
+    a.net[1].wimg = p->wimg ? p->wimg + (int64_t)a.net[0].nl * FWD_WIMG : nullptr;
+    a.net[0].wimg_cs = a.net[1].wimg_cs = p->wimg_cs;
+}
+
+int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
+    FusedArgs a{};
+    fused_args(p, C, a);
+    a.net[0].wimg = a.net[1].wimg = nullptr;           // set below when the bf16x6 kernel stages them
     // 12-wave workgroups (one per CU, 84 KB LDS) unless that grid would leave most of the 256 CUs idle
     const int64_t blocks12 = (int64_t)C * (cdiv(p->nets[0].rows, 192) + cdiv(p->nets[1].rows, 192));
     int nw = blocks12 >= 192 ? 12 : 4;
@@ -581,11 +642,12 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
             p->img_by_fwd = true;
         }
         if (p->fwd_wimg && p->wimg) {
-            // pre-split weight images, DMA-staged by the forward (FWD_WIMG bytes per fused layer)
+            // pre-split weight images, DMA-staged by the forward (FWD_WIMG bytes per fused layer); kept current by the
+            // scatter when the plan built its image maps, else split here from the packed weights
             a.net[0].wimg = p->wimg;
             a.net[1].wimg = p->wimg + (int64_t)a.net[0].nl * FWD_WIMG;
             a.net[0].wimg_cs = a.net[1].wimg_cs = p->wimg_cs;
-            HIPCHK(launch_split_wimg(a, s));
+            if (!p->img_by_scatter) HIPCHK(launch_split_wimg(a, s));
         }
         HIPCHK(launch_fwd_fused_bf(a, nwb, s));
         return 0;
@@ -716,7 +778,8 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
 
 int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
                        hipStream_t s, const LeapArgs* leap) {
-    HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s));
+    const ScatterImg si = scatter_img(p);
+    HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s, p->img_by_scatter ? &si : nullptr));
     const bool want_grad = grad != nullptr && out == nullptr;
     // the pre-split contraction images (bf16x6 sides, gradient evaluations) are written by the fused forward
     // when it runs; otherwise k_split_blocks makes them below
@@ -1182,7 +1245,8 @@ int deeponet_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, 
     a.ldd = ld_residue(128, 8);       // deltas [16][136]: float4 row reads of 16 rows are conflict free
     a.ldw = ld_residue(128, 4);       // W image [128][132]: b32 reads of rows 4 apart hit distinct bank groups
     a.count = (float)((double)N * npts);
-    e = launch_scatter(p->packed, p->dp, 1, theta, p->K, p->smap_w, p->smap_wt, s);
+    const ScatterImg si = scatter_img(p);
+    e = launch_scatter(p->packed, p->dp, 1, theta, p->K, p->smap_w, p->smap_wt, s, p->img_by_scatter ? &si : nullptr);
     int rc = e == hipSuccess ? deeponet_forward_layers(p, 1, s, false) : 0;
     SensArgs* dev_a = nullptr;
     if (e == hipSuccess && rc == 0) e = talloc((void**)&dev_a, sizeof(SensArgs));
