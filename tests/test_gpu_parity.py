@@ -130,6 +130,33 @@ def test_forward_without_weight_images_matches(cuda_device, monkeypatch):
     assert dlp.max() < 2e-6 and dg.max() < 2e-5, (dlp.max(), dg.max())
 
 
+def test_weight_images_kept_by_scatter_bitwise(cuda_device, monkeypatch):
+    """Weight images split once per plan and kept current by the scatter (default) == split from the packed weights
+    every evaluation (VIHMC_IMG_SCATTER=0), bit for bit, over a sequence of different thetas per chain and across a
+    single-chain sensitivity call (which scatters chain 0 too)."""
+    c = deeponet_case("deeponet_burgers")
+    rng = np.random.default_rng(5)
+    C = 3
+    base = c.thetas[0]
+    seq = [torch.tensor(np.stack([base + 0.01 * rng.standard_normal(base.size).astype(np.float32) for _ in range(C)]),
+                        device=cuda_device) for _ in range(3)]
+    res = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("VIHMC_IMG_SCATTER", env)
+        eng = engine_for(c, max_chains=C)
+        out = []
+        for i, th in enumerate(seq):
+            if i == 1:
+                N, P = np.asarray(c.prob.y).shape[-2:]
+                eng.sensitivity(th[2], pts=np.random.default_rng(1).integers(0, P, (N, 4)).astype(np.int32))
+            lp, g = eng.logp_grad(th)
+            out.append((lp.cpu(), g.cpu()))
+        res.append(out)
+        eng.close()
+    for (la, ga), (lb, gb) in zip(*res):
+        assert torch.equal(la, lb) and torch.equal(ga, gb)
+
+
 @pytest.mark.parametrize("name", ["deeponet_small", "deeponet_odd_full"])
 def test_deeponet_engine_vs_fp64_oracle_many_chains(name, cuda_device):
     """C chains with independent thetas in one launch == each chain against the fp64 oracle."""
