@@ -132,7 +132,14 @@ struct ReduceJob {
     const float* src; int64_t in_cs; int64_t part_stride; int32_t n_parts; int32_t len;
     float* dst; int64_t dst_cs;
 };
-hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s);
+// Likelihood statistics of the contraction (k_contract_stats): ll from the per-wave (sum r^2, sum G) pairs and
+// d ll / d b0 into packed slot 0 of gp. Optionally run as one extra grid slice of the weight-gradient reduce.
+struct StatsJob {
+    const double* stats; int64_t stats_cs; int32_t n_waves;
+    float* lik; float* gp; int64_t gp_cs; double count; int32_t loss; float tau_out;
+};
+hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s,
+                         const StatsJob* stats = nullptr);
 hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_waves, int C, float* lik,
                                  float* gp, int64_t gp_cs, double count, int loss, float tau_out, hipStream_t s);
 // Leapfrog update fused into the gradient gather (vihmc_trajectory on DeepONet plans), hamiltorch's order with

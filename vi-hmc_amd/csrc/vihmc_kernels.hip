@@ -88,9 +88,52 @@ __global__ void k_scatter(float* packed, int64_t dp, const float* theta, int K, 
     }
 }
 
-// Fixed-order sum of partial slabs (p = 0, 1, ... sequentially -- bitwise reproducible); 4 consecutive
+__device__ double block_sum_256(double v, double* sh) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+    }
+    __syncthreads();
+    return t;   // valid in thread 0
+}
+
+__device__ void contract_stats_body(const StatsJob& J, int c) {
+    __shared__ double sh[8];
+    const double* st = J.stats + c * J.stats_cs;
+    double ssq = 0.0, gs = 0.0;
+    for (int i = threadIdx.x; i < J.n_waves; i += blockDim.x) {
+        ssq += st[2 * i];
+        gs += st[2 * i + 1];
+    }
+    ssq = block_sum_256(ssq, sh);
+    gs = block_sum_256(gs, sh);
+    if (threadIdx.x == 0) {
+        double ll;
+        if (J.loss == 0) {
+            const double v = fmax((double)J.tau_out, 1e-6);
+            ll = -0.5 * (J.count * log(v) + ssq / v);
+        } else {
+            ll = -0.5 * (double)J.tau_out * ssq;
+        }
+        J.lik[c] = (float)ll;
+        J.gp[c * J.gp_cs] = (float)gs;   // d ll / d b0 (packed slot 0)
+    }
+}
+
+__global__ __launch_bounds__(256) void k_contract_stats(StatsJob J) { contract_stats_body(J, blockIdx.x); }
+
+// Fixed-order sum of partial slabs (p = 0, 1, ... sequentially -- bitwise reproducible); grid slice y = n_jobs
+// (when present) runs the likelihood statistics instead (saves their launch after side A); 4 consecutive
 // elements per thread as float4 when the job's strides allow, 8 slab loads in flight ahead of the adds.
-__global__ void k_reduce(const ReduceJob* jobs) {
+__global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_jobs, StatsJob sj) {
+    if ((int)blockIdx.y == n_jobs) {                   // the optional likelihood-statistics slice
+        if (blockIdx.x == 0) contract_stats_body(sj, blockIdx.z);
+        return;
+    }
     const ReduceJob J = jobs[blockIdx.y];
     const int c = blockIdx.z;
     const bool vec = ((J.len | J.part_stride | J.in_cs | J.dst_cs) & 3) == 0 &&
@@ -136,45 +179,6 @@ __global__ void k_reduce(const ReduceJob* jobs) {
     }
     for (; p < n; ++p) s += src[p * st];
     J.dst[c * J.dst_cs + e] = s;
-}
-
-__device__ double block_sum_256(double v, double* sh) {
-    v = wave_sum(v);
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) sh[w] = v;
-    __syncthreads();
-    double t = 0.0;
-    if (threadIdx.x == 0) {
-        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
-    }
-    __syncthreads();
-    return t;   // valid in thread 0
-}
-
-__global__ __launch_bounds__(256) void k_contract_stats(const double* stats, int64_t stats_cs, int n_waves,
-                                                        float* lik, float* gp, int64_t gp_cs, double count,
-                                                        int loss, float tau_out) {
-    __shared__ double sh[8];
-    const int c = blockIdx.x;
-    const double* st = stats + c * stats_cs;
-    double ssq = 0.0, gs = 0.0;
-    for (int i = threadIdx.x; i < n_waves; i += blockDim.x) {
-        ssq += st[2 * i];
-        gs += st[2 * i + 1];
-    }
-    ssq = block_sum_256(ssq, sh);
-    gs = block_sum_256(gs, sh);
-    if (threadIdx.x == 0) {
-        double ll;
-        if (loss == 0) {
-            const double v = fmax((double)tau_out, 1e-6);
-            ll = -0.5 * (count * log(v) + ssq / v);
-        } else {
-            ll = -0.5 * (double)tau_out * ssq;
-        }
-        lik[c] = (float)ll;
-        gp[c * gp_cs] = (float)gs;   // d ll / d b0 (packed slot 0)
-    }
 }
 
 // Gradient gather + prior: grid (GATHER_SPLIT slices, C); each block writes its partial log-prior
@@ -514,16 +518,17 @@ hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, 
     VIHMC_LAUNCH(k_scatter, g, blk, 0, s, packed, dp, theta, K, smap_w, smap_wt, si ? *si : ScatterImg{});
 }
 
-hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s) {
+hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s,
+                         const StatsJob* stats) {
     // grid sized for the scalar path; vectorised jobs leave 3/4 of the x-blocks idle (cheap exits)
-    dim3 g((max_len + 255) / 256, n_jobs, C), blk(256);
-    VIHMC_LAUNCH(k_reduce, g, blk, 0, s, jobs_dev);
+    dim3 g((max_len + 255) / 256, n_jobs + (stats ? 1 : 0), C), blk(256);
+    VIHMC_LAUNCH(k_reduce, g, blk, 0, s, jobs_dev, n_jobs, stats ? *stats : StatsJob{});
 }
 
 hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_waves, int C, float* lik,
                                  float* gp, int64_t gp_cs, double count, int loss, float tau_out, hipStream_t s) {
-    VIHMC_LAUNCH(k_contract_stats, dim3(C), dim3(256), 0, s, stats, stats_cs, n_waves, lik, gp, gp_cs, count,
-                 loss, tau_out);
+    const StatsJob J{stats, stats_cs, n_waves, lik, gp, gp_cs, count, loss, tau_out};
+    VIHMC_LAUNCH(k_contract_stats, dim3(C), dim3(256), 0, s, J);
 }
 
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
@@ -537,7 +542,7 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
         hipLaunchKernelGGL(k_gather_prior<false>, dim3(GATHER_SPLIT, C), dim3(256), 0, s, gp, gp_cs, smap, theta, K,
                            prior_mu, prior_inv_var, prior_scale, grad, lp_part, LeapArgs{});
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || logp == nullptr) return e;   // no log-prob wanted (inner leapfrog steps)
     static_assert(GATHER_SPLIT <= 64, "one lane per partial");
     VIHMC_LAUNCH(k_logp_finalize, dim3(C), dim3(64), 0, s, lp_part, GATHER_SPLIT, lik, prior_const, prior_scale,
                  logp);

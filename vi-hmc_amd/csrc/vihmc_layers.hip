@@ -105,13 +105,7 @@ __device__ __forceinline__ void rowdot_epilogue(const RowdotProb& P, int c, int 
 // under the activation math instead of stalling the MFMA stream. KF = 0 reads P.K and prefetches one
 // 16-wide k-block ahead.
 template <int NT, int MS, int MODE, int KF>
-__global__ __launch_bounds__(256, 3) void k_rowdot2(RowdotArgs args) {
-    extern __shared__ float bs[];
-    int b = blockIdx.x;
-    const int first = args.C * args.p[0].tiles;
-    const bool second = b >= first;
-    const RowdotProb P = second ? args.p[1] : args.p[0];
-    if (second) b -= first;
+__device__ __forceinline__ void rowdot_body(const RowdotProb& P, int b, float* bs) {
     const int c = b / P.tiles;
     const int grp = b - c * P.tiles;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
@@ -276,6 +270,36 @@ __global__ __launch_bounds__(256, 3) void k_rowdot2(RowdotArgs args) {
             }
             rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc);
         }
+    }
+}
+
+template <int NT, int MS, int MODE, int KF>
+__global__ __launch_bounds__(256, 3) void k_rowdot2(RowdotArgs args) {
+    extern __shared__ float bs[];
+    int b = blockIdx.x;
+    const int first = args.C * args.p[0].tiles;
+    const bool second = b >= first;
+    const RowdotProb P = second ? args.p[1] : args.p[0];
+    if (second) b -= first;
+    rowdot_body<NT, MS, MODE, KF>(P, b, bs);
+}
+
+// Input layers (round 2): the first problem (branch, K = 101 padded to KF0 = 104) takes the whole-tile
+// register preload of the KF path, the second (trunk, K = 5) the run-time-K path, instead of the run-time-K
+// body (26 serial 16-long k blocks with one dependent global load each) for both. Measured neutral on one
+// box: 37.1 vs 37.3 us per launch at C = 16 (profiles/r02_input/README.md) -- the branch workgroups do not
+// set this launch; VIHMC_ROWDOT_IN_KF=0 selects the run-time-K body. A VALU kernel for both input layers
+// (LDS-staged 4 x 4 register blocks for the branch, 4 outputs per thread for the trunk) measured 45-51 us
+// and was not kept (profiles/r02_input/input_layer_valu_experiment.patch).
+template <int NT, int MS, int KF0>
+__global__ __launch_bounds__(256, 3) void k_rowdot_in(RowdotArgs args) {
+    extern __shared__ float bs[];
+    int b = blockIdx.x;
+    const int first = args.C * args.p[0].tiles;
+    if (b >= first) {
+        rowdot_body<NT, MS, MODE_FWD, 0>(args.p[1], b - first, bs);
+    } else {
+        rowdot_body<NT, MS, MODE_FWD, KF0>(args.p[0], b, bs);
     }
 }
 
@@ -541,6 +565,15 @@ size_t rowdot_lds_bytes(const RowdotArgs& a) {
     return m;
 }
 
+// VIHMC_ROWDOT_IN_KF=0: the input layers through the run-time-K body for both nets (A/B timing)
+static bool rowdot_in_kf() {
+    static const bool on = [] {
+        const char* e = std::getenv("VIHMC_ROWDOT_IN_KF");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 template <int MS, int MODE>
 static hipError_t rowdot_nt(const RowdotArgs& a, int nt, hipStream_t s) {
     const int blocks = a.C * a.p[0].tiles + (a.nprob > 1 ? a.C * a.p[1].tiles : 0);
@@ -548,6 +581,11 @@ static hipError_t rowdot_nt(const RowdotArgs& a, int nt, hipStream_t s) {
     dim3 g(blocks), blk(256);
     const bool k100 = a.p[0].K == 100 && (a.nprob < 2 || a.p[1].K == 100);
     if (k100 && nt == 7) VIHMC_LAUNCH_L((k_rowdot2<7, MS, MODE, 100>), g, blk, shm, s, a);
+    // branch + trunk input layers of the Burgers DeepONet (K = 101 -> 104 padded columns, K <= 100 run time):
+    // the padded operand columns are zero (packed W rows, the uploaded input rows), so KF0 = 104 is exact
+    const bool kin = MODE == MODE_FWD && a.nprob == 2 && (a.p[0].K + 3) / 4 * 4 == 104 && a.p[0].lda >= 104 &&
+                     a.p[0].ldb >= 104 && a.p[1].K <= 100;
+    if (kin && nt == 7 && rowdot_in_kf()) VIHMC_LAUNCH_L((k_rowdot_in<7, MS, 104>), g, blk, shm, s, a);
     switch (nt) {
         case 1: VIHMC_LAUNCH_L((k_rowdot2<1, MS, MODE, 0>), g, blk, shm, s, a);
         case 2: VIHMC_LAUNCH_L((k_rowdot2<2, MS, MODE, 0>), g, blk, shm, s, a);

@@ -796,8 +796,13 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         HIPCHK(launch_contract(a, C, want_grad, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
     }
-    HIPCHK(launch_contract_stats(p->stats, p->stats_cs, stats_waves, C, p->lik_buf, p->gp, p->dp,
-                                 (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out, s));
+    // gradient evaluations: the statistics run as a slice of the weight-gradient reduce (nothing reads lik or
+    // gp slot 0 before the gather)
+    const StatsJob stats_job{p->stats, p->stats_cs, stats_waves, p->lik_buf, p->gp, p->dp,
+                             (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out};
+    if (!want_grad)
+        HIPCHK(launch_contract_stats(p->stats, p->stats_cs, stats_waves, C, p->lik_buf, p->gp, p->dp,
+                                     (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out, s));
     if (want_grad) {
         Net& b = p->nets[0];
         Net& t = p->nets[1];
@@ -892,7 +897,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
             }
         }
         if (bwd_stop) HIPCHK(hipEventRecord(bwd_stop, s));
-        HIPCHK(launch_reduce(p->jobsW, p->n_jobsW, p->max_lenW, C, s));
+        HIPCHK(launch_reduce(p->jobsW, p->n_jobsW, p->max_lenW, C, s, &stats_job));
     }
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
                                p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, s,
@@ -1131,7 +1136,9 @@ int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, con
         HIPCHK(launch_leap_open(theta_in, theta_out, p_in, p_out, g_in, eps, inv_mass, p->K, C, s));
         for (int st = 0; st < L; ++st) {
             LeapArgs lf{p_out, theta_out, eps, inv_mass, st == L - 1 ? 1 : 0};
-            if (int rc = deeponet_eval(p, theta_out, C, logp_out, g_out, nullptr, s, &lf)) return rc;
+            // only the end point's log-prob is returned: the intermediate evaluations skip k_logp_finalize
+            if (int rc = deeponet_eval(p, theta_out, C, st == L - 1 ? logp_out : nullptr, g_out, nullptr, s, &lf))
+                return rc;
         }
         return 0;
     });
