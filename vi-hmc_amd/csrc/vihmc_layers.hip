@@ -31,8 +31,20 @@ __device__ __forceinline__ float tanh_fast(float x) {
     return ax < 0.25f ? small : big;
 }
 
+#ifndef ROWDOT_TANH_CHEAP
+#define ROWDOT_TANH_CHEAP 1   // 0: tanh_fast above (Taylor / exp-rcp, ~17 VALU + 2 transcendental)
+#endif
+
+// (1 - t) / (1 + t), t = exp(-2|x|): the fused forward's form (vihmc_fused.hip tanh_f), 6 VALU + 2
+// transcendental, absolute error <= ~1.2e-7. The input layers' epilogue is the VALU bound of that launch (the
+// trunk's 16.3 M outputs at C = 16, profiles/r02_input/README.md).
+__device__ __forceinline__ float tanh_cheap(float x) {
+    const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(x));
+    return copysignf((1.f - t) * __builtin_amdgcn_rcpf(1.f + t), x);
+}
+
 __device__ __forceinline__ float act_apply_l(int act, float z) {
-    if (act == ACT_TANH) return tanh_fast(z);
+    if (act == ACT_TANH) return ROWDOT_TANH_CHEAP ? tanh_cheap(z) : tanh_fast(z);
     if (act == ACT_RELU) return fmaxf(z, 0.f);
     return z;
 }
