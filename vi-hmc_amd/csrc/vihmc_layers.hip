@@ -72,11 +72,50 @@ __host__ __device__ constexpr int rowdot_ldb(int k4) { return k4 + ((24 - (k4 & 
 // Epilogue of one row tile: bias + activation (FWD) or * act'(h) (BWD), float4 stores; columns in
 // [Nn, ldo) are written as zeros (padding read by the next GEMM). (A branch-free variant templated on
 // the activation measured ~10% slower on the hidden layers; see profiles/README.md.)
+// stg (forward only, ROWDOT_STAGE = 1): the wave's 16 x ldo LDS region. The transposed accumulators give each
+// store instruction 16 rows x 64 B, which leaves partial 128-B lines (PMC: 94.8 MB written per input-layer launch
+// for 71.7 MB of h_0); staged through LDS, the wave writes the 16-row block (contiguous in HBM) as 1-KB stores.
+// Measured slower and off by default: input layers 44.3 vs 35.6 us at C = 16 (the staging's 28 KB of LDS drops
+// the launch to 2 workgroups per CU; profiles/r02_input/README.md).
+#ifndef ROWDOT_STAGE
+#define ROWDOT_STAGE 0
+#endif
 template <int NT, int MS, int MODE>
 __device__ __forceinline__ void rowdot_epilogue(const RowdotProb& P, int c, int m0, int lr, int lg,
-                                                const f32x4 (&acc)[MS][NT]) {
+                                                const f32x4 (&acc)[MS][NT], float* stg = nullptr) {
     float* O = P.O + c * P.o_cs;
     const float* H = P.H + c * P.h_cs;
+    if (MODE == MODE_FWD && stg != nullptr) {
+        const int lane = lr + 16 * lg;
+#pragma unroll
+        for (int s = 0; s < MS; ++s) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int n = 16 * t + 4 * lg;
+                if (n >= P.ldo) continue;
+                // bias per tile (hoisting all NT float4 spilled at the 168-VGPR budget)
+                const float4 bv = P.bias ? *reinterpret_cast<const float4*>(P.bias + c * P.bias_cs + n)
+                                         : float4{0.f, 0.f, 0.f, 0.f};
+                float4 o;
+                o.x = n + 0 < P.Nn ? act_apply_l(P.act, acc[s][t][0] + bv.x) : 0.f;
+                o.y = n + 1 < P.Nn ? act_apply_l(P.act, acc[s][t][1] + bv.y) : 0.f;
+                o.z = n + 2 < P.Nn ? act_apply_l(P.act, acc[s][t][2] + bv.z) : 0.f;
+                o.w = n + 3 < P.Nn ? act_apply_l(P.act, acc[s][t][3] + bv.w) : 0.f;
+                *reinterpret_cast<float4*>(stg + lr * P.ldo + n) = o;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const int mb = m0 + 16 * s;
+            const int rows = min(16, P.M - mb);
+            if (rows > 0) {
+                const int nf4 = rows * (P.ldo >> 2);
+                float4* dst = reinterpret_cast<float4*>(O + (int64_t)mb * P.ldo);
+                const float4* src = reinterpret_cast<const float4*>(stg);
+                for (int e = lane; e < nf4; e += 64) dst[e] = src[e];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        return;
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const int n = 16 * t + 4 * lg;
@@ -126,6 +165,7 @@ __device__ __forceinline__ void rowdot_body(const RowdotProb& P, int b, float* b
     const int KK = KF > 0 ? KF : P.K;
     const int K4 = (KK + 3) & ~3;
     const int LDB = rowdot_ldb(K4);
+    float* stg = (MODE == MODE_FWD && ROWDOT_STAGE) ? bs + P.Nn * LDB + wave * 16 * P.ldo : nullptr;
 
     // stage B (rows n < Nn, K4 floats each; global row stride ldb >= K4, zero padded)
     {
@@ -216,7 +256,7 @@ __device__ __forceinline__ void rowdot_body(const RowdotProb& P, int b, float* b
             // first half of the next tile's A goes out before the epilogue (hidden under it), the rest
             // after it (register budget: 3 waves/SIMD = 168 VGPRs)
             if (tile + 1 < tile_end) VIHMC_RD_LOAD_A(tile + 1, 0, NKB / 2, false)
-            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc);
+            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc, stg);
             if (tile + 1 < tile_end) VIHMC_RD_LOAD_A(tile + 1, NKB / 2, NKB, true)
         }
 #undef VIHMC_RD_LOAD_A
@@ -280,7 +320,7 @@ __device__ __forceinline__ void rowdot_body(const RowdotProb& P, int b, float* b
 #pragma unroll
                     for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t], a[s], acc[s][t]);
             }
-            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc);
+            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc, stg);
         }
     }
 }
@@ -569,10 +609,12 @@ __global__ __launch_bounds__(BWD_THREADS, 4) void k_bwd_ws(BwdArgs args) {
     do { hipLaunchKernelGGL(kern, grid, block, shm, s, __VA_ARGS__); return hipGetLastError(); } while (0)
 
 size_t rowdot_lds_bytes(const RowdotArgs& a) {
+    // B image [Nn][ldb] + (forward, ROWDOT_STAGE) one 16 x ldo output block per wave
     size_t m = 0;
     for (int i = 0; i < a.nprob; ++i) {
         const int k4 = (a.p[i].K + 3) & ~3;
-        m = std::max(m, sizeof(float) * (size_t)a.p[i].Nn * rowdot_ldb(k4));
+        m = std::max(m, sizeof(float) * ((size_t)a.p[i].Nn * rowdot_ldb(k4) +
+                                         (ROWDOT_STAGE ? (size_t)ROWDOT_WAVES * 16 * a.p[i].ldo : 0)));
     }
     return m;
 }
