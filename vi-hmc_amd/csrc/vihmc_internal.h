@@ -39,6 +39,7 @@ struct RowdotProb {
 struct RowdotArgs {
     RowdotProb p[2];
     int32_t nprob, C;
+    int32_t ms0;            // row sub-tiles per wave of problem 0 when it differs from the launch's (input layers)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -108,6 +109,9 @@ struct ContractProb {
 
 // launchers (vihmc_kernels.hip)
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s);
+// The grouped input-layer launch (branch K = 101 on the whole-tile KF = 104 path, trunk run-time K) applies:
+// problem 0 may then use its own row sub-tiles per wave (RowdotArgs::ms0).
+bool rowdot_in_ok(const RowdotArgs& a, int nt);
 hipError_t launch_contract(const ContractProb& p, int C, bool with_grad, hipStream_t s);
 hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s);
 hipError_t launch_contract_bf_b(const ContractProb& p, int C, hipStream_t s);
@@ -196,12 +200,13 @@ int fwd_img_bias_off(int n);
 int fwd_img_tail_off(int n, int col);
 bool fwd_fused_bf_needs_wimg();                     // the bf16x6 forward reads the fp32 k tail of the image
 int fwd_fused_bf_waves();                           // its waves per workgroup (16 rows each)
-// Nonzero when a translation unit was built with a timing-only ablation (FWD_ABL, CB_ABL, BB_ABL: wrong
+// Nonzero when a translation unit was built with a timing-only ablation (FWD_ABL, CB_ABL, BB_ABL, RD_ONLY_FIRST: wrong
 // results) or phase-stamp instrumentation (CB_STAMP, BB_STAMP). vihmc_version() reports them and plan
 // creation refuses such a library unless VIHMC_ALLOW_DIAG=1 (the A/B scripts' variant builds).
 int diag_switches_fused();
 int diag_switches_contract_bf();
 int diag_switches_bwd_bf();
+int diag_switches_layers();
 int diag_switches();
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, int nw, hipStream_t s);     // bf16x6, 12 (or 4) waves

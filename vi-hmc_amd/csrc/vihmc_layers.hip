@@ -343,7 +343,8 @@ __global__ __launch_bounds__(256, 3) void k_rowdot2(RowdotArgs args) {
 // set this launch; VIHMC_ROWDOT_IN_KF=0 selects the run-time-K body. A VALU kernel for both input layers
 // (LDS-staged 4 x 4 register blocks for the branch, 4 outputs per thread for the trunk) measured 45-51 us
 // and was not kept (profiles/r02_input/input_layer_valu_experiment.patch).
-template <int NT, int MS, int KF0>
+// MS0: row sub-tiles per wave of the branch (1: twice the workgroups of MS = 2 for its 16,000 rows at C = 16).
+template <int NT, int MS, int KF0, int MS0>
 __global__ __launch_bounds__(256, 3) void k_rowdot_in(RowdotArgs args) {
     extern __shared__ float bs[];
     int b = blockIdx.x;
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(256, 3) void k_rowdot_in(RowdotArgs args) {
     if (b >= first) {
         rowdot_body<NT, MS, MODE_FWD, 0>(args.p[1], b - first, bs);
     } else {
-        rowdot_body<NT, MS, MODE_FWD, KF0>(args.p[0], b, bs);
+        rowdot_body<NT, MS0, MODE_FWD, KF0>(args.p[0], b, bs);
     }
 }
 
@@ -628,18 +629,31 @@ static bool rowdot_in_kf() {
     return on;
 }
 
+#ifndef RD_ONLY_FIRST
+#define RD_ONLY_FIRST 0   // timing-only (wrong results): 1 = grouped row-dot launches run the first problem's
+                          // workgroups only (the branch part of the input layers)
+#endif
+int diag_switches_layers() { return RD_ONLY_FIRST; }
+
+// branch + trunk input layers of the Burgers DeepONet (K = 101 -> 104 padded columns, K <= 100 run time): the
+// padded operand columns are zero (packed W rows, the uploaded input rows), so KF0 = 104 is exact
+bool rowdot_in_ok(const RowdotArgs& a, int nt) {
+    return rowdot_in_kf() && nt == 7 && a.nprob == 2 && (a.p[0].K + 3) / 4 * 4 == 104 && a.p[0].lda >= 104 &&
+           a.p[0].ldb >= 104 && a.p[1].K <= 100;
+}
+
 template <int MS, int MODE>
 static hipError_t rowdot_nt(const RowdotArgs& a, int nt, hipStream_t s) {
-    const int blocks = a.C * a.p[0].tiles + (a.nprob > 1 ? a.C * a.p[1].tiles : 0);
+    const int blocks = a.C * a.p[0].tiles + (a.nprob > 1 && !RD_ONLY_FIRST ? a.C * a.p[1].tiles : 0);
     const size_t shm = rowdot_lds_bytes(a);
     dim3 g(blocks), blk(256);
     const bool k100 = a.p[0].K == 100 && (a.nprob < 2 || a.p[1].K == 100);
     if (k100 && nt == 7) VIHMC_LAUNCH_L((k_rowdot2<7, MS, MODE, 100>), g, blk, shm, s, a);
-    // branch + trunk input layers of the Burgers DeepONet (K = 101 -> 104 padded columns, K <= 100 run time):
-    // the padded operand columns are zero (packed W rows, the uploaded input rows), so KF0 = 104 is exact
-    const bool kin = MODE == MODE_FWD && a.nprob == 2 && (a.p[0].K + 3) / 4 * 4 == 104 && a.p[0].lda >= 104 &&
-                     a.p[0].ldb >= 104 && a.p[1].K <= 100;
-    if (kin && nt == 7 && rowdot_in_kf()) VIHMC_LAUNCH_L((k_rowdot_in<7, MS, 104>), g, blk, shm, s, a);
+    if (MODE == MODE_FWD && rowdot_in_ok(a, nt)) {
+        if (a.ms0 == 1) VIHMC_LAUNCH_L((k_rowdot_in<7, MS, 104, 1>), g, blk, shm, s, a);
+        VIHMC_LAUNCH_L((k_rowdot_in<7, MS, 104, MS>), g, blk, shm, s, a);
+    }
+    if (a.ms0 != 0 && a.ms0 != MS) return hipErrorInvalidValue;
     switch (nt) {
         case 1: VIHMC_LAUNCH_L((k_rowdot2<1, MS, MODE, 0>), g, blk, shm, s, a);
         case 2: VIHMC_LAUNCH_L((k_rowdot2<2, MS, MODE, 0>), g, blk, shm, s, a);

@@ -209,7 +209,9 @@ struct vihmc_plan {
 };
 
 namespace vihmc {
-int diag_switches() { return diag_switches_fused() | diag_switches_contract_bf() | diag_switches_bwd_bf(); }
+int diag_switches() {
+    return diag_switches_fused() | diag_switches_contract_bf() | diag_switches_bwd_bf() | diag_switches_layers();
+}
 }  // namespace vihmc
 
 namespace {
@@ -657,6 +659,16 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
     return 0;
 }
 
+// VIHMC_ROWDOT_IN_MS1=1: the branch input layer at 16 rows per wave (twice the workgroups) instead of the launch's
+// 32. Measured slower, off by default: 39.1 vs 36.0 us per input-layer launch at C = 16 (profiles/r02_input/)
+static bool rowdot_in_ms1() {
+    static const bool on = [] {
+        const char* e = std::getenv("VIHMC_ROWDOT_IN_MS1");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 // Forward through both MLPs (grouped launches: branch + trunk layer j together); the hidden 100 -> 100
 // stack goes through the fused kernel when its shape allows.
 int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img) {
@@ -712,6 +724,13 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img) {
             nt = std::max(nt, nt_of(L.n_out));
         }
         if (a.nprob == 1) a.p[1] = a.p[0];
+        // input layers: the branch (one tile per workgroup) at 16 rows per wave when the launch runs 32
+        if (j == 0 && ms == 2 && rowdot_in_ms1() && rowdot_in_ok(a, nt)) {
+            RowdotProb& q = a.p[0];
+            q.ntiles = cdiv(q.M, ROWDOT_WAVES * 16);
+            q.tiles = cdiv(q.ntiles, q.tpw);
+            a.ms0 = 1;
+        }
         HIPCHK(launch_rowdot(a, nt, ms, MODE_FWD, s));
     }
     return 0;
@@ -1390,7 +1409,8 @@ const char* vihmc_last_error(void) { return g_err.c_str(); }
 const char* vihmc_version(void) {
     static std::string v = "vihmc 0.2.0 gfx950 diag=" + std::to_string(vihmc::diag_switches_fused()) + "," +
                            std::to_string(vihmc::diag_switches_contract_bf()) + "," +
-                           std::to_string(vihmc::diag_switches_bwd_bf());
+                           std::to_string(vihmc::diag_switches_bwd_bf()) + "," +
+                           std::to_string(vihmc::diag_switches_layers());
     return v.c_str();
 }
 
