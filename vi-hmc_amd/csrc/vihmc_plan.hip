@@ -107,7 +107,7 @@ struct vihmc_plan {
     int qchunksA = 1, qperA = 32;          // side A splits its q range only for small chain counts
     float* partA = nullptr;
     int64_t partA_cs = 0;
-    ReduceJob* jobsA = nullptr;
+    ReduceJob* jobsA = nullptr;            // (qchunksA > 1) the side-B and side-A reduce jobs, one launch
     int lenA = 0;
     double* stats = nullptr;
     int64_t stats_cs = 0;
@@ -524,7 +524,9 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             ja.dst = p->nets[1].delta[0];
             ja.dst_cs = p->nets[1].delta_cs;
             p->lenA = ja.len;
-            if (int rc = p->upload(&p->jobsA, &ja, 1)) return rc;
+            // both contraction reduces in one launch (independent outputs: branch and trunk deltas)
+            const ReduceJob both[2] = {jb, ja};
+            if (int rc = p->upload(&p->jobsA, both, 2)) return rc;
         }
         std::vector<ReduceJob> jw;
         for (int net = 0; net < 2; ++net) {
@@ -863,8 +865,8 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         if (int rc = p->timing_begin(VIHMC_T_CONTRACT_B, s, &stop)) return rc;
         HIPCHK(launch_contract(q, C, true, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
-        HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s));
-        if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 1, p->lenA, C, s));
+        if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 2, std::max(p->lenA, p->lenB), C, s));
+        else HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s));
 
         // backward through both MLPs, last layer first: one fused launch per layer (branch + trunk
         // grouped) computes delta_{l-1} and the dW / db partial slabs
