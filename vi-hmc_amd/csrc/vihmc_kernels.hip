@@ -126,6 +126,10 @@ __device__ void contract_stats_body(const StatsJob& J, int c) {
 
 __global__ __launch_bounds__(256) void k_contract_stats(StatsJob J) { contract_stats_body(J, blockIdx.x); }
 
+#ifndef REDUCE_GROUP_MIN
+#define REDUCE_GROUP_MIN 32   // slab count from which a block's four waves split the slabs (see k_reduce)
+#endif
+
 // Fixed-order sum of partial slabs (p = 0, 1, ... sequentially -- bitwise reproducible); grid slice y = n_jobs
 // (when present) runs the likelihood statistics instead (saves their launch after side A); 4 consecutive
 // elements per thread as float4 when the job's strides allow, 8 slab loads in flight ahead of the adds.
@@ -138,6 +142,54 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
     const int c = blockIdx.z;
     const bool vec = ((J.len | J.part_stride | J.in_cs | J.dst_cs) & 3) == 0 &&
                      ((reinterpret_cast<uintptr_t>(J.src) | reinterpret_cast<uintptr_t>(J.dst)) & 15) == 0;
+    if (vec && J.n_parts >= REDUCE_GROUP_MIN) {
+        // many slabs (the weight-gradient partials of a one-chain plan: ~160 row chunks per trunk layer): the block's
+        // four waves split the slabs (wave g sums p = g, g + 4, ... in order), then wave 0 adds the three other
+        // waves' sums in order -- still a fixed order; one thread walking 160 slabs was latency-bound (17.7 us for
+        // 60 MB at C = 1). Block-uniform branch (J and vec are per block), so the barrier is safe.
+        __shared__ float4 gsum[3][64];
+        if ((int)blockIdx.x * 256 >= J.len) return;   // whole block past this job (the grid fits the longest job)
+        const int x = threadIdx.x & 63, g = threadIdx.x >> 6;
+        const int eg = (blockIdx.x * 64 + x) * 4;
+        const bool ok = eg < J.len;
+        const float* sp = J.src + c * J.in_cs + (ok ? eg : 0);
+        const int64_t st = J.part_stride;
+        const int n = ok ? J.n_parts : 0;               // lanes past the end load nothing
+        float4 s = {0.f, 0.f, 0.f, 0.f};
+        int p = g;
+        for (; p + 28 < n; p += 32) {
+            float4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(sp + (p + 4 * u) * st);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                s.x += v[u].x;
+                s.y += v[u].y;
+                s.z += v[u].z;
+                s.w += v[u].w;
+            }
+        }
+        for (; p < n; p += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(sp + p * st);
+            s.x += v.x;
+            s.y += v.y;
+            s.z += v.z;
+            s.w += v.w;
+        }
+        if (g > 0) gsum[g - 1][x] = s;
+        __syncthreads();
+        if (g == 0 && ok) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                s.x += gsum[q][x].x;
+                s.y += gsum[q][x].y;
+                s.z += gsum[q][x].z;
+                s.w += gsum[q][x].w;
+            }
+            *reinterpret_cast<float4*>(J.dst + c * J.dst_cs + eg) = s;
+        }
+        return;
+    }
     const int e = (blockIdx.x * blockDim.x + threadIdx.x) * (vec ? 4 : 1);
     if (e >= J.len) return;
     const float* src = J.src + c * J.in_cs + e;
