@@ -150,12 +150,20 @@ hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_wa
 // every product and sum rounded separately: p += eps g; then on the last step p -= (eps / 2) g, otherwise
 // theta += eps p (eps inv_mass p with a diagonal mass). p and theta are updated in place (theta is the
 // evaluation's own input, read by the same thread first).
+// The scatter of a new position into the plan's packed weights (+ kept weight images), done by the kernel that
+// computes that position (the gradient gather of the previous leapfrog step, or the trajectory's opening kernel)
+// instead of a k_scatter launch at the head of the next evaluation. packed == null: none.
+struct ScatterArgs {
+    float* packed; int64_t dp; const int32_t* smap_w; const int32_t* smap_wt; ScatterImg si;
+};
 struct LeapArgs {
     float* p;               // [C, K]
     float* th;              // [C, K]
     const float* eps;       // [C]
     const float* inv_mass;  // [K] or null
     int32_t last;
+    ScatterArgs sc;         // scatter the new theta (not on the last step); packed == null: the next evaluation does
+    int32_t scattered_in;   // this evaluation's theta is already scattered (skip its k_scatter)
 };
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
                                const float* prior_mu, const float* prior_inv_var, double prior_const,
@@ -164,7 +172,8 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
 // the opening half step and first position step of a trajectory: p_out = p_in + (eps / 2) g_in,
 // th_out = th_in + eps p_out (eps inv_mass p_out)
 hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out, const float* g_in,
-                            const float* eps, const float* inv_mass, int K, int C, hipStream_t s);
+                            const float* eps, const float* inv_mass, int K, int C, hipStream_t s,
+                            const ScatterArgs* sc = nullptr);
 
 // Fused hidden-layer forward (width 100 -> 100 layers of both nets, one launch): every wave keeps 16 rows
 // of activations in registers through all fused layers; per layer the weights + bias of the next layer

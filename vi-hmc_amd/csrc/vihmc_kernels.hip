@@ -61,31 +61,35 @@ __global__ void k_init_packed(float* packed, int64_t dp, const float* frozen, co
     }
 }
 
+// sampled value k of chain c -> packed W, W^T and (when kept by the scatter) the forward's weight images
+__device__ __forceinline__ void scatter_one(float* packed, int64_t dp, const int32_t* smap_w, const int32_t* smap_wt,
+                                            const ScatterImg& si, int c, int k, float v) {
+    packed[c * dp + smap_w[k]] = v;
+    const int32_t t = smap_wt[k];
+    if (t >= 0) packed[c * dp + t] = v;
+    if (si.img_w != nullptr) {
+        unsigned char* img = si.img + c * si.img_cs;
+        const int32_t o = si.img_w[k];
+        if (o >= 0) {
+            // the three planes exactly as k_split_wimg splits them
+            const __bf16 a = (__bf16)v;
+            const float r = v - (float)a;
+            const __bf16 b = (__bf16)r;
+            const __bf16 cc = (__bf16)(r - (float)b);
+            *reinterpret_cast<__bf16*>(img + o) = a;
+            *reinterpret_cast<__bf16*>(img + o + si.plane) = b;
+            *reinterpret_cast<__bf16*>(img + o + 2 * si.plane) = cc;
+        }
+        const int32_t f = si.img_f[k];
+        if (f >= 0) *reinterpret_cast<float*>(img + f) = v;
+    }
+}
+
 __global__ void k_scatter(float* packed, int64_t dp, const float* theta, int K, const int32_t* smap_w,
                           const int32_t* smap_wt, ScatterImg si) {
     const int c = blockIdx.y;
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
-        const float v = theta[(int64_t)c * K + k];
-        packed[c * dp + smap_w[k]] = v;
-        const int32_t t = smap_wt[k];
-        if (t >= 0) packed[c * dp + t] = v;
-        if (si.img_w != nullptr) {
-            unsigned char* img = si.img + c * si.img_cs;
-            const int32_t o = si.img_w[k];
-            if (o >= 0) {
-                // the three planes exactly as k_split_wimg splits them
-                const __bf16 a = (__bf16)v;
-                const float r = v - (float)a;
-                const __bf16 b = (__bf16)r;
-                const __bf16 cc = (__bf16)(r - (float)b);
-                *reinterpret_cast<__bf16*>(img + o) = a;
-                *reinterpret_cast<__bf16*>(img + o + si.plane) = b;
-                *reinterpret_cast<__bf16*>(img + o + 2 * si.plane) = cc;
-            }
-            const int32_t f = si.img_f[k];
-            if (f >= 0) *reinterpret_cast<float*>(img + f) = v;
-        }
-    }
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x)
+        scatter_one(packed, dp, smap_w, smap_wt, si, c, k, theta[(int64_t)c * K + k]);
 }
 
 __device__ double block_sum_256(double v, double* sh) {
@@ -268,7 +272,9 @@ __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t g
                 pn = pn - (0.5f * e) * g;
             } else {
                 const float step = lf.inv_mass ? (e * lf.inv_mass[k]) * pn : e * pn;
-                lf.th[o] = th + step;
+                const float tn = th + step;
+                lf.th[o] = tn;
+                if (lf.sc.packed) scatter_one(lf.sc.packed, lf.sc.dp, lf.sc.smap_w, lf.sc.smap_wt, lf.sc.si, c, k, tn);
             }
             lf.p[o] = pn;
         }
@@ -278,7 +284,8 @@ __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t g
 }
 
 __global__ __launch_bounds__(256) void k_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out,
-                                                   const float* g_in, const float* eps, const float* inv_mass, int K) {
+                                                   const float* g_in, const float* eps, const float* inv_mass, int K,
+                                                   ScatterArgs sc) {
 #pragma clang fp contract(off)
     const int c = blockIdx.y;
     const float e = eps[c], he = 0.5f * e;
@@ -287,7 +294,9 @@ __global__ __launch_bounds__(256) void k_leap_open(const float* th_in, float* th
         const float pn = p_in[o] + he * g_in[o];
         const float step = inv_mass ? (e * inv_mass[k]) * pn : e * pn;
         p_out[o] = pn;
-        th_out[o] = th_in[o] + step;
+        const float tn = th_in[o] + step;
+        th_out[o] = tn;
+        if (sc.packed) scatter_one(sc.packed, sc.dp, sc.smap_w, sc.smap_wt, sc.si, c, k, tn);
     }
 }
 
@@ -601,9 +610,9 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
 }
 
 hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out, const float* g_in,
-                            const float* eps, const float* inv_mass, int K, int C, hipStream_t s) {
+                            const float* eps, const float* inv_mass, int K, int C, hipStream_t s, const ScatterArgs* sc) {
     VIHMC_LAUNCH(k_leap_open, dim3((K + 1023) / 1024, C), dim3(256), 0, s, th_in, th_out, p_in, p_out, g_in, eps,
-                 inv_mass, K);
+                 inv_mass, K, sc ? *sc : ScatterArgs{});
 }
 
 // the plan's layers are exactly MlpBnn's widths (then the compile-time form runs); VIHMC_MLP_FIX=0: never

@@ -661,6 +661,15 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
     return 0;
 }
 
+// VIHMC_FUSE_SCATTER=0: trajectory evaluations run their own k_scatter (A/B timing)
+static bool fuse_scatter() {
+    static const bool on = [] {
+        const char* e = std::getenv("VIHMC_FUSE_SCATTER");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 // VIHMC_ROWDOT_IN_MS1=1: the branch input layer at 16 rows per wave (twice the workgroups) instead of the launch's
 // 32. Measured slower, off by default: 39.1 vs 36.0 us per input-layer launch at C = 16 (profiles/r02_input/)
 static bool rowdot_in_ms1() {
@@ -800,7 +809,8 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
 int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
                        hipStream_t s, const LeapArgs* leap) {
     const ScatterImg si = scatter_img(p);
-    HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s, p->img_by_scatter ? &si : nullptr));
+    if (!(leap && leap->scattered_in))
+        HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s, p->img_by_scatter ? &si : nullptr));
     const bool want_grad = grad != nullptr && out == nullptr;
     // the pre-split contraction images (bf16x6 sides, gradient evaluations) are written by the fused forward
     // when it runs; otherwise k_split_blocks makes them below
@@ -1154,9 +1164,16 @@ int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, con
         hipStream_t s = static_cast<hipStream_t>(stream);
         // opening half step + first position step, then L evaluations whose gradient gather applies the
         // momentum step and the next position step in place (theta_out / p_out are the running state)
-        HIPCHK(launch_leap_open(theta_in, theta_out, p_in, p_out, g_in, eps, inv_mass, p->K, C, s));
+        // every new position is scattered into the packed weights / images by the kernel that computes it (the opening
+        // kernel, then each step's gradient gather), so the evaluations skip their k_scatter (VIHMC_FUSE_SCATTER=0:
+        // the evaluations scatter as usual)
+        const bool fuse = fuse_scatter();
+        const ScatterImg si = scatter_img(p);
+        const ScatterArgs sc{p->packed, p->dp, p->smap_w, p->smap_wt, p->img_by_scatter ? si : ScatterImg{}};
+        HIPCHK(launch_leap_open(theta_in, theta_out, p_in, p_out, g_in, eps, inv_mass, p->K, C, s, fuse ? &sc : nullptr));
         for (int st = 0; st < L; ++st) {
-            LeapArgs lf{p_out, theta_out, eps, inv_mass, st == L - 1 ? 1 : 0};
+            LeapArgs lf{p_out, theta_out, eps, inv_mass, st == L - 1 ? 1 : 0, fuse && st < L - 1 ? sc : ScatterArgs{},
+                        fuse ? 1 : 0};
             // only the end point's log-prob is returned: the intermediate evaluations skip k_logp_finalize
             if (int rc = deeponet_eval(p, theta_out, C, st == L - 1 ? logp_out : nullptr, g_out, nullptr, s, &lf))
                 return rc;
