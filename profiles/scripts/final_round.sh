@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r02bt_gpu_tests.txt 2>&1 && \
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r02bt_smoke.txt 2>&1 && \
-bash profiles/round_profile.sh r02bt
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r02bv_gpu_tests.txt 2>&1 && \
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r02bv_smoke.txt 2>&1 && \
+bash profiles/round_profile.sh r02bv
