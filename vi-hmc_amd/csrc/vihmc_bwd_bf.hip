@@ -588,6 +588,10 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         const unsigned char* wrow1 = smw + BB_W + min(16 * (t0 + 1) + lr, P.n_in - 1) * BB_WPITCH + 16 * lg;
         const float* wtl = reinterpret_cast<const float*>(smw + BB_WT);
         const int wr0 = min(16 * t0 + lr, P.n_in - 1), wr1 = min(16 * (t0 + 1) + lr, P.n_in - 1);
+#ifndef B2_HGLOBAL
+#define B2_HGLOBAL 0    // 1: the dX epilogue's h as fp32 global loads (L2) issued at the sub-tile head, instead of three
+                        // LDS plane reads + reconstruction (same values: the split is exact)
+#endif
 #ifndef B2_DEFER
 #define B2_DEFER 0      // 1: the dX epilogue of sub-tile i runs after sub-tile i+1's MFMAs are issued (branch-free, in
                         // their basic block, so its VALU fills their issue gaps); 0: right after its own MFMAs
@@ -606,6 +610,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             // store offsets (OOB: nothing pending / not this workgroup's row / past NI4)
             f32x4 accp[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
             bf16x4 hq[2][3] = {};
+            f32x4 hgp[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
             uint32_t offp[2] = {bf6::OOB, bf6::OOB};
             auto epilogue = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -614,7 +619,8 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                     f32x4 o;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float hv = ((float)hq[u][2][r] + (float)hq[u][1][r]) + (float)hq[u][0][r];
+                        const float hv = B2_HGLOBAL ? hgp[u][r]
+                                                    : ((float)hq[u][2][r] + (float)hq[u][1][r]) + (float)hq[u][0][r];
                         const float gd = TANH ? 1.f - hv * hv : act_grad_bf(P.act, hv);
                         o[r] = (col + r < P.n_in) ? accp[u][r] * gd : 0.f;
                     }
@@ -626,6 +632,19 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 __syncthreads();
                 VIHMC_BB_STAMP(i, 0)
                 if (!P.has_dx) continue;
+#if B2_HGLOBAL
+                // act'(h) operands as fp32 straight from H (the rows the staging waves just read: L2 hits), issued
+                // before this sub-tile's MFMAs: no plane reads / reconstruction VALU in the epilogue
+                f32x4 hgv[2];
+                {
+                    const int mm = min(sub + 16 * h + lr, P.M - 1);
+#pragma unroll
+                    for (int u = 0; u < NU; ++u) {
+                        const int col = min(16 * (t0 + u) + 4 * lg, NI4 - 4);
+                        hgv[u] = *reinterpret_cast<const f32x4*>(H + (int64_t)mm * P.ldh + col);
+                    }
+                }
+#endif
                 if (i == 0) {
 #pragma unroll
                     for (int kb = 0; kb < 3; ++kb)
@@ -667,8 +686,12 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
                     const int col = 16 * (t0 + u) + 4 * lg;
+#if B2_HGLOBAL
+                    hgp[u] = hgv[u];
+#else
 #pragma unroll
                     for (int p = 0; p < 3; ++p) hq[u][p] = *reinterpret_cast<const bf16x4*>(hrow + p * BB_PLANE + 2 * col);
+#endif
                     offp[u] = (m < r1 && col < NI4) ? (uint32_t)(m * P.ldh + col) * 4u : bf6::OOB;
                     accp[u] = acc[u];
                 }
