@@ -311,6 +311,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from vihmc.data import deeponet_problem
+    from vihmc.dist import gather_ragged_pool, max_over_ranks
     from vihmc.engine import DeepONetEngine, trunk_features
     from vihmc.layout import DeepONetSpec
     from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner
@@ -354,18 +355,14 @@ def main():
     k_ms, k_n = eng.timing_class(dom_cls)
     eng.timing(-1, False)
     grad_evals = ev.n_grad
-    T = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(T, op=dist.ReduceOp.MAX)
-    T = float(T.item())
+    T = max_over_ranks(t1 - t0, dev)
 
     extra = {}
     if args.gather and world > 1:
-        local_pool = runner.samples[:, :int(runner.counts.min())].contiguous()
-        pool = torch.empty((world,) + tuple(local_pool.shape), device=dev)
+        # ragged-safe: a chain that hit a LogProbError stores fewer samples, so ranks may differ in length
         torch.cuda.synchronize()
         g0 = time.perf_counter()
-        dist.all_gather_into_tensor(pool, local_pool)
+        pool, _ = gather_ragged_pool(runner.samples, runner.counts)
         torch.cuda.synchronize()
         extra["allgather_ms"] = (time.perf_counter() - g0) * 1e3
         extra["allgather_bytes"] = pool.numel() * 4

@@ -64,3 +64,76 @@ def test_gloo_world2_pool_equals_single_process(tmp_path, total):
     ref = _sample(range(total))
     assert torch.equal(got["pool"], ref.stacked())
     assert float(got["acc"][0]) == float(ref.accepted.sum())
+
+
+class _NaNAt:
+    """Wraps a CPU evaluator: chain 0's log-prob is NaN on gradient call number ``at`` (a LogProbError: the
+    sampler rejects without storing, so that chain ends with fewer stored samples than the others)."""
+
+    def __init__(self, ev, at):
+        self.ev, self.at, self.calls = ev, at, 0
+        self.device, self.K = ev.device, ev.K
+
+    def logp_grad(self, theta):
+        lp, g = self.ev.logp_grad(theta)
+        self.calls += 1
+        if self.calls == self.at:
+            lp = lp.clone()
+            lp[0] = float("nan")
+        return lp, g
+
+    def logp(self, theta):
+        return self.ev.logp(theta)
+
+
+def _bench_worker(rank, ws, port, out_path):
+    """bench.py's multi-rank tail on gloo: per-rank runner, ragged pool all-gather, max-over-ranks wall."""
+    import sys
+    import time
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(here, ".."), os.path.join(here, "..", "vi-hmc_amd")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    from test_sampler import bnn_fn
+    from vihmc import samplers as S
+    from vihmc.dist import gather_ragged_pool, max_over_ranks
+    fn, th0, _ = bnn_fn()
+    chains = chain_block(5, rank, ws)
+    C = len(chains)
+    ev = S.AutogradEvaluator(fn, th0.numel(), "cpu")
+    if rank == 1:
+        ev = _NaNAt(ev, at=9)                          # rank 1, its first chain: one LogProbError mid-run
+    runner = S.HMCRunner(ev, th0[None].repeat(C, 1), 8, 4, 5e-4, burn=0,
+                         rng=S.ChainRNG(C, th0.numel(), "cpu", seeds=chain_seeds(chains)), strict_rng=True)
+    t0 = time.perf_counter()
+    for _ in range(8):
+        runner.step()
+    wall = time.perf_counter() - t0 + (0.25 if rank == 1 else 0.0)
+    T = max_over_ranks(wall, "cpu")
+    pool, counts = gather_ragged_pool(runner.samples, runner.counts)
+    local = [runner.samples[i, :int(runner.counts[i])].clone() for i in range(C)]
+    torch.save({"pool": pool, "counts": counts, "local": local, "T": T, "wall": wall},
+               out_path + f".{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_pool_with_logprob_error(tmp_path):
+    out = str(tmp_path / "bench")
+    mp.start_processes(_bench_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    r0 = torch.load(out + ".0", weights_only=True)
+    r1 = torch.load(out + ".1", weights_only=True)
+    # the job's time is the slowest rank's, on every rank
+    assert r0["T"] == r1["T"] == max(r0["wall"], r1["wall"])
+    # ragged: rank 1's first chain (job chain 3) stored one sample fewer than the rest
+    counts = r0["counts"].tolist()
+    assert counts == r1["counts"].tolist() and len(counts) == 5
+    assert counts[3] == counts[0] - 1 and len({counts[i] for i in (0, 1, 2, 4)}) == 1
+    assert torch.equal(r0["pool"], r1["pool"])
+    local = r0["local"] + r1["local"]
+    for c in range(5):
+        n = counts[c]
+        assert torch.equal(r0["pool"][c, :n], local[c])
+        assert not r0["pool"][c, n:].any()                # padding

@@ -109,9 +109,9 @@ def test_bf16x6_paths_match_fp32_mfma_paths(cuda_device):
     assert dg.max() < 2e-5
 
 
-def test_forward_without_weight_images_matches(cuda_device, monkeypatch):
-    """VIHMC_FWD_WIMG=0 at plan creation: the hidden layers run the fp32-MFMA fused forward (the bf16x6 one
-    needs the pre-split images for its f32 k tail) -- same evaluation to fp32-level agreement."""
+def test_forward_without_weight_images_matches(cuda_device):
+    """Plan option fwd_wimg = 0: the hidden layers run the fp32-MFMA fused forward (the bf16x6 one needs the
+    pre-split images for its f32 k tail) -- same evaluation to fp32-level agreement."""
     c = deeponet_case("deeponet_burgers")
     rng = np.random.default_rng(11)
     C = 4
@@ -119,9 +119,9 @@ def test_forward_without_weight_images_matches(cuda_device, monkeypatch):
     th = torch.tensor(np.stack([base + 0.01 * rng.standard_normal(base.size).astype(np.float32) for _ in range(C)]),
                       device=cuda_device)
     res = []
-    for env in ("1", "0"):
-        monkeypatch.setenv("VIHMC_FWD_WIMG", env)
+    for on in (1, 0):
         eng = engine_for(c, max_chains=C)
+        eng.option("fwd_wimg", on)
         lp, g = eng.logp_grad(th)
         res.append((lp.double().cpu().numpy(), g.double().cpu().numpy()))
         eng.close()
@@ -130,9 +130,9 @@ def test_forward_without_weight_images_matches(cuda_device, monkeypatch):
     assert dlp.max() < 2e-6 and dg.max() < 2e-5, (dlp.max(), dg.max())
 
 
-def test_weight_images_kept_by_scatter_bitwise(cuda_device, monkeypatch):
+def test_weight_images_kept_by_scatter_bitwise(cuda_device):
     """Weight images split once per plan and kept current by the scatter (default) == split from the packed weights
-    every evaluation (VIHMC_IMG_SCATTER=0), bit for bit, over a sequence of different thetas per chain and across a
+    every evaluation (plan option img_scatter = 0), bit for bit, over a sequence of different thetas per chain and across a
     single-chain sensitivity call (which scatters chain 0 too)."""
     c = deeponet_case("deeponet_burgers")
     rng = np.random.default_rng(5)
@@ -141,9 +141,10 @@ def test_weight_images_kept_by_scatter_bitwise(cuda_device, monkeypatch):
     seq = [torch.tensor(np.stack([base + 0.01 * rng.standard_normal(base.size).astype(np.float32) for _ in range(C)]),
                         device=cuda_device) for _ in range(3)]
     res = []
-    for env in ("1", "0"):
-        monkeypatch.setenv("VIHMC_IMG_SCATTER", env)
+    for on in (1, 0):
         eng = engine_for(c, max_chains=C)
+        eng.option("img_scatter", on)
+        assert eng.get_option("img_scatter") == on
         out = []
         for i, th in enumerate(seq):
             if i == 1:

@@ -18,10 +18,10 @@ from oracle.deeponet_ref import TorchDeepONetRef, deeponet_layout
 pytestmark = pytest.mark.gpu
 
 
-def _compare(res, fn, th0, seeds, S, L, eps, burn=0, atol=1e-4):
+def _compare(res, fn, th0, seeds, S, L, eps, burn=0, atol=1e-4, inv_mass=None):
     for c, s in enumerate(seeds):
         g = torch.Generator().manual_seed(s)
-        out, st = HR.sample(fn, th0, S, L, eps, burn=burn, generator=g, return_stats=True)
+        out, st = HR.sample(fn, th0, S, L, eps, burn=burn, generator=g, return_stats=True, inv_mass=inv_mass)
         assert res.accepted[c].cpu().tolist() == st["accepts"]
         mine = [t.cpu() for t in res.chain(c)]
         assert len(mine) == len(out)
@@ -64,6 +64,42 @@ def test_deeponet_chains_gpu_vs_scalar_reference(cuda_device):
     assert res.n_grad_evals == 2 * (1 + 15 * 7)
 
 
+@pytest.mark.parametrize("kind", ["deeponet", "bnn"])
+def test_inv_mass_fused_trajectory_vs_scalar_reference(kind, cuda_device):
+    """The VI-preconditioned mass matrix (diagonal inv_mass = sigma_VI^2 of the sampled coordinates, rescaled to
+    O(1)) on the engine's fused trajectory path vs the scalar hamiltorch restatement with the same mass and the
+    reference's own torch log-prob: identical accept sequences, positions within 1e-4."""
+    from vihmc.engine import DeepONetEngine, MLPEngine, trunk_features
+    from vihmc.samplers import ChainRNG, EngineEvaluator, run_chains
+    if kind == "deeponet":
+        c = deeponet_case("deeponet_small")
+        p = c.prob
+        eng = DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
+                             c.prior_sd, c.loss, c.tau_out, max_chains=2, device=cuda_device)
+        sig = np.asarray(p.sigma, np.float64)[p.grad_ind]
+        lay = deeponet_layout(c.spec.in_branch, c.spec.width_branch, c.spec.depth_branch, c.spec.in_trunk,
+                              c.spec.width_trunk, c.spec.depth_trunk, c.spec.out)
+        fn = TorchDeepONetRef(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, c.prior_mu, c.prior_sd, c.loss,
+                              c.tau_out).log_prob
+        S, L, eps, seeds = 12, 7, 2e-3, [30, 31]
+    else:
+        c = bnn_case("bnn_vi_hmc")
+        g = c.g
+        eng = MLPEngine(c.spec, c.data["x_train"], c.data["y_train"], g["mu"], c.idx, c.prior_mu, c.prior_sd, c.loss,
+                        c.tau_out, max_chains=2, device=cuda_device)
+        sig = np.abs(np.asarray(g["mu"], np.float64)[c.idx]) * 0.1 + 0.01
+        fn = TorchBNNRef(mlp_layout(), c.data["x_train"], c.data["y_train"], g["mu"], c.idx,
+                         prior_list=list(g["prior_var"]), loss=c.loss, tau_out=c.tau_out).log_prob
+        S, L, eps, seeds = 12, 20, 5e-4, [40, 41]
+    inv_mass = torch.tensor(sig ** 2 / np.mean(sig ** 2), dtype=torch.float32)
+    assert getattr(eng, "fused_trajectory", False)
+    th0 = torch.tensor(c.thetas[0])
+    res = run_chains(EngineEvaluator(eng), th0[None].repeat(2, 1), S, L, eps, inv_mass=inv_mass,
+                     rng=ChainRNG(2, th0.numel(), cuda_device, seeds=seeds))
+    _compare(res, fn, th0, seeds, S, L, eps, inv_mass=inv_mass)
+    assert 0 < float(res.accepted.float().mean())
+
+
 def test_sharding_independence(cuda_device):
     """A chain's samples depend only on its seed, not on which/how many chains share the launch."""
     from vihmc.engine import MLPEngine
@@ -81,15 +117,21 @@ def test_sharding_independence(cuda_device):
     assert torch.equal(full.stacked()[2:], part.stacked())
 
 
-@pytest.mark.parametrize("variant", ["hmc", "inv_mass", "nuts"])
-def test_deeponet_fused_trajectory_bitwise_equals_stepwise(variant, cuda_device):
+@pytest.mark.parametrize("variant,case,fuse_scatter", [("hmc", "deeponet_small", 1),
+                                                       ("inv_mass", "deeponet_small", 1),
+                                                       ("nuts", "deeponet_small", 1),
+                                                       ("inv_mass", "deeponet_refshape", 1),
+                                                       ("hmc", "deeponet_refshape", 0)])
+def test_deeponet_fused_trajectory_bitwise_equals_stepwise(variant, case, fuse_scatter, cuda_device):
     """vihmc_trajectory on a DeepONet plan (leapfrog updates fused into the gradient gather) == L separate
-    evaluations driven by the torch elementwise updates, bit for bit: positions, accepts, log-probs, step sizes."""
+    evaluations driven by the torch elementwise updates, bit for bit: positions, accepts, log-probs, step sizes.
+    deeponet_refshape is width 100: the bf16x6 fused forward, the weight images kept current by the scatter and by
+    the leapfrog's own scatter in k_leap_open / k_gather_prior<LEAP> (fuse_scatter = 1) or by k_scatter (0)."""
     from vihmc.engine import DeepONetEngine, trunk_features
     from vihmc.samplers import ChainRNG, EngineEvaluator, Sampler, run_chains
-    c = deeponet_case("deeponet_small")
+    c = deeponet_case(case)
     p = c.prob
-    C = 3
+    C = 3 if case == "deeponet_small" else 2
     th0 = torch.tensor(c.thetas[0])
     kw = dict(burn=2)
     if variant == "inv_mass":
@@ -101,7 +143,9 @@ def test_deeponet_fused_trajectory_bitwise_equals_stepwise(variant, cuda_device)
         eng = DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
                              c.prior_sd, c.loss, c.tau_out, max_chains=C, device=cuda_device)
         eng.fused_trajectory = fused
-        out.append(run_chains(EngineEvaluator(eng), th0[None].repeat(C, 1), 8, 7, 2e-3,
+        eng.option("fuse_scatter", fuse_scatter)
+        S, L, eps = (8, 7, 2e-3) if case == "deeponet_small" else (5, 3, 5e-3)
+        out.append(run_chains(EngineEvaluator(eng), th0[None].repeat(C, 1), S, L, eps,
                               rng=ChainRNG(C, th0.numel(), cuda_device, seeds=[20 + i for i in range(C)]), **kw))
     a, b = out
     assert torch.equal(a.accepted, b.accepted)

@@ -48,6 +48,28 @@ def test_hmc_splitting_config4_script(tmp_path):
     assert len(f) == 1 and np.load(tmp_path / f[0]).shape[1] == 172401
 
 
+def _full_prior(d, D=172401, seed=3):
+    """means_flattened / stds_flattened as the reference's full-parameter scripts read them (no uid)."""
+    import torch
+    rs = np.random.default_rng(seed)
+    os.makedirs(d, exist_ok=True)
+    torch.save(torch.from_numpy((0.05 * rs.standard_normal(D)).astype(np.float32)), os.path.join(d, "means_flattened"))
+    torch.save(torch.from_numpy((0.01 + 0.02 * rs.random(D)).astype(np.float32)), os.path.join(d, "stds_flattened"))
+    return d
+
+
+def test_hmc_splitting_and_nuts_load_prior(tmp_path):
+    """cfg.load_prior / cfg.init_prior on the full-parameter scripts: {prior_file}/means_flattened and
+    stds_flattened, no uid and no gradient indices (main_HMC_splitting.py:343-344, NUTS_DeepOnets.py:270-271)."""
+    pf = _full_prior(str(tmp_path / "prior"))
+    so = run("main_HMC_splitting.py", ["--num-samples", "3", "--n-train", "8", "--out-dir", str(tmp_path / "s"),
+                                       "--prior-file", pf], tmp_path)
+    assert "Number of splits:  2" in so and "Expected MSE" in so
+    so = run("NUTS_DeepOnets.py", ["--num-samples", "4", "--burn", "2", "--out-dir", str(tmp_path / "n"),
+                                   "--prior-file", pf], tmp_path)
+    assert "final step sizes" in so and "Expected MSE" in so
+
+
 def test_nuts_deeponets_script(tmp_path):
     so = run("NUTS_DeepOnets.py", ["--num-samples", "5", "--burn", "2", "--out-dir", str(tmp_path)], tmp_path)
     assert "final step sizes" in so and "Expected MSE" in so

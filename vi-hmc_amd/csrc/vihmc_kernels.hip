@@ -262,7 +262,9 @@ __global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t g
         const float d = th - prior_mu[k];
         const float iv = prior_inv_var[k];
         lp += -0.5 * (double)d * (double)d * (double)iv;
-        const float g = gp[c * gp_cs + smap[k]] - d * iv * inv_scale;
+        // one explicit fma after a rounded product: the same rounding in both instantiations whatever the
+        // contraction pragma around them (the fused trajectory is bitwise the step-by-step path)
+        const float g = __builtin_fmaf(-__fmul_rn(d, iv), inv_scale, gp[c * gp_cs + smap[k]]);
         if (grad) grad[o] = g;
         if (LEAP) {
 #pragma clang fp contract(off)

@@ -72,50 +72,13 @@ __host__ __device__ constexpr int rowdot_ldb(int k4) { return k4 + ((24 - (k4 & 
 // Epilogue of one row tile: bias + activation (FWD) or * act'(h) (BWD), float4 stores; columns in
 // [Nn, ldo) are written as zeros (padding read by the next GEMM). (A branch-free variant templated on
 // the activation measured ~10% slower on the hidden layers; see profiles/README.md.)
-// stg (forward only, ROWDOT_STAGE = 1): the wave's 16 x ldo LDS region. The transposed accumulators give each
-// store instruction 16 rows x 64 B, which leaves partial 128-B lines (PMC: 94.8 MB written per input-layer launch
-// for 71.7 MB of h_0); staged through LDS, the wave writes the 16-row block (contiguous in HBM) as 1-KB stores.
-// Measured slower and off by default: input layers 44.3 vs 35.6 us at C = 16 (the staging's 28 KB of LDS drops
-// the launch to 2 workgroups per CU; profiles/r02_input/README.md).
-#ifndef ROWDOT_STAGE
-#define ROWDOT_STAGE 0
-#endif
+// (Staging the output block through LDS for 1-KB row-major stores was measured slower: input layers 44.3 vs
+// 35.6 us at C = 16, the staging LDS halves the resident workgroups; profiles/r02_input/README.md.)
 template <int NT, int MS, int MODE>
 __device__ __forceinline__ void rowdot_epilogue(const RowdotProb& P, int c, int m0, int lr, int lg,
-                                                const f32x4 (&acc)[MS][NT], float* stg = nullptr) {
+                                                const f32x4 (&acc)[MS][NT]) {
     float* O = P.O + c * P.o_cs;
     const float* H = P.H + c * P.h_cs;
-    if (MODE == MODE_FWD && stg != nullptr) {
-        const int lane = lr + 16 * lg;
-#pragma unroll
-        for (int s = 0; s < MS; ++s) {
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const int n = 16 * t + 4 * lg;
-                if (n >= P.ldo) continue;
-                // bias per tile (hoisting all NT float4 spilled at the 168-VGPR budget)
-                const float4 bv = P.bias ? *reinterpret_cast<const float4*>(P.bias + c * P.bias_cs + n)
-                                         : float4{0.f, 0.f, 0.f, 0.f};
-                float4 o;
-                o.x = n + 0 < P.Nn ? act_apply_l(P.act, acc[s][t][0] + bv.x) : 0.f;
-                o.y = n + 1 < P.Nn ? act_apply_l(P.act, acc[s][t][1] + bv.y) : 0.f;
-                o.z = n + 2 < P.Nn ? act_apply_l(P.act, acc[s][t][2] + bv.z) : 0.f;
-                o.w = n + 3 < P.Nn ? act_apply_l(P.act, acc[s][t][3] + bv.w) : 0.f;
-                *reinterpret_cast<float4*>(stg + lr * P.ldo + n) = o;
-            }
-            __builtin_amdgcn_wave_barrier();
-            const int mb = m0 + 16 * s;
-            const int rows = min(16, P.M - mb);
-            if (rows > 0) {
-                const int nf4 = rows * (P.ldo >> 2);
-                float4* dst = reinterpret_cast<float4*>(O + (int64_t)mb * P.ldo);
-                const float4* src = reinterpret_cast<const float4*>(stg);
-                for (int e = lane; e < nf4; e += 64) dst[e] = src[e];
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        return;
-    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const int n = 16 * t + 4 * lg;
@@ -165,7 +128,6 @@ __device__ __forceinline__ void rowdot_body(const RowdotProb& P, int b, float* b
     const int KK = KF > 0 ? KF : P.K;
     const int K4 = (KK + 3) & ~3;
     const int LDB = rowdot_ldb(K4);
-    float* stg = (MODE == MODE_FWD && ROWDOT_STAGE) ? bs + P.Nn * LDB + wave * 16 * P.ldo : nullptr;
 
     // stage B (rows n < Nn, K4 floats each; global row stride ldb >= K4, zero padded)
     {
@@ -256,7 +218,7 @@ __device__ __forceinline__ void rowdot_body(const RowdotProb& P, int b, float* b
             // first half of the next tile's A goes out before the epilogue (hidden under it), the rest
             // after it (register budget: 3 waves/SIMD = 168 VGPRs)
             if (tile + 1 < tile_end) VIHMC_RD_LOAD_A(tile + 1, 0, NKB / 2, false)
-            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc, stg);
+            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc);
             if (tile + 1 < tile_end) VIHMC_RD_LOAD_A(tile + 1, NKB / 2, NKB, true)
         }
 #undef VIHMC_RD_LOAD_A
@@ -320,7 +282,7 @@ __device__ __forceinline__ void rowdot_body(const RowdotProb& P, int b, float* b
 #pragma unroll
                     for (int s = 0; s < MS; ++s) acc[s][t] = mfma(w[t], a[s], acc[s][t]);
             }
-            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc, stg);
+            rowdot_epilogue<NT, MS, MODE>(P, c, m0, lr, lg, acc);
         }
     }
 }
@@ -610,23 +572,13 @@ __global__ __launch_bounds__(BWD_THREADS, 4) void k_bwd_ws(BwdArgs args) {
     do { hipLaunchKernelGGL(kern, grid, block, shm, s, __VA_ARGS__); return hipGetLastError(); } while (0)
 
 size_t rowdot_lds_bytes(const RowdotArgs& a) {
-    // B image [Nn][ldb] + (forward, ROWDOT_STAGE) one 16 x ldo output block per wave
+    // B image [Nn][ldb]
     size_t m = 0;
     for (int i = 0; i < a.nprob; ++i) {
         const int k4 = (a.p[i].K + 3) & ~3;
-        m = std::max(m, sizeof(float) * ((size_t)a.p[i].Nn * rowdot_ldb(k4) +
-                                         (ROWDOT_STAGE ? (size_t)ROWDOT_WAVES * 16 * a.p[i].ldo : 0)));
+        m = std::max(m, sizeof(float) * (size_t)a.p[i].Nn * rowdot_ldb(k4));
     }
     return m;
-}
-
-// VIHMC_ROWDOT_IN_KF=0: the input layers through the run-time-K body for both nets (A/B timing)
-static bool rowdot_in_kf() {
-    static const bool on = [] {
-        const char* e = std::getenv("VIHMC_ROWDOT_IN_KF");
-        return !e || std::atoi(e) != 0;
-    }();
-    return on;
 }
 
 #ifndef RD_ONLY_FIRST
@@ -638,7 +590,7 @@ int diag_switches_layers() { return RD_ONLY_FIRST; }
 // branch + trunk input layers of the Burgers DeepONet (K = 101 -> 104 padded columns, K <= 100 run time): the
 // padded operand columns are zero (packed W rows, the uploaded input rows), so KF0 = 104 is exact
 bool rowdot_in_ok(const RowdotArgs& a, int nt) {
-    return rowdot_in_kf() && nt == 7 && a.nprob == 2 && (a.p[0].K + 3) / 4 * 4 == 104 && a.p[0].lda >= 104 &&
+    return nt == 7 && a.nprob == 2 && (a.p[0].K + 3) / 4 * 4 == 104 && a.p[0].lda >= 104 &&
            a.p[0].ldb >= 104 && a.p[1].K <= 100;
 }
 
@@ -649,11 +601,7 @@ static hipError_t rowdot_nt(const RowdotArgs& a, int nt, hipStream_t s) {
     dim3 g(blocks), blk(256);
     const bool k100 = a.p[0].K == 100 && (a.nprob < 2 || a.p[1].K == 100);
     if (k100 && nt == 7) VIHMC_LAUNCH_L((k_rowdot2<7, MS, MODE, 100>), g, blk, shm, s, a);
-    if (MODE == MODE_FWD && rowdot_in_ok(a, nt)) {
-        if (a.ms0 == 1) VIHMC_LAUNCH_L((k_rowdot_in<7, MS, 104, 1>), g, blk, shm, s, a);
-        VIHMC_LAUNCH_L((k_rowdot_in<7, MS, 104, MS>), g, blk, shm, s, a);
-    }
-    if (a.ms0 != 0 && a.ms0 != MS) return hipErrorInvalidValue;
+    if (MODE == MODE_FWD && rowdot_in_ok(a, nt)) VIHMC_LAUNCH_L((k_rowdot_in<7, MS, 104, MS>), g, blk, shm, s, a);
     switch (nt) {
         case 1: VIHMC_LAUNCH_L((k_rowdot2<1, MS, MODE, 0>), g, blk, shm, s, a);
         case 2: VIHMC_LAUNCH_L((k_rowdot2<2, MS, MODE, 0>), g, blk, shm, s, a);

@@ -135,14 +135,13 @@ struct vihmc_plan {
     // evaluation is 4 stream operations instead of ~20 kernel launches
     std::vector<std::pair<int, hipGraphExec_t>> graphs;
     hipStream_t cap_stream = nullptr;
-    // bf16x6 forward: weights pre-split once per evaluation (k_split_wimg) and DMA-staged; VIHMC_FWD_WIMG=0
-    // runs the fp32-MFMA fused forward instead (the bf16x6 one reads the images' fp32 k tail)
+    // bf16x6 forward: weights pre-split (kept current by the scatter, or k_split_wimg per evaluation) and
+    // DMA-staged; plan option fwd_wimg = 0 runs the fp32-MFMA fused forward instead (the bf16x6 one reads the
+    // images' fp32 k tail)
     unsigned char* wimg = nullptr;
     int64_t wimg_cs = 0;
-    int fwd_wimg = [] {
-        const char* e = std::getenv("VIHMC_FWD_WIMG");
-        return e ? (std::atoi(e) != 0 ? 1 : 0) : 1;
-    }();
+    int fwd_wimg = 1;
+    int fuse_scatter = 1;       // plan option: trajectory evaluations take theta already scattered by the leapfrog
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
     int graph_on = -1;          // -1: follow VIHMC_GRAPH
     // hidden-layer forward products as exact 3-way bf16 splits (6 bf16 MFMA products, fp32 accumulate;
@@ -253,8 +252,6 @@ void fused_args(vihmc_plan* p, int C, FusedArgs& a);
 // evaluation, or no images).
 int image_maps(vihmc_plan* p, const vihmc_deeponet_desc* d, const int64_t* idx) {
     if (!fused_forward_ok(p)) return 0;
-    if (const char* e = std::getenv("VIHMC_IMG_SCATTER"))      // 0: split per evaluation (A/B)
-        if (std::atoi(e) == 0) return 0;
     std::vector<int32_t> fw(p->D, -1), ff(p->D, -1);
     int img = 0;
     const vihmc_linear* tabs[2] = {d->branch, d->trunk};
@@ -456,11 +453,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             // the branch workgroups alone set that launch (41 us of 64-us-class launches at C = 16). Its chunks
             // are cut to VIHMC_BWD_L0_ROWS rows (default 128: 4 sub-tiles) so they fit beside the trunk ones.
             L.rows_per_chunk = n.rows_per_chunk;
-            if (j == 0 && L.n_in >= 64) {
-                int r0 = 128;
-                if (const char* e = std::getenv("VIHMC_BWD_L0_ROWS")) r0 = std::max(32, std::atoi(e) / 32 * 32);
-                L.rows_per_chunk = std::min(n.rows_per_chunk, r0);
-            }
+            if (j == 0 && L.n_in >= 64) L.rows_per_chunk = std::min(n.rows_per_chunk, 128);
             L.n_chunks = cdiv(n.rows, L.rows_per_chunk);
             L.part_stride = r4((int64_t)L.n_out * L.ldi + L.n_out);
             L.part_off = po;
@@ -474,8 +467,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         // side A: workgroups own 128 trunk rows and sweep the branch rows; split the sweep (partial
         // dZ_trunk slabs + fixed-order reduce) only when too few workgroups would fill the chip
         const int og_a = cdiv(p->P, CONTRACT_OWN_PER_WG), og_b = cdiv(p->N, CONTRACT_OWN_PER_WG);
-        int qa = std::max(1, std::min(8, (int)std::lround(1024.0 / ((double)C * og_a))));
-        if (const char* e = std::getenv("VIHMC_QSPLIT_A")) qa = std::max(1, std::min(64, std::atoi(e)));
+        const int qa = std::max(1, std::min(8, (int)std::lround(1024.0 / ((double)C * og_a))));
         // multiple of 32 rows: whole blocks of the pre-split image for k_contract_bf (and 16-row chunks)
         p->qperA = (int)(((int64_t)cdiv(p->N, qa) + CONTRACT_SPLIT_ROWS - 1) / CONTRACT_SPLIT_ROWS * CONTRACT_SPLIT_ROWS);
         p->qchunksA = cdiv(p->N, p->qperA);
@@ -490,7 +482,6 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             qc = std::max(1, (int)std::lround(256.0 / ((double)C * cdiv(p->N, CONTRACT_BF_B_OWN))));
             qc = std::min(qc, cdiv(p->P, CONTRACT_SPLIT_ROWS));
         }
-        if (const char* e = std::getenv("VIHMC_QSPLIT_B")) qc = std::max(1, std::min(256, std::atoi(e)));
         p->qperB = (int)(((int64_t)cdiv(p->P, qc) + CONTRACT_SPLIT_ROWS - 1) / CONTRACT_SPLIT_ROWS * CONTRACT_SPLIT_ROWS);
         p->qchunksB = cdiv(p->P, p->qperB);
         p->partB_cs = r64((int64_t)p->qchunksB * p->N * p->ldz);
@@ -583,15 +574,6 @@ bool fused_forward_ok(const vihmc_plan* p) {
     return true;
 }
 
-// VIHMC_FWD_IMG=0: the contraction images come from k_split_blocks instead of the forward (A/B timing)
-bool fwd_writes_img() {
-    static const bool on = [] {
-        const char* e = std::getenv("VIHMC_FWD_IMG");
-        return !e || std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 void fused_args(vihmc_plan* p, int C, FusedArgs& a) {
     a.C = C;
     a.packed = p->packed;
@@ -624,20 +606,12 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
     a.net[0].wimg = a.net[1].wimg = nullptr;           // set below when the bf16x6 kernel stages them
     // 12-wave workgroups (one per CU, 84 KB LDS) unless that grid would leave most of the 256 CUs idle
     const int64_t blocks12 = (int64_t)C * (cdiv(p->nets[0].rows, 192) + cdiv(p->nets[1].rows, 192));
-    int nw = blocks12 >= 192 ? 12 : 4;
-    if (const char* e = std::getenv("VIHMC_FWD_WAVES")) {
-        const int v = std::atoi(e);
-        if (v == 4 || v == 12 || v == 16) nw = v;
-    }
-    // bf16x6 at 12 waves, or at 4 for small chain counts (VIHMC_FWD_BF4=0: the fp32 4-wave kernel there instead)
-    static const bool bf4 = [] {
-        const char* e = std::getenv("VIHMC_FWD_BF4");
-        return !e || std::atoi(e) != 0;
-    }();
+    const int nw = blocks12 >= 192 ? 12 : 4;
+    // bf16x6 at 12 waves, or at 4 for small chain counts
     const int nwb = nw == 12 ? fwd_fused_bf_waves() : 4;
-    if (p->fwd_bf16x6 && (nw == 12 || (nw == 4 && bf4)) && (!fwd_fused_bf_needs_wimg() || (p->fwd_wimg && p->wimg))) {
+    if (p->fwd_bf16x6 && (!fwd_fused_bf_needs_wimg() || (p->fwd_wimg && p->wimg))) {
         for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * nwb);
-        if (img && fwd_writes_img()) {
+        if (img) {
             // the contraction's pre-split images of the branch (side A) and trunk (side B) outputs
             a.net[0].qimg = p->qsplitA;
             a.net[0].qimg_cs = p->qsplitA_cs;
@@ -659,25 +633,6 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
     for (int net = 0; net < 2; ++net) a.net[net].nblk = cdiv(p->nets[net].rows, 16 * nw);
     HIPCHK(launch_fwd_fused(a, nw, s));
     return 0;
-}
-
-// VIHMC_FUSE_SCATTER=0: trajectory evaluations run their own k_scatter (A/B timing)
-static bool fuse_scatter() {
-    static const bool on = [] {
-        const char* e = std::getenv("VIHMC_FUSE_SCATTER");
-        return !e || std::atoi(e) != 0;
-    }();
-    return on;
-}
-
-// VIHMC_ROWDOT_IN_MS1=1: the branch input layer at 16 rows per wave (twice the workgroups) instead of the launch's
-// 32. Measured slower, off by default: 39.1 vs 36.0 us per input-layer launch at C = 16 (profiles/r02_input/)
-static bool rowdot_in_ms1() {
-    static const bool on = [] {
-        const char* e = std::getenv("VIHMC_ROWDOT_IN_MS1");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
 }
 
 // Forward through both MLPs (grouped launches: branch + trunk layer j together); the hidden 100 -> 100
@@ -735,13 +690,6 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img) {
             nt = std::max(nt, nt_of(L.n_out));
         }
         if (a.nprob == 1) a.p[1] = a.p[0];
-        // input layers: the branch (one tile per workgroup) at 16 rows per wave when the launch runs 32
-        if (j == 0 && ms == 2 && rowdot_in_ms1() && rowdot_in_ok(a, nt)) {
-            RowdotProb& q = a.p[0];
-            q.ntiles = cdiv(q.M, ROWDOT_WAVES * 16);
-            q.tiles = cdiv(q.ntiles, q.tpw);
-            a.ms0 = 1;
-        }
         HIPCHK(launch_rowdot(a, nt, ms, MODE_FWD, s));
     }
     return 0;
@@ -852,7 +800,6 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         q.qimg = p->qsplitB;
         q.qimg_cs = p->qsplitB_cs;
         q.xcd_group = ((int64_t)C * p->qchunksB) % 8 == 0 ? 1 : 0;
-        if (const char* e = std::getenv("VIHMC_XCD_GROUP")) q.xcd_group = q.xcd_group && std::atoi(e) != 0;
         q.b0 = p->packed;
         q.b0_cs = p->dp;
         q.out = p->partB;
@@ -1167,7 +1114,7 @@ int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, con
         // every new position is scattered into the packed weights / images by the kernel that computes it (the opening
         // kernel, then each step's gradient gather), so the evaluations skip their k_scatter (VIHMC_FUSE_SCATTER=0:
         // the evaluations scatter as usual)
-        const bool fuse = fuse_scatter();
+        const bool fuse = p->fuse_scatter != 0;
         const ScatterImg si = scatter_img(p);
         const ScatterArgs sc{p->packed, p->dp, p->smap_w, p->smap_wt, p->img_by_scatter ? si : ScatterImg{}};
         HIPCHK(launch_leap_open(theta_in, theta_out, p_in, p_out, g_in, eps, inv_mass, p->K, C, s, fuse ? &sc : nullptr));
@@ -1392,6 +1339,8 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter"
+
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
     const std::string k(key);
@@ -1399,7 +1348,10 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "contract_bf16x6") p->contract_bf16x6 = value ? 1 : 0;
     else if (k == "bwd_bf16x6") p->bwd_bf16x6 = value ? 1 : 0;
     else if (k == "graph") p->graph_on = value ? 1 : 0;
-    else return fail("unknown plan option '" + k + "' (fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph)");
+    else if (k == "fwd_wimg") p->fwd_wimg = value ? 1 : 0;
+    else if (k == "fuse_scatter") p->fuse_scatter = value ? 1 : 0;
+    else if (k == "img_scatter") p->img_by_scatter = value && p->smap_img;   // 0: split the images per evaluation
+    else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     // captured graphs embed the kernel choice
     for (auto& g : p->graphs) (void)hipGraphExecDestroy(g.second);
     p->graphs.clear();
@@ -1413,7 +1365,10 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "contract_bf16x6") *value = p->contract_bf16x6 && p->W == 100;
     else if (k == "bwd_bf16x6") *value = p->bwd_bf16x6;
     else if (k == "graph") *value = p->graph_on;
-    else return fail("unknown plan option '" + k + "' (fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph)");
+    else if (k == "fwd_wimg") *value = p->fwd_wimg;
+    else if (k == "fuse_scatter") *value = p->fuse_scatter;
+    else if (k == "img_scatter") *value = p->img_by_scatter ? 1 : 0;
+    else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
 }
 

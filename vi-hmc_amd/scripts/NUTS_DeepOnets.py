@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from vihmc import configs  # noqa: E402
-from vihmc.data import load_vi_artefacts  # noqa: E402
+from vihmc.data import load_full_prior  # noqa: E402
 from vihmc.dist import chain_seeds  # noqa: E402
 from vihmc.operator import DeepONet, define_model_log_prob_nuts, flatten, get_burgers_data  # noqa: E402
 from vihmc.postprocess import post_burn_per_chain, predictive, print_summary  # noqa: E402
@@ -37,7 +37,7 @@ def run_HMC(cfg):
     sizes = [p.nelement() for p in net.parameters()]
     shapes = [p.shape for p in net.parameters()]
     if cfg.load_prior or cfg.init_prior:
-        mean_params, std_params, _ = load_vi_artefacts(cfg.prior_file, cfg.prior_uid)
+        mean_params, std_params = load_full_prior(cfg.prior_file)
     tau_list = [torch.from_numpy(mean_params), torch.from_numpy(std_params)] if cfg.load_prior else \
         [torch.tensor(cfg.prior_var)] * len(sizes)
     tr_data, vld_data = get_burgers_data(cfg)
@@ -72,8 +72,12 @@ def main():
     ap.add_argument("--burn", type=int, default=None)
     ap.add_argument("--chains", type=int, default=None)
     ap.add_argument("--out-dir", default=None)
+    ap.add_argument("--prior-file", default=None,
+                    help="directory holding means_flattened / stds_flattened: sets cfg.load_prior and cfg.init_prior")
     args = ap.parse_args()
     over = {}
+    if args.prior_file:
+        over.update(prior_file=args.prior_file.rstrip("/"), load_prior=True, init_prior=True)
     if args.num_samples:
         over.update(num_samples=args.num_samples, burn=max(1, args.num_samples // 10))
     if args.burn:

@@ -24,11 +24,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from vihmc import configs  # noqa: E402
-from vihmc.data import load_vi_artefacts  # noqa: E402
-from vihmc.dist import all_reduce_sum, chain_block, chain_seeds  # noqa: E402
+from vihmc.data import load_full_prior  # noqa: E402
+from vihmc.dist import chain_block, chain_seeds  # noqa: E402
 from vihmc.engine import DeepONetEngine, trunk_features  # noqa: E402
 from vihmc.operator import DeepONet, define_split_model_log_prob, flatten, get_burgers_data  # noqa: E402
-from vihmc.postprocess import append_fname, post_burn_per_chain, predictive, print_summary  # noqa: E402
+from vihmc.postprocess import append_fname, pool_ranks, post_burn_per_chain, predictive, print_summary  # noqa: E402
 from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner, Integrator, Sampler  # noqa: E402
 
 
@@ -54,7 +54,7 @@ def run_HMC(cfg):
     net = DeepONet(cfg.width_branch, cfg.width_trunk, cfg.in_branch, cfg.in_trunk, cfg.branch_depth, cfg.trunk_depth,
                    cfg.activation, cfg.output_neurons)
     if cfg.load_prior or cfg.init_prior:
-        mean_params, std_params, _ = load_vi_artefacts(cfg.prior_file, cfg.prior_uid)
+        mean_params, std_params = load_full_prior(cfg.prior_file)
     tau_list = [torch.from_numpy(mean_params), torch.from_numpy(std_params)] if cfg.load_prior else \
         [torch.tensor(cfg.prior_var)]
     tr_data, vld_data = get_split_data(cfg)
@@ -92,10 +92,7 @@ def run_HMC(cfg):
                           np.arange(D), pm, ps, cfg.loss, cfg.tau_out, max_chains=min(16, cfg.num_samples + 1),
                           device=dev)
     p = predictive(veng, post_burn_per_chain(res.samples, res.counts, 0), yv)
-    n = torch.tensor([float(p.n)], dtype=torch.float64, device=dev)
-    all_reduce_sum(p.pred_sum)
-    all_reduce_sum(n)
-    p.n = int(n.item())
+    pool_ranks(p)                                          # job-wide sums and per-sample lists
     if rank == 0:
         print_summary(p, yv)
     return res
@@ -107,8 +104,12 @@ def main():
     ap.add_argument("--chains", type=int, default=None)
     ap.add_argument("--n-train", type=int, default=None)
     ap.add_argument("--out-dir", default=None)
+    ap.add_argument("--prior-file", default=None,
+                    help="directory holding means_flattened / stds_flattened: sets cfg.load_prior and cfg.init_prior")
     args = ap.parse_args()
     over = {}
+    if args.prior_file:
+        over.update(prior_file=args.prior_file.rstrip("/"), load_prior=True, init_prior=True)
     if args.num_samples:
         over.update(num_samples=args.num_samples, burn=args.num_samples // 2)
     if args.chains:

@@ -17,8 +17,8 @@ import torch.distributed as dist  # noqa: E402
 
 from vihmc import bnn, configs  # noqa: E402
 from vihmc.data import load_vi_artefacts, save_vi_artefacts  # noqa: E402
-from vihmc.dist import all_reduce_sum, chain_block, chain_seeds  # noqa: E402
-from vihmc.postprocess import post_burn_per_chain, predictive  # noqa: E402
+from vihmc.dist import chain_block, chain_seeds  # noqa: E402
+from vihmc.postprocess import pool_ranks, post_burn_per_chain, predictive  # noqa: E402
 from vihmc.samplers import ChainRNG, EngineEvaluator, run_chains  # noqa: E402
 
 
@@ -70,10 +70,7 @@ def draw_and_validate(cfg, full_hmc=False):
     # posterior predictive from each chain's own post-burn samples (chains that hit a LogProbError store fewer);
     # prediction sums all-reduced over ranks, the sample pool itself never moves
     p = predictive(fval._vihmc_engine, post_burn_per_chain(res.samples, res.counts, cfg.burn), y_val)
-    n = torch.tensor([float(p.n)], dtype=torch.float64, device=dev)
-    all_reduce_sum(p.pred_sum)
-    all_reduce_sum(n)
-    p.n = int(n.item())
+    pool_ranks(p)                                          # job-wide sums and per-sample lists
     if rank == 0:
         yv = y_val.to(dev)
         print("acceptance rate per chain:", [round(float(a), 3) for a in res.accepted.float().mean(1)])

@@ -29,11 +29,11 @@ import torch.distributed as dist  # noqa: E402
 
 from vihmc import configs  # noqa: E402
 from vihmc.data import deeponet_problem, load_vi_artefacts, save_vi_artefacts  # noqa: E402
-from vihmc.dist import all_reduce_sum, chain_block, chain_seeds, gather_pool  # noqa: E402
+from vihmc.dist import chain_block, chain_seeds, gather_ragged_pool  # noqa: E402
 from vihmc.engine import DeepONetEngine, trunk_features  # noqa: E402
 from vihmc.operator import DeepONet, define_model_log_prob, flatten, get_burgers_data  # noqa: E402
-from vihmc.postprocess import (append_fname, load_pooled_samples, post_burn_per_chain, predictive,  # noqa: E402
-                               print_summary)
+from vihmc.postprocess import (append_fname, load_pooled_samples, pool_ranks, post_burn_per_chain,  # noqa: E402
+                               predictive, print_summary)
 from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner, Sampler  # noqa: E402
 
 
@@ -92,12 +92,10 @@ def run_VI_HMC(cfg, gather=False):
         for c in range(cfg.num_chains):
             append_fname(cfg.out_dir, f"{dt_string}_c{c}")
     if gather:
-        n_min = res.counts.min().reshape(1).clone()
-        if ws > 1:
-            dist.all_reduce(n_min, op=dist.ReduceOp.MIN)
-        pool = gather_pool(res.samples[:, :int(n_min)].contiguous())   # one RCCL all-gather over xGMI
+        # one RCCL all-gather over xGMI; chains store different counts after a LogProbError
+        pool, pool_counts = gather_ragged_pool(res.samples, res.counts)
         if rank == 0:
-            print("pooled samples:", tuple(pool.shape))
+            print("pooled samples:", tuple(pool.shape), "stored per chain:", pool_counts.tolist())
     # posterior predictive on the validation set: this rank's chains (each its own post-burn samples),
     # prediction sums all-reduced over ranks
     evaluate(cfg, net.spec, mu, sigma, grad_ind, vld_data, post_burn_per_chain(res.samples, res.counts, cfg.burn),
@@ -112,10 +110,7 @@ def evaluate(cfg, spec, mu, sigma, grad_ind, vld_data, sample_sets, dev, rank, t
                           *((mu[grad_ind], sigma[grad_ind]) if cfg.load_prior else (0.0, cfg.prior_var ** 0.5)),
                           loss=cfg.loss, tau_out=cfg.tau_out, max_chains=min(16, n_max), device=dev)
     p = predictive(veng, sample_sets, yv)
-    n = torch.tensor([float(p.n)], dtype=torch.float64, device=dev)
-    all_reduce_sum(p.pred_sum)
-    all_reduce_sum(n)
-    p.n = int(n.item())
+    pool_ranks(p)                                          # job-wide sums and per-sample lists
     if rank == 0 and p.mse:
         print_summary(p, yv)
         np.save(f"{cfg.out_dir}sample_mse_{tag}.npy", np.asarray(p.mse))

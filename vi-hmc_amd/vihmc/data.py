@@ -168,6 +168,16 @@ def save_vi_artefacts(prior_file: str, uid: str, mu: np.ndarray, sigma: np.ndarr
     np.save(f"{prior_file}/gradient_indices_{uid}.npy", np.asarray(grad_ind, np.int64))
 
 
+def load_full_prior(prior_file: str):
+    """The full-parameter HMC scripts' prior: ``{prior_file}/means_flattened`` and ``stds_flattened`` (no uid, no
+    gradient indices: Operator_network/HMC/main_HMC_splitting.py:343-344, NUTS_DeepOnets.py:270-271), loaded with
+    ``weights_only=True``."""
+    import torch
+    mu = torch.load(f"{prior_file}/means_flattened", weights_only=True, map_location="cpu")
+    sd = torch.load(f"{prior_file}/stds_flattened", weights_only=True, map_location="cpu")
+    return mu.numpy().astype(np.float32), sd.numpy().astype(np.float32)
+
+
 def load_vi_artefacts(prior_file: str, uid: str):
     """Loads with non-executing loaders only (``weights_only=True``, ``allow_pickle=False``)."""
     import torch

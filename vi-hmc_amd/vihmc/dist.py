@@ -53,6 +53,47 @@ def gather_pool(local: torch.Tensor, total_chains: Optional[int] = None) -> torc
     return torch.cat(blocks)
 
 
+def gather_ragged_pool(samples: torch.Tensor, counts: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All-gather per-rank sample stores ``samples`` [C_local, S_cap, K] whose chain c holds ``counts[c]``
+    valid samples. Chains that hit a ``LogProbError`` store fewer samples (hamiltorch appends nothing for
+    them), so ranks differ in both the chain count and the stored length: every rank trims to its own
+    longest chain, the blocks are padded to the job-wide maxima (one small all-gather of the shapes first)
+    and exchanged by ONE all_gather_into_tensor. Returns the pool [C_total, S_max, K] (padding rows zero)
+    and the per-chain counts [C_total], in rank order on every rank."""
+    rank, ws = world()
+    n_valid = int(counts.max().item()) if counts.numel() else 0
+    valid = torch.arange(n_valid, device=samples.device)[None, :] < counts.to(samples.device)[:, None]
+    local = torch.where(valid[:, :, None], samples[:, :n_valid], torch.zeros((), dtype=samples.dtype,
+                                                                             device=samples.device))
+    if ws == 1:
+        return local, counts.clone()
+    shape = torch.tensor([local.shape[0], local.shape[1]], device=local.device, dtype=torch.long)
+    shapes = [torch.zeros_like(shape) for _ in range(ws)]
+    dist.all_gather(shapes, shape)
+    shapes = [(int(s[0].item()), int(s[1].item())) for s in shapes]
+    cmax = max(s[0] for s in shapes)
+    smax = max(s[1] for s in shapes)
+    K = samples.shape[2]
+    blk = torch.zeros((cmax, smax, K), device=local.device, dtype=local.dtype)
+    blk[:local.shape[0], :local.shape[1]] = local
+    cnt = torch.zeros(cmax, device=local.device, dtype=torch.long)
+    cnt[:counts.numel()] = counts
+    out = torch.empty((ws * cmax, smax, K), device=local.device, dtype=local.dtype)
+    dist.all_gather_into_tensor(out, blk)
+    out_cnt = torch.empty(ws * cmax, device=local.device, dtype=torch.long)
+    dist.all_gather_into_tensor(out_cnt, cnt)
+    keep = torch.cat([torch.arange(r * cmax, r * cmax + shapes[r][0], device=local.device) for r in range(ws)])
+    return out[keep], out_cnt[keep]
+
+
+def max_over_ranks(x: float, device) -> float:
+    """The job's time for a per-rank wall time: the maximum over ranks (bench.py's contract)."""
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    if world()[1] > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
     if world()[1] > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)

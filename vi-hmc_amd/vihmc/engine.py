@@ -203,8 +203,10 @@ class _Engine:
         _lib.check(self.L.vihmc_graph_enable(self._plan, int(on)), "vihmc_graph_enable")
 
     def option(self, key: str, value: int):
-        """vihmc_plan_option: "fwd_bf16x6" (hidden-layer forward on the bf16 MFMA with exact 3-way splits),
-        "graph"."""
+        """vihmc_plan_option: "fwd_bf16x6" / "contract_bf16x6" / "bwd_bf16x6" (the bf16x6 forms, exact 3-way
+        splits), "graph", "fwd_wimg" (0: the fp32-MFMA fused forward), "img_scatter" (0: the forward's weight images
+        split every evaluation instead of kept by the scatter), "fuse_scatter" (0: trajectory evaluations run their
+        own scatter)."""
         _lib.check(self.L.vihmc_plan_option(self._plan, key.encode(), int(value)), f"vihmc_plan_option({key})")
 
     def get_option(self, key: str) -> int:

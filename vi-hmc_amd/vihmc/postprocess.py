@@ -10,8 +10,8 @@ Mirrors the reference's post-processing with the same file formats:
 * ``post_burn_per_chain`` -- each chain's own stored samples after burn (chains that hit a LogProbError
   store fewer samples; nothing requires equal counts).
 
-Sums across ranks (chain-sharded runs) are all-reduced by the caller (vihmc.dist.all_reduce_sum); only the
-prediction sums and counts move, never the sample pool.
+Across ranks (chain-sharded runs) ``pool_ranks`` all-reduces the prediction sums and counts and all-gathers
+the per-sample MSE / log-probability lists; the sample pool itself never moves.
 """
 from __future__ import annotations
 
@@ -81,6 +81,25 @@ def predictive(engine, sample_sets: Sequence[torch.Tensor], y: torch.Tensor, wit
                 if with_rel_l2:
                     res.rel_l2 += list(l2_relative_error_t(yd.double(), out.double()).cpu().numpy())
     return res
+
+
+def pool_ranks(p: Predictive) -> Predictive:
+    """Job-wide predictive of a chain-sharded run: the prediction sums and counts all-reduced, the per-sample
+    MSE / log-probability lists all-gathered in rank order (a few floats per sample), so every summary line
+    covers every rank's samples. No-op in a single-process run."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return p
+    n = torch.tensor([float(p.n)], dtype=torch.float64, device=p.pred_sum.device)
+    dist.all_reduce(p.pred_sum)
+    dist.all_reduce(n)
+    p.n = int(n.item())
+    lists = [None] * dist.get_world_size()
+    dist.all_gather_object(lists, (p.mse, p.log_prob, p.rel_l2))
+    p.mse = [v for l in lists for v in l[0]]
+    p.log_prob = [v for l in lists for v in l[1]]
+    p.rel_l2 = [v for l in lists for v in l[2]]
+    return p
 
 
 def print_summary(p: Predictive, y: torch.Tensor, with_rel_l2: bool = False):
