@@ -87,6 +87,42 @@ def cpu_baseline(prob, L, step_size, seconds):
                       f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
 
 
+def cpu_baseline_bnn(seconds, L=196, eps=5e-4):
+    """BNN VI-HMC (configs 2-3) on the CPU: the reference closure's torch ops (oracle/bnn_ref.TorchBNNRef: width
+    [10, 10] tanh, 20 shipped points, NLL variance 0.0025, prior N(0, 1) per tensor) in the scalar hamiltorch loop,
+    the same K = 90 sampled indices as leg_bnn, 1 chain, 1 thread (the tiny ops run fastest on one thread: SURVEY
+    §6), bounded to ~`seconds`."""
+    sys.path.insert(0, ROOT)
+    from oracle import hamiltorch_ref as HR
+    from oracle.bnn_ref import TorchBNNRef, mlp_layout
+    from vihmc.data import bnn_data, bnn_init
+    from vihmc.layout import MLPSpec
+    spec = MLPSpec()
+    x, y, _, _ = bnn_data()
+    mu = bnn_init(spec, seed=0)
+    idx = np.sort(np.random.default_rng(11).choice(spec.n_params, 90, replace=False))
+    ref = TorchBNNRef(mlp_layout(), x, y, mu, idx, prior_list=[1.0] * 6, loss="NLL", tau_out=0.0025)
+    th = torch.tensor(mu[idx])
+    g = torch.Generator().manual_seed(0)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    n = 0
+    t0 = time.perf_counter()
+    try:
+        while True:
+            th = HR.sample(ref.log_prob, th, 1, L, eps, generator=g)[-1]
+            n += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+    finally:
+        torch.set_num_threads(nt)
+    dt = time.perf_counter() - t0
+    return {"value": L * n / dt, "unit": "leapfrog-steps/s (1 chain)", "cores": 1, "kind": "port",
+            "sample": f"1 chain x {n} HMC samples (L={L}, eps={eps}; hamiltorch: L+1 grad + 2 value evals each) in "
+                      f"{dt:.1f} s, oracle/bnn_ref.TorchBNNRef (the reference's torch ops) + "
+                      f"oracle/hamiltorch_ref.sample, torch {torch.__version__} CPU, 1 thread"}
+
+
 def cpu_throughput(procs, seconds, L, step_size):
     """One process per core at one thread, one chain each: oracle/cpu_throughput.py."""
     sys.path.insert(0, ROOT)
@@ -248,6 +284,7 @@ def leg_bnn(dev, C, steps=10, L=196, eps=5e-4):
     # g in and out per chain, x / y / frozen weights / index map once
     byts = C * 6 * 4 * K + 2 * 4 * x.size + 4 * D + 4 * K
     lf = C * L * steps / dt
+    kern = "k_mlp_traj_bnn" if eng.get_option("mlp_fast") else "k_mlp_traj"
     eng.close()
     return {"workload": f"BNN VI-HMC (configs 2-3), {C} chain(s) per GPU, L = {L}", "chains": C,
             "leapfrog_steps_per_s": lf, "us_per_leapfrog_step": 1e6 * dt / (L * steps),
@@ -255,8 +292,9 @@ def leg_bnn(dev, C, steps=10, L=196, eps=5e-4):
             "kernel_share_of_wall": avg * L * steps / 1e3 / dt,
             "algorithmic_bytes_per_launch": byts,
             "hbm_frac": byts / (avg * L / 1e3) / 1e9 / HBM_PEAK_GBS,
-            "note": "latency-bound: one k_mlp_traj launch per HMC iteration (one wave per chain, the whole "
-                    "leapfrog trajectory in LDS); the HBM fraction is from algorithmic bytes"}
+            "kernel": kern,
+            "note": "latency-bound: one trajectory launch per HMC iteration (one wave per chain, theta / p / g and the "
+                    "per-row activations in registers); the HBM fraction is from algorithmic bytes"}
 
 
 def ess_phase(args, ev, runner, K, dev, chains, world):
@@ -432,6 +470,12 @@ def main():
     line.update(extra)
     if side:
         line["side_legs"] = side
+    if world == 1 and args.cpu_seconds > 0 and "bnn_config2_1_chain" in side:
+        bc = cpu_baseline_bnn(min(args.cpu_seconds, 10.0))
+        side["bnn_cpu_baseline"] = bc
+        side["bnn_config2_1_chain"]["speedup_vs_cpu"] = side["bnn_config2_1_chain"]["leapfrog_steps_per_s"] / bc["value"]
+        side["bnn_config3_8_chains"]["speedup_per_chain_vs_cpu"] = \
+            side["bnn_config3_8_chains"]["leapfrog_steps_per_s"] / 8 / bc["value"]
     if world == 1 and args.cpu_seconds > 0:
         cb = cpu_baseline(prob, args.L, args.step_size, args.cpu_seconds)
         line["cpu_baseline"] = cb

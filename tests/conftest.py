@@ -20,3 +20,10 @@ def cuda_device():
     if not torch.cuda.is_available():
         pytest.fail("gpu-marked test run without a visible HIP device")
     return torch.device("cuda", 0)
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Measured parity errors of the GPU tests (tests/parity.py) -> $VIHMC_PARITY_LOG, default
+    gpurun_out/parity_errors.json (copied into profiles/ as the round's record)."""
+    import parity
+    parity.write(os.environ.get("VIHMC_PARITY_LOG", os.path.join(ROOT, "gpurun_out", "parity_errors.json")))

@@ -1,14 +1,13 @@
 """HIP path vs oracle / reference goldens, through the C-ABI (libvihmc.so via vihmc.engine).
 
-Tolerances (fp32 kernels, different summation order from torch's CPU kernels):
-  logp: |Δ| <= 2e-5·|logp| + 1e-3 (DeepONet: per-lane fp64 accumulation of r² keeps this tight)
-  grad: ||Δ|| <= 2e-4·||grad|| and elementwise atol 1e-4·max|grad|
-  predictions: rtol 1e-4, atol 1e-4·max|pred|
+Tolerances: every error is recorded and checked by tests/parity.py against a bound per (test, quantity) set
+from the errors measured on the MI355X (about 4x the largest over the test's cases; profiles/r03_parity_errors.json).
 """
 import numpy as np
 import pytest
 import torch
 
+import parity
 from goldens import BNN_CASES, DEEPONET_CASES, bnn_case, deeponet_case, load, spec_of
 from oracle.deeponet_ref import deeponet_layout, np_logp_grad
 
@@ -28,13 +27,29 @@ def engine_for(c, max_chains=4, device="cuda:0"):
                           c.prior_sd, c.loss, c.tau_out, max_chains=max_chains, device=device)
 
 
-def check_logp(lp, ref):
-    assert abs(lp - ref) <= 2e-5 * abs(ref) + 1e-3, (lp, ref)
+def check_logp(lp, ref, note=""):
+    parity.check("logp_rel", abs(lp - ref) / max(abs(ref), 1.0), note)
 
 
-def check_grad(g, ref):
-    assert rel_norm(g, ref) < 2e-4
-    np.testing.assert_allclose(g, ref, rtol=2e-3, atol=1e-4 * np.abs(ref).max())
+def check_grad(g, ref, note=""):
+    g = np.asarray(g, np.float64)
+    ref = np.asarray(ref, np.float64)
+    parity.check("grad_relnorm", rel_norm(g, ref), note)
+    parity.check("grad_elem", np.abs(g - ref).max() / np.abs(ref).max(), note)
+
+
+def check_grad_sub(g, sub, gs, ref_norm, note=""):
+    """full-shape goldens: a 4,096-entry subsample of the gradient and the norm of the whole gradient"""
+    g = np.asarray(g, np.float64)
+    gs = np.asarray(gs, np.float64)
+    parity.check("grad_elem", np.abs(g[sub] - gs).max() / np.abs(gs).max(), note)
+    parity.check("grad_norm_rel", abs(np.linalg.norm(g) - ref_norm) / ref_norm, note)
+
+
+def check_pred(out, pred, note=""):
+    out = np.asarray(out, np.float64)
+    pred = np.asarray(pred, np.float64)
+    parity.check("pred_elem", np.abs(out - pred).max() / np.abs(pred).max(), note)
 
 
 @pytest.mark.parametrize("name", DEEPONET_CASES + ["deeponet_burgers"])
@@ -45,19 +60,16 @@ def test_deeponet_engine_matches_golden(name, cuda_device):
     lp, g = eng.logp_grad(th)
     lp, g = lp.cpu().numpy(), g.cpu().numpy()
     for t in range(len(c.thetas)):
-        check_logp(float(lp[t]), float(c.g[f"logp{t}"]))
+        check_logp(float(lp[t]), float(c.g[f"logp{t}"]), f"{name} theta{t}")
         if f"grad{t}" in c.g:
-            check_grad(g[t], c.g[f"grad{t}"])
+            check_grad(g[t], c.g[f"grad{t}"], f"{name} theta{t}")
         else:
-            sub = c.g["grad_subsample"]
-            gs = c.g[f"grad{t}_sub"]
-            np.testing.assert_allclose(g[t][sub], gs, rtol=2e-3, atol=2e-4 * np.abs(gs).max())
-            assert np.linalg.norm(g[t].astype(np.float64)) == pytest.approx(float(c.g[f"grad{t}_norm"]), rel=2e-4)
+            check_grad_sub(g[t], c.g["grad_subsample"], c.g[f"grad{t}_sub"], float(c.g[f"grad{t}_norm"]),
+                           f"{name} theta{t}")
         if f"pred{t}" in c.g:
             lpf, out = eng.forward(th[t:t + 1])
-            pred = c.g[f"pred{t}"]
-            np.testing.assert_allclose(out[0].cpu().numpy(), pred, rtol=1e-4, atol=1e-4 * np.abs(pred).max())
-            check_logp(float(lpf[0]), float(c.g[f"logp{t}"]))
+            check_pred(out[0].cpu().numpy(), c.g[f"pred{t}"], f"{name} theta{t}")
+            check_logp(float(lpf[0]), float(c.g[f"logp{t}"]), f"{name} forward theta{t}")
 
 
 @pytest.mark.parametrize("C,fwd_bf16x6,contract_bf16x6,bwd_bf16x6", [(1, 1, 1, 1), (4, 1, 1, 1), (16, 1, 1, 1),
@@ -78,10 +90,9 @@ def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, contract_bf16x6, 
     sub = c.g["grad_subsample"]
     for i in range(C):
         t = i % n
-        check_logp(float(lp[i]), float(c.g[f"logp{t}"]))
-        gs = c.g[f"grad{t}_sub"]
-        np.testing.assert_allclose(g[i][sub], gs, rtol=2e-3, atol=2e-4 * np.abs(gs).max())
-        assert np.linalg.norm(g[i].astype(np.float64)) == pytest.approx(float(c.g[f"grad{t}_norm"]), rel=2e-4)
+        note = f"C={C} forms={fwd_bf16x6}{contract_bf16x6}{bwd_bf16x6} chain {i}"
+        check_logp(float(lp[i]), float(c.g[f"logp{t}"]), note)
+        check_grad_sub(g[i], sub, c.g[f"grad{t}_sub"], float(c.g[f"grad{t}_norm"]), note)
 
 
 def test_bf16x6_paths_match_fp32_mfma_paths(cuda_device):
@@ -105,8 +116,8 @@ def test_bf16x6_paths_match_fp32_mfma_paths(cuda_device):
     dlp = np.abs(res[1][0] - res[0][0]) / np.abs(res[0][0])
     dg = np.linalg.norm(res[1][1] - res[0][1], axis=1) / np.linalg.norm(res[0][1], axis=1)
     print(f"bf16x6 vs fp32 MFMA: logp rel max {dlp.max():.2e}, grad rel-norm max {dg.max():.2e}")
-    assert dlp.max() < 2e-6
-    assert dg.max() < 2e-5
+    parity.check("logp_rel", dlp.max(), "bf16x6 vs fp32-MFMA forms, 16 chains")
+    parity.check("grad_relnorm", dg.max(), "bf16x6 vs fp32-MFMA forms, 16 chains")
 
 
 def test_forward_without_weight_images_matches(cuda_device):
@@ -127,7 +138,8 @@ def test_forward_without_weight_images_matches(cuda_device):
         eng.close()
     dlp = np.abs(res[1][0] - res[0][0]) / np.abs(res[0][0])
     dg = np.linalg.norm(res[1][1] - res[0][1], axis=1) / np.linalg.norm(res[0][1], axis=1)
-    assert dlp.max() < 2e-6 and dg.max() < 2e-5, (dlp.max(), dg.max())
+    parity.check("logp_rel", dlp.max(), "fwd_wimg 0 vs 1")
+    parity.check("grad_relnorm", dg.max(), "fwd_wimg 0 vs 1")
 
 
 def test_weight_images_kept_by_scatter_bitwise(cuda_device):
@@ -174,8 +186,8 @@ def test_deeponet_engine_vs_fp64_oracle_many_chains(name, cuda_device):
     for i in range(C):
         rl, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, thetas[i], c.prior_mu,
                                  c.prior_sd, c.loss, c.tau_out, full=c.full)
-        check_logp(float(lp[i]), rl)
-        check_grad(g[i].cpu().numpy(), rg)
+        check_logp(float(lp[i]), rl, f"{name} chain {i} vs fp64 oracle")
+        check_grad(g[i].cpu().numpy(), rg, f"{name} chain {i} vs fp64 oracle")
     # a smaller C on the same plan only touches the first C chains and agrees bit for bit
     lp2, g2 = eng.logp_grad(torch.tensor(thetas[:3], device=cuda_device))
     assert torch.equal(lp2, lp[:3]) and torch.equal(g2, g[:3])
@@ -227,8 +239,8 @@ def test_deeponet_split_shards_engine(cuda_device):
                              np.arange(spec.n_params), 0.0, float(np.sqrt(g["prior_var"])), str(g["loss"]),
                              float(g["tau_out"]), prior_scale=2.0, device=cuda_device)
         lp, gr = eng.logp_grad(th)
-        check_logp(float(lp[0]), float(g[f"logp_shard{m}"]))
-        check_grad(gr[0].cpu().numpy(), g[f"grad_shard{m}"])
+        check_logp(float(lp[0]), float(g[f"logp_shard{m}"]), f"shard {m}")
+        check_grad(gr[0].cpu().numpy(), g[f"grad_shard{m}"], f"shard {m}")
 
 
 def test_deeponet_nonfinite_is_not_an_error(cuda_device):
@@ -268,14 +280,14 @@ def test_bnn_engine_matches_golden(name, cuda_device):
     th = torch.tensor(np.stack(c.thetas), device=cuda_device)
     lp, gr = eng.logp_grad(th)
     for t in range(2):
-        check_logp(float(lp[t]), float(g[f"logp{t}"]))
-        check_grad(gr[t].cpu().numpy(), g[f"grad{t}"])
+        check_logp(float(lp[t]), float(g[f"logp{t}"]), f"{name} theta{t}")
+        check_grad(gr[t].cpu().numpy(), g[f"grad{t}"], f"{name} theta{t}")
     val = MLPEngine(c.spec, c.data["x_val"], c.data["y_val"], g["mu"], c.idx, c.prior_mu, c.prior_sd, c.loss,
                     c.tau_out, max_chains=2, device=cuda_device)
     lpv, pred = val.forward(th)
     for t in range(2):
-        check_logp(float(lpv[t]), float(g[f"val_logp{t}"]))
-        np.testing.assert_allclose(pred[t].cpu().numpy(), g[f"val_pred{t}"], rtol=1e-4, atol=1e-4)
+        check_logp(float(lpv[t]), float(g[f"val_logp{t}"]), f"{name} validation theta{t}")
+        check_pred(pred[t].cpu().numpy(), g[f"val_pred{t}"], f"{name} validation theta{t}")
 
 
 def test_split_shards_small_rows_on_concurrent_streams(cuda_device):

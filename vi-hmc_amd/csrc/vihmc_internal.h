@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <vector>
 
 namespace vihmc {
 
@@ -230,6 +231,9 @@ struct MlpArgs {
     const float* prior_mu; const float* prior_inv_var;
     double prior_const; float prior_scale; int32_t loss; float tau_out;
     const float* theta; float* logp; float* grad; float* out;
+    // register-resident BNN kernels (vihmc_bnn.hip): canonical weight position of every flat parameter, of every
+    // sampled index, and the gradient-tile position of every sampled index (null: the shape is not the BNN's)
+    const int32_t* canon; const int32_t* cpos; const int32_t* goff;
 };
 hipError_t launch_mlp(const MlpArgs& a, int C, int maxw, hipStream_t s);
 size_t mlp_lds_bytes(int D, int n_layers, int maxw);
@@ -243,6 +247,14 @@ struct MlpTrajArgs {
     int32_t cache;                 // set by launch_mlp_traj: 1 = data rows / index map / prior / mass cached in LDS
 };
 hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int maxw, hipStream_t s);
+// the reference BNN shape (1 -> 10 -> 10 -> 1, a bias on every layer) as register-resident kernels
+constexpr int BNN_IN = 1, BNN_H1 = 10, BNN_H2 = 10, BNN_OUT = 1;
+constexpr int BNN_CANON = 152;      // canonical weight floats ([W1 | b1 | W2 | b2 | W3 | b3], 4-aligned blocks)
+constexpr int BNN_KS = 3;           // sampled indices per lane (K <= 192)
+bool mlp_bnn_fast_ok(const MlpArgs& a);
+void mlp_bnn_maps(const MlpArgs& a, std::vector<int32_t>& canon, std::vector<int32_t>& gpos);
+hipError_t launch_mlp_bnn(const MlpArgs& a, int C, hipStream_t s);
+hipError_t launch_mlp_traj_bnn(const MlpArgs& a, const MlpTrajArgs& t, int C, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
 // Sensitivity scores (vihmc_sens.hip): mean over the selected outputs f[n][p] of (df/dtheta)^2 for every

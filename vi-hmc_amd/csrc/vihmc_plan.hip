@@ -142,6 +142,7 @@ struct vihmc_plan {
     int64_t wimg_cs = 0;
     int fwd_wimg = 1;
     int fuse_scatter = 1;       // plan option: trajectory evaluations take theta already scattered by the leapfrog
+    int mlp_fast = 1;           // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
     int graph_on = -1;          // -1: follow VIHMC_GRAPH
     // hidden-layer forward products as exact 3-way bf16 splits (6 bf16 MFMA products, fp32 accumulate;
@@ -994,6 +995,26 @@ int build_mlp(vihmc_plan* p, const vihmc_mlp_desc* d, const float* x, const floa
     a.prior_scale = p->lik.prior_scale;
     a.loss = p->lik.loss;
     a.tau_out = p->lik.tau_out;
+    // the reference BNN shape runs on the register-resident kernels (vihmc_bnn.hip): their parameter maps
+    a.canon = reinterpret_cast<const int32_t*>(1);   // shape probe only (mlp_bnn_fast_ok reads the table)
+    const bool bnn = mlp_bnn_fast_ok(a);
+    a.canon = a.cpos = a.goff = nullptr;
+    if (bnn) {
+        std::vector<int32_t> canon, gpos;
+        mlp_bnn_maps(a, canon, gpos);
+        std::vector<int32_t> cpos(p->K), goff(p->K);
+        for (int k = 0; k < p->K; ++k) {
+            cpos[k] = canon[idx32[k]];
+            goff[k] = gpos[idx32[k]];
+        }
+        int32_t *dc, *dcp, *dgo;
+        if (int rc = p->upload(&dc, canon.data(), p->D)) return rc;
+        if (int rc = p->upload(&dcp, cpos.data(), p->K)) return rc;
+        if (int rc = p->upload(&dgo, goff.data(), p->K)) return rc;
+        a.canon = dc;
+        a.cpos = dcp;
+        a.goff = dgo;
+    }
     return 0;
 }
 
@@ -1006,7 +1027,8 @@ int mlp_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* grad,
     a.out = out;
     hipEvent_t stop = nullptr;
     if (int rc = p->timing_begin(VIHMC_T_MLP, s, &stop)) return rc;
-    HIPCHK(launch_mlp(a, C, p->maxw, s));
+    if (p->mlp_fast && mlp_bnn_fast_ok(a)) HIPCHK(launch_mlp_bnn(a, C, s));
+    else HIPCHK(launch_mlp(a, C, p->maxw, s));
     if (stop) HIPCHK(hipEventRecord(stop, s));
     return 0;
 }
@@ -1089,7 +1111,8 @@ int vihmc_mlp_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out,
         MlpTrajArgs t{theta_in, theta_out, p_in, p_out, g_in, g_out, logp_out, eps, inv_mass, L, 0};
         hipEvent_t stop = nullptr;
         if (int rc = p->timing_begin(VIHMC_T_MLP, s, &stop, L)) return rc;
-        HIPCHK(launch_mlp_traj(p->mlp, t, C, p->maxw, s));
+        if (p->mlp_fast && mlp_bnn_fast_ok(p->mlp)) HIPCHK(launch_mlp_traj_bnn(p->mlp, t, C, s));
+        else HIPCHK(launch_mlp_traj(p->mlp, t, C, p->maxw, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
         return 0;
     });
@@ -1339,7 +1362,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1351,6 +1374,7 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "fwd_wimg") p->fwd_wimg = value ? 1 : 0;
     else if (k == "fuse_scatter") p->fuse_scatter = value ? 1 : 0;
     else if (k == "img_scatter") p->img_by_scatter = value && p->smap_img;   // 0: split the images per evaluation
+    else if (k == "mlp_fast") p->mlp_fast = value ? 1 : 0;
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     // captured graphs embed the kernel choice
     for (auto& g : p->graphs) (void)hipGraphExecDestroy(g.second);
@@ -1368,6 +1392,7 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "fwd_wimg") *value = p->fwd_wimg;
     else if (k == "fuse_scatter") *value = p->fuse_scatter;
     else if (k == "img_scatter") *value = p->img_by_scatter ? 1 : 0;
+    else if (k == "mlp_fast") *value = p->mlp_fast && p->kind == 1 && mlp_bnn_fast_ok(p->mlp);
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
 }
