@@ -257,7 +257,7 @@ def leg_split_c1(spec, dev, L, eps, steps=10):
     return out
 
 
-def leg_bnn(dev, C, steps=10, L=196, eps=5e-4):
+def leg_bnn(dev, C, steps=10, L=196, eps=5e-4, fast=True):
     """BNN VI-HMC (Neural_network/VI_HMC, configs 2 and 3): width [10, 10] tanh, 20 shipped training points,
     NLL variance 0.0025, prior N(0, 1), K = 90 sensitive parameters of D = 141 (seeded), L = 196, eps = 5e-4."""
     from vihmc.data import bnn_data, bnn_init
@@ -272,6 +272,8 @@ def leg_bnn(dev, C, steps=10, L=196, eps=5e-4):
     K = idx.size
     eng = MLPEngine(spec, x, y, mu, idx, 0.0, prior_per_tensor(spec.tensor_sizes, K, [1.0] * 6), "NLL", 0.0025,
                     max_chains=C, device=dev)
+    if not fast:
+        eng.option("mlp_fast", 0)                           # the generic LDS kernels (A/B)
     ev = EngineEvaluator(eng)
     th0 = torch.tensor(mu[idx], device=dev)[None].repeat(C, 1)
     r = HMCRunner(ev, th0, steps + 2, L, eps, rng=ChainRNG(C, K, dev, seeds=[1000 + c for c in range(C)]))

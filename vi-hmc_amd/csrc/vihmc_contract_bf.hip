@@ -106,7 +106,9 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
     // Q chunks: blocks of the pre-split image (vihmc_split_blocks), copied global -> LDS by the D waves
     // with wave-wide DMA (global_load_lds_dwordx4: 1 KB per instruction, no VGPRs, no VALU)
     const unsigned char* qblk = P.qimg + c * P.qimg_cs + (int64_t)(q_lo / CB_QC) * CB_BLOCK;
-    // side A's image by the builtin LDS-DMA (the asm form measured 2 % slower here, 411 -> 419 us; side B uses it)
+    // side A's image by the builtin LDS-DMA. The asm form (the wait for chunk i+1 at the end of the D iteration instead
+    // of before its first LDS read) runs side A 3 % faster but the evaluation not at all: r03, 378 vs 390 us for side A,
+    // 1.489 vs 1.488 ms per evaluation -- the other kernels slowed by as much (the chip is at its power limit)
 #define VIHMC_CB_BAR() __syncthreads();
 #define VIHMC_CB_GLDS(CI, BUF)                                                                              \
     for (int k = wave - 8; k < CB_GLDS; k += CBA_DW)                                                        \
@@ -139,19 +141,20 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
         // targets and G^T through buffer resources: 32-bit offsets, rows past the end read 0 and owner
         // rows past Mo are dropped by the hardware range check (no exec-mask branches per element)
         const __amdgpu_buffer_rsrc_t yrs = make_rsrc_c(Yc, (uint32_t)((int64_t)P.Mq * P.ldy * 4));
-        // G^T exchange buffer, chunk-blocked: element (o, q) at ((q / 32) * ldg + o) * 32 + q % 32 (ldg = Mo
-        // rows per block) -- one chunk of one workgroup is 128 rows x 128 B, contiguous
+        // G^T exchange buffer, 16-row blocked: element (o, q) at ((q / 16) * ldg + o) * 16 + q % 16 (ldg = Mo rows
+        // per block). A 16-row S tile of one wave's 16 owner rows is 16 x 64 B = 1 KB contiguous, and lane (lr, lg)
+        // holds its 16-B piece (q = 4lg .. 4lg+3 of owner row o0 + lr) as the accumulator quad: one whole-line store
+        // per tile straight from the accumulators (no lane exchange)
         const __amdgpu_buffer_rsrc_t grs = make_rsrc_c(
             P.gout ? P.gout + c * P.gout_cs : P.Y,
             P.gout ? (uint32_t)((int64_t)((P.Mq + CB_QC - 1) / CB_QC) * P.ldg * CB_QC * 4) : 0u);
         const int oo = o0 + lr;
         const bool ovalid = oo < P.Mo;
+        // every owner row of this wave exists (all but the last owner tile): with a whole chunk, no masking
+        const bool wave_valid = o0 + 16 <= P.Mo;
         const uint32_t yoff = (uint32_t)((4 * lg) * P.ldy + min(oo, P.Mo - 1)) * 4u;
-        // G^T store offsets (see the stores): rows o0 + (lr & 7) and o0 + 8 + (lr & 7), q half by lr >= 8
-        const int gxr = o0 + (lr & 7), gyr = gxr + 8;
-        const int gq = (lr < 8 ? 0 : 16) + 4 * lg;
-        const uint32_t gx_off = gxr < P.Mo ? (uint32_t)(((q_lo / CB_QC) * P.ldg + gxr) * CB_QC + gq) * 4u : OOB_C;
-        const uint32_t gy_off = gyr < P.Mo ? (uint32_t)(((q_lo / CB_QC) * P.ldg + gyr) * CB_QC + gq) * 4u : OOB_C;
+        const uint32_t g_off = ovalid ? (uint32_t)(((q_lo / 16) * P.ldg + oo) * 16 + 4 * lg) * 4u : OOB_C;
+        const uint32_t gblk = (uint32_t)P.ldg * 64u;            // bytes per 16-row block
         const uint32_t ystep = (uint32_t)P.ldy * 4u;
         // targets [sub][r] one chunk ahead in two register sets used alternately (the loop is unrolled by
         // two), so no register copy forces a wait on the newest loads and the G^T stores
@@ -170,18 +173,18 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
             VIHMC_CB_STAMP(i, 0)
             {
                 const int q0 = q_lo + i * CB_QC;
-                const bool full = q0 + CB_QC <= q_hi;
+                const bool nomask = q0 + CB_QC <= q_hi && wave_valid;   // wave-uniform
                 const unsigned char* img = smc + (i % CB_NQBUF) * CB_QIMG;
                 VIHMC_CB_YLOAD(yn, min(i + 1, nchunks - 1))
                 unsigned char* gimg = smc + CB_NQBUF * CB_QIMG + (i & 1) * CB_GIMG + w * (CB_GIMG / 8);
                 float ps = 0.f, gp = 0.f;
-                f32x4 gs[2];
+                f32x4 rv[2];
 #pragma unroll
                 for (int sub = 0; sub < 2; ++sub) {
                     const unsigned char* row = img + (16 * sub + lr) * CB_PITCH + 16 * lg;
                     const float qt = reinterpret_cast<const float*>(img + CB_TAIL)[(16 * sub + lr) * 4 + lg];
-                    // the exact f32 tail (features 96..99) seeds the accumulator
-                    f32x4 sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(qt, otl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                    // the exact f32 tail (features 96..99) on top of the output bias b0 seeds the accumulator
+                    f32x4 sacc = __builtin_amdgcn_mfma_f32_16x16x4f32(qt, otl, f32x4{b0, b0, b0, b0}, 0, 0, 0);
 #pragma unroll
                     for (int kb = 0; kb < 3; ++kb) {
                         bf16x8 qa[3];
@@ -190,45 +193,40 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                             qa[p] = *reinterpret_cast<const bf16x8*>(row + p * CB_PLANE + 64 * kb);
                         sacc = six(qa, ob[kb], sacc);
                     }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) rv[sub][r] = sacc[r] - yv[sub][r];
+                }
+                if (!nomask) {
+                    // a partial last chunk (branch rows past q_hi: zero image rows, so S = b0) or owner rows past Mo
+                    // (the last owner tile): those residuals are not the workgroup's
+#pragma unroll
+                    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            rv[sub][r] = (ovalid && q0 + 16 * sub + 4 * lg + r < q_hi) ? rv[sub][r] : 0.f;
+                }
+#pragma unroll
+                for (int sub = 0; sub < 2; ++sub) {
                     f32x4 g;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int qq = q0 + 16 * sub + 4 * lg + r;
-                        const bool ok = ovalid && (full || qq < q_hi);
-                        float rv = sacc[r] + b0 - yv[sub][r];
-                        rv = ok ? rv : 0.f;
-                        g[r] = P.gscale * rv;
-                        ps = fmaf(rv, rv, ps);
+                        g[r] = P.gscale * rv[sub][r];
+                        ps = fmaf(rv[sub][r], rv[sub][r], ps);
                         gp += g[r];
                     }
                     reinterpret_cast<f32x4*>(gimg)[sub * 64 + lane] = g;
-                    gs[sub] = g;
 #if CB_STAMP
                     if (sub == 0) {
                         asm volatile("" :: "v"(g));
                         VIHMC_CB_STAMP(i, 2)
                     }
 #endif
-                }
-                if (P.gout) {
-                    // Whole 128-B lines per store: lanes lr and lr ^ 8 swap halves (DPP row_ror:8), so
-                    // store X covers rows o0 + (lr & 7) and store Y rows o0 + 8 + (lr & 7), each row's 32
-                    // q values from 8 lanes (sub 0 from lr < 8, sub 1 from lr >= 8): 1 KB contiguous.
-                    const bool lo = lr < 8;
-                    f32x4 recv;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float sv = lo ? gs[1][r] : gs[0][r];
-                        recv[r] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(sv), 0x128, 0xF, 0xF, false));
-                    }
-                    const f32x4 X = lo ? gs[0] : recv;
-                    const f32x4 Y = lo ? recv : gs[1];
-                    const uint32_t cofs = (uint32_t)i * (uint32_t)P.ldg * (CB_QC * 4u);
-                    // whole lines in a partial chunk too: its q >= q_hi elements are G = 0 (rv zeroed above)
-                    // and land in the padding of the chunk-blocked layout (q_hi < Mq only at chunk boundaries,
-                    // qperA being a multiple of 32), which no workgroup owns
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, X), grs, gx_off + cofs, 0, 0);
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, Y), grs, gy_off + cofs, 0, 0);
+                    // whole lines in a partial chunk too: its q >= q_hi elements are G = 0 (rv zeroed above) and
+                    // land in the padding of the blocked layout (q_hi < Mq only at chunk boundaries, qperA being a
+                    // multiple of 32), which no workgroup owns
+                    if (P.gout)
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_c, g), grs,
+                                                               g_off + (uint32_t)(2 * i + sub) * gblk, 0, 0);
                 }
                 // sum r^2 (no cancellation): per-chunk fp32 partial of 8 terms per lane, then fp64
                 ssq += (double)ps;
@@ -408,15 +406,14 @@ __global__ __launch_bounds__(CBB_THREADS, 1) void k_contract_bf_b(ContractProb P
     // buffer loads with the whole offset in the range-checked VGPR: rows past Mq read 0, rows past q_hi
     // (another workgroup's range, only in a partial last chunk) are sent out of range
     const float* Gc = P.Y + c * P.y_cs;
-    // chunk-blocked G^T (see k_contract_bf): element (q, o) at ((o / 32) * ldy + q) * 32 + o % 32 with
-    // ldy = Mq rows per block; this wave's 32 owner rows are one block
+    // 16-row blocked G^T (see k_contract_bf): element (q, o) at ((o / 16) * ldy + q) * 16 + o % 16 with ldy = Mq
+    // rows per block; this wave's 16 owner rows are one block (64 B per trunk row q)
+    static_assert(CBB_NS == 1, "one 16-row owner block per wave");
     const __amdgpu_buffer_rsrc_t grs =
         make_rsrc_c(Gc, (uint32_t)((int64_t)((P.Mo + CB_QC - 1) / CB_QC) * P.ldy * CB_QC * 4));
     uint32_t gcol[CBB_NS];
-#pragma unroll
-    for (int s = 0; s < CBB_NS; ++s)
-        gcol[s] = (uint32_t)(((o0 / CB_QC) * P.ldy) * CB_QC + (o0 % CB_QC) + 16 * s + lr) * 4u;
-    const uint32_t ystep = CB_QC * 4u;
+    gcol[0] = (uint32_t)((o0 / 16) * P.ldy * 16 + lr) * 4u;
+    const uint32_t ystep = 16 * 4u;
     float ga_[CBB_NS][8], gb_[CBB_NS][8];
 #define VIHMC_CBB_GLOAD(GN, CI)                                                                             \
     {                                                                                                       \
