@@ -156,6 +156,13 @@ int vihmc_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, int
  * (Operator_network/VI/main_VI_deeponet.py:58-79) without re-creating the plan. */
 int vihmc_plan_set_data(vihmc_plan* p, const float* x_branch, const float* y, void* stream);
 
+/* cfg.sample_data (Operator_network/VI_HMC/main_VI_HMC_burgers.py:131-134, `ind = sample(range(x2.shape[1]),
+ * cfg.p)`): make the plan's P trunk rows the rows ind[0..P) of the full grid. trunk_all [P_all, in_trunk]
+ * (trunk features), y_all [N, P_all], ind [P] int32 in [0, P_all) -- all device pointers; the caller draws and
+ * checks the indices. Gathered on `stream` (ordered before later evaluations on it); a pure copy. */
+int vihmc_plan_set_trunk_rows(vihmc_plan* p, const float* trunk_all, const float* y_all, int64_t P_all,
+                              const int32_t* ind, void* stream);
+
 int     vihmc_plan_kind(const vihmc_plan* p);
 int64_t vihmc_plan_n_params(const vihmc_plan* p);
 int     vihmc_plan_K(const vihmc_plan* p);

@@ -218,6 +218,44 @@ def deeponet_cases(out, full_size=True):
     return probr, th1
 
 
+def deeponet_sampledata_case(out):
+    """cfg.sample_data (main_VI_HMC_burgers.py:127-137): each non-predict call evaluates at
+    ``random.sample(range(P_all), cfg.p)`` trunk rows. Python's ``random`` is seeded, then the reference closure
+    is called three times in a row; the drawn rows are replayed from the same seed and stored with the outputs."""
+    import random
+    M = import_ref("Operator_network/VI_HMC", "main_VI_HMC_burgers")
+    cfg = M.cfg
+    small = DeepONetSpec(width_branch=16, width_trunk=16, in_branch=12, in_trunk=5, depth_branch=3, depth_trunk=3)
+    prob = deeponet_problem(seed=3, n=6, nt=5, nx=7, spec=small, k=300)
+    tmp = tempfile.mkdtemp()
+    cfg.branch_depth, cfg.trunk_depth, cfg.activation = small.depth_branch, small.depth_trunk, small.activation
+    cfg.load_prior, cfg.sample_data, cfg.p = False, True, 20
+    cfg.prior_file, cfg.prior_uid = tmp, "deeponet_sampledata"
+    save_vi_artefacts(tmp, "deeponet_sampledata", prob.mu, prob.sigma, prob.grad_ind)
+    net = M.DeepONet(small.width_branch, small.width_trunk, small.in_branch, small.in_trunk, small.depth_branch,
+                     small.depth_trunk, small.activation, small.output_neurons)
+    tr = (torch.from_numpy(prob.branch_in), torch.from_numpy(prob.trunk_in), torch.from_numpy(prob.y))
+    fn = M.define_model_log_prob(net, cfg.loss, tr, [torch.tensor(cfg.prior_var)], cfg.tau_out, device="cpu")
+    th0 = prob.mu[prob.grad_ind]
+    th1 = (th0 + 0.05 * np.random.default_rng(13).standard_normal(th0.size)).astype(np.float32)
+    thetas = [th0, th1, th0]
+    seed, P_all = 2024, prob.trunk_in.shape[1]
+    random.seed(seed)
+    res = {}
+    for t, th in enumerate(thetas):
+        res[f"logp{t}"], res[f"grad{t}"] = ref_logp_grad(fn, th)
+        res[f"theta{t}"] = th
+        print("deeponet_sampledata", t, "logp", res[f"logp{t}"])
+    random.seed(seed)
+    for t in range(len(thetas)):
+        res[f"ind{t}"] = np.asarray(random.sample(range(P_all), cfg.p), np.int64)
+    cfg.sample_data = False
+    np.savez_compressed(os.path.join(out, "deeponet_sampledata.npz"), spec=np.array([16, 16, 12, 5, 3, 3, 16]),
+                        loss=cfg.loss, tau_out=cfg.tau_out, prior_var=cfg.prior_var, branch_in=prob.branch_in,
+                        trunk_in=prob.trunk_in, y=prob.y, mu=prob.mu, sigma=prob.sigma, grad_ind=prob.grad_ind,
+                        p=20, seed=seed, **res)
+
+
 def deeponet_split_cases(out):
     """Full-parameter split closures (Operator_network/HMC/main_HMC_splitting.py:79-258)."""
     M = import_ref("Operator_network/HMC", "main_HMC_splitting")
@@ -526,6 +564,9 @@ if __name__ == "__main__":
         deeponet_split_loadprior_case(HERE)
         deeponet_split_burgers_cases(HERE)
         sys.exit(0)
+    if "--sampledata-only" in sys.argv:
+        deeponet_sampledata_case(HERE)
+        sys.exit(0)
     if "--nuts-only" in sys.argv:
         deeponet_nuts_case(HERE)
         sys.exit(0)
@@ -536,5 +577,6 @@ if __name__ == "__main__":
     deeponet_split_loadprior_case(HERE)
     deeponet_split_burgers_cases(HERE)
     deeponet_nuts_case(HERE)
+    deeponet_sampledata_case(HERE)
     sensitivity_cases(HERE)
     vi_cases(HERE)

@@ -51,6 +51,8 @@ BOUNDS = {
     ("test_deeponet_engine_vs_fp64_oracle_many_chains", "grad_relnorm"): 5e-07,   # max 1.01e-07 over 14
     ("test_deeponet_engine_vs_fp64_oracle_many_chains", "logp_rel"): 9e-07,   # max 2.11e-07 over 14
     ("test_deeponet_nonfinite_is_not_an_error", "logp_rel"): 5e-06,   # max 1.06e-06 over 1
+    ("test_deeponet_sample_data_closure_matches_golden", "grad_relnorm"): 4e-07,   # max 8.97e-08 over 6
+    ("test_deeponet_sample_data_closure_matches_golden", "logp_rel"): 3e-05,   # max 5.44e-06 over 6
     ("test_deeponet_split_shards_engine", "grad_elem"): 6e-07,   # max 1.29e-07 over 2
     ("test_deeponet_split_shards_engine", "grad_relnorm"): 4e-07,   # max 8.70e-08 over 2
     ("test_deeponet_split_shards_engine", "logp_rel"): 4e-06,   # max 8.57e-07 over 2

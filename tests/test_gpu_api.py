@@ -53,6 +53,55 @@ def test_deeponet_closure_autograd_and_predict(tmp_path, cuda_device):
         np.testing.assert_allclose(preds[t].cpu().numpy(), pr, rtol=1e-4, atol=1e-4 * np.abs(pr).max())
 
 
+def test_deeponet_sample_data_closure_matches_golden(tmp_path, cuda_device):
+    """cfg.sample_data (main_VI_HMC_burgers.py:127-137): after random.seed(seed) the closure's three successive
+    calls draw the reference's trunk rows (vihmc_plan_set_trunk_rows gathers them on the device) and give the
+    reference's log-prob and gradient; the engine path draws the same rows per call; predict stays on the full
+    grid; the fused trajectory is off while rows are redrawn per evaluation."""
+    import random
+    import parity
+    from vihmc import configs
+    from vihmc.data import save_vi_artefacts
+    from vihmc.operator import define_model_log_prob
+    from vihmc.samplers import EngineEvaluator
+    g = load("deeponet_sampledata")
+    spec = spec_of(g)
+    save_vi_artefacts(str(tmp_path), "g", g["mu"], g["sigma"], g["grad_ind"])
+    cfg = configs.load("burgers_vi_hmc", prior_file=str(tmp_path), prior_uid="g", branch_depth=3, trunk_depth=3,
+                       sample_data=True, p=int(g["p"]), prior_var=float(g["prior_var"]))
+    tr = (torch.from_numpy(g["branch_in"]), torch.from_numpy(g["trunk_in"]), torch.from_numpy(g["y"]))
+    f = define_model_log_prob(spec, str(g["loss"]), tr, [torch.tensor(cfg.prior_var)], float(g["tau_out"]),
+                              device=cuda_device, cfg=cfg)
+    eng = f._vihmc_engine
+    assert eng.P == int(g["p"]) and not EngineEvaluator(eng).fused_trajectory
+
+    def check(lp, gr, t, how):
+        ref, rg = float(g[f"logp{t}"]), np.asarray(g[f"grad{t}"], np.float64)
+        parity.check("logp_rel", abs(lp - ref) / max(abs(ref), 1.0), f"{how} call{t}")
+        gr = np.asarray(gr, np.float64)
+        parity.check("grad_relnorm", np.linalg.norm(gr - rg) / np.linalg.norm(rg), f"{how} call{t}")
+
+    random.seed(int(g["seed"]))
+    for t in range(3):
+        p = torch.tensor(g[f"theta{t}"], device=cuda_device).requires_grad_()
+        lp = f(p)
+        gr, = torch.autograd.grad(lp, p)
+        check(float(lp), gr.cpu().numpy(), t, "closure")
+    random.seed(int(g["seed"]))
+    for t in range(3):
+        lp, gr = eng.logp_grad(torch.tensor(g[f"theta{t}"], device=cuda_device)[None])
+        check(float(lp[0]), gr[0].cpu().numpy(), t, "engine")
+    with pytest.raises(RuntimeError):
+        eng.trajectory(torch.zeros(1, eng.K, device=cuda_device), torch.zeros(1, eng.K, device=cuda_device),
+                       torch.zeros(1, eng.K, device=cuda_device), 1e-3, 2)
+    with pytest.raises(ValueError):
+        eng.set_trunk_rows([0] * (eng.P - 1) + [g["trunk_in"].shape[1]])
+    fp = define_model_log_prob(spec, str(g["loss"]), tr, [torch.tensor(cfg.prior_var)], float(g["tau_out"]),
+                               predict=True, device=cuda_device, cfg=cfg)
+    _, out = fp(torch.tensor(g["theta0"], device=cuda_device))
+    assert tuple(out.shape) == g["y"].shape
+
+
 def test_sample_with_closure_matches_scalar_reference(tmp_path, cuda_device):
     from vihmc.operator import define_model_log_prob
     from vihmc.samplers import sample

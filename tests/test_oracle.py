@@ -149,6 +149,26 @@ def test_deeponet_nuts_closure_golden():
     assert rel_norm(gr, g["grad"]) < 1e-4
 
 
+def test_deeponet_sample_data_golden():
+    """cfg.sample_data (main_VI_HMC_burgers.py:127-137): three successive reference calls after random.seed(seed),
+    each at random.sample(range(P_all), p) trunk rows -- the stored rows replay from the seed, and the oracle at
+    those rows gives the reference's outputs."""
+    import random
+    g = load("deeponet_sampledata")
+    spec = spec_of(g)
+    P_all, p = g["trunk_in"].shape[1], int(g["p"])
+    random.seed(int(g["seed"]))
+    for t in range(3):
+        ind = np.asarray(random.sample(range(P_all), p))
+        np.testing.assert_array_equal(ind, g[f"ind{t}"])
+        lp, gr, _ = np_logp_grad(layout_of(spec), g["branch_in"], g["trunk_in"][:, ind], g["y"][:, ind], g["mu"],
+                                 g["grad_ind"], g[f"theta{t}"], 0.0, float(np.sqrt(g["prior_var"])), str(g["loss"]),
+                                 float(g["tau_out"]))
+        assert lp == pytest.approx(float(g[f"logp{t}"]), rel=2e-5, abs=1e-3)
+        assert rel_norm(gr, g[f"grad{t}"]) < 1e-4
+    assert abs(float(g["logp0"]) - float(g["logp2"])) > 1e-3     # same theta, different rows
+
+
 @pytest.mark.parametrize("name", BNN_CASES)
 def test_bnn_oracles_match_golden(name):
     c = bnn_case(name)

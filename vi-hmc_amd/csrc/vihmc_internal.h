@@ -175,6 +175,8 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
 hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out, const float* g_in,
                             const float* eps, const float* inv_mass, int K, int C, hipStream_t s,
                             const ScatterArgs* sc = nullptr);
+hipError_t launch_gather_trunk(const float* feat_all, int in_t, const float* y_all, int64_t P_all,
+                               const int32_t* ind, int P, int N, float* input, int ld_in, float* y, hipStream_t s);
 
 // Fused hidden-layer forward (width 100 -> 100 layers of both nets, one launch): every wave keeps 16 rows
 // of activations in registers through all fused layers; per layer the weights + bias of the next layer

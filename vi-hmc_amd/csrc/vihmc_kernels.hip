@@ -563,9 +563,36 @@ __global__ __launch_bounds__(64) void k_mlp_traj(MlpArgs a, int W, MlpTrajArgs t
     if (lane == 0) t.lp_out[c] = (float)lp;
 }
 
+// cfg.sample_data (Operator_network/VI_HMC/main_VI_HMC_burgers.py:131-134): the evaluation sees the trunk rows
+// ind[0..P) of the full sensor grid -- trunk features [P_all][in_t] -> plan input [P][ld_in] (pad columns stay
+// zero), targets y_all[n][ind[j]] -> y [N][P]. Pure copy (bit-exact); indices checked on the host.
+__global__ __launch_bounds__(256) void k_gather_trunk(const float* __restrict__ feat_all, int in_t,
+                                                     const float* __restrict__ y_all, int64_t P_all,
+                                                     const int32_t* __restrict__ ind, int P, int N,
+                                                     float* __restrict__ input, int ld_in, float* __restrict__ y) {
+    const int64_t total = (int64_t)N * P, nin = (int64_t)P * in_t;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total + nin; i += (int64_t)gridDim.x * 256) {
+        if (i < total) {
+            const int64_t n = i / P, j = i - n * P;
+            y[i] = y_all[n * P_all + ind[j]];
+        } else {
+            const int64_t k = i - total, j = k / in_t, f = k - j * in_t;
+            input[j * ld_in + f] = feat_all[(int64_t)ind[j] * in_t + f];
+        }
+    }
+}
+
 // =============================================================================================
 // launchers
 // =============================================================================================
+hipError_t launch_gather_trunk(const float* feat_all, int in_t, const float* y_all, int64_t P_all,
+                               const int32_t* ind, int P, int N, float* input, int ld_in, float* y, hipStream_t s) {
+    const int64_t work = (int64_t)N * P + (int64_t)P * in_t;
+    hipLaunchKernelGGL(k_gather_trunk, dim3((unsigned)std::min<int64_t>((work + 255) / 256, 2048)), dim3(256), 0, s,
+                       feat_all, in_t, y_all, P_all, ind, P, N, input, ld_in, y);
+    return hipGetLastError();
+}
+
 #define VIHMC_LAUNCH(kern, grid, block, shm, s, ...) \
     do { hipLaunchKernelGGL(kern, grid, block, shm, s, __VA_ARGS__); return hipGetLastError(); } while (0)
 

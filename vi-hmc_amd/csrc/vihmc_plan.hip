@@ -1312,6 +1312,19 @@ int vihmc_plan_set_data(vihmc_plan* p, const float* x_branch, const float* y, vo
     });
 }
 
+int vihmc_plan_set_trunk_rows(vihmc_plan* p, const float* trunk_all, const float* y_all, int64_t P_all,
+                              const int32_t* ind, void* stream) {
+    return guarded([&]() -> int {
+        if (!p || !trunk_all || !y_all || !ind) return fail("null argument");
+        if (p->kind != 0) return fail("vihmc_plan_set_trunk_rows: DeepONet plans only");
+        if (P_all < p->P) return fail("vihmc_plan_set_trunk_rows: P_all smaller than the plan's P");
+        Net& t = p->nets[1];
+        HIPCHK(launch_gather_trunk(trunk_all, t.L[0].n_in, y_all, P_all, ind, p->P, p->N, t.input, t.ld_in, p->y,
+                                   static_cast<hipStream_t>(stream)));
+        return 0;
+    });
+}
+
 int vihmc_plan_kind(const vihmc_plan* p) { return p ? p->kind : -1; }
 int64_t vihmc_plan_n_params(const vihmc_plan* p) { return p ? p->D : -1; }
 int vihmc_plan_K(const vihmc_plan* p) { return p ? p->K : -1; }

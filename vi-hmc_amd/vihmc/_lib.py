@@ -59,6 +59,7 @@ SIGNATURES = {
                                  c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "vihmc_sensitivity": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_plan_set_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vihmc_plan_set_trunk_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "vihmc_plan_kind": (c_int, [c_void_p]),
     "vihmc_plan_n_params": (c_int64, [c_void_p]),
     "vihmc_plan_K": (c_int, [c_void_p]),

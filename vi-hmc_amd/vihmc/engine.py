@@ -8,6 +8,7 @@ device-resident, enqueued on torch's current HIP stream with no host synchronisa
 from __future__ import annotations
 
 import ctypes
+import random
 from typing import Optional, Sequence
 
 import numpy as np
@@ -48,6 +49,7 @@ class _Engine:
         self.device = torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
         self._plan = ctypes.c_void_p()
         self.L = _lib.lib()
+        self._sample_rng = None               # cfg.sample_data: redraw the trunk rows before each evaluation
 
     # ---- plan lifetime ---------------------------------------------------------------------------
     def _created(self, rc, what):
@@ -85,6 +87,8 @@ class _Engine:
                   grad: Optional[torch.Tensor] = None):
         """theta [C, K] -> (logp [C], grad [C, K]) on the engine's device."""
         th = self._theta(theta)
+        if self._sample_rng is not None:
+            self._redraw()
         C = th.shape[0]
         if logp is None:
             logp = torch.empty(C, device=self.device, dtype=torch.float32)
@@ -97,6 +101,8 @@ class _Engine:
 
     def logp(self, theta: torch.Tensor, logp: Optional[torch.Tensor] = None) -> torch.Tensor:
         th = self._theta(theta)
+        if self._sample_rng is not None:
+            self._redraw()
         C = th.shape[0]
         if logp is None:
             logp = torch.empty(C, device=self.device, dtype=torch.float32)
@@ -122,6 +128,8 @@ class _Engine:
         plans L evaluations with the momentum / position steps fused into their gradient gather): from theta
         [C, K], the fresh momentum and the gradient at theta, L steps of size eps (python float or per-chain [C])
         -> (theta_L, p_L, logp_L, grad_L), bitwise the step-by-step path."""
+        if self._sample_rng is not None:
+            raise RuntimeError("cfg.sample_data redraws the trunk rows per evaluation: use the step-by-step path")
         th = self._theta(theta)
         C = th.shape[0]
         p = momentum.to(self.device, torch.float32).contiguous()
@@ -152,6 +160,53 @@ class _Engine:
             rc = self.L.vihmc_plan_set_data(self._plan, xb.data_ptr(), yy.data_ptr(), self._stream())
         _lib.check(rc, "vihmc_plan_set_data")
         self._keep_data = (xb, yy)          # the copy is asynchronous on the stream
+
+    def set_sample_grid(self, trunk_feat_all: torch.Tensor, y_all: torch.Tensor):
+        """The full trunk grid cfg.sample_data draws from (main_VI_HMC_burgers.py:131-134): trunk features
+        [P_all, in_trunk] (as the plan was built with, i.e. after any feature map) and targets [N, P_all],
+        kept resident on the device; select rows with set_trunk_rows."""
+        ft = torch.as_tensor(trunk_feat_all).to(device=self.device, dtype=torch.float32).contiguous()
+        ya = torch.as_tensor(y_all).to(device=self.device, dtype=torch.float32).contiguous()
+        if ft.dim() != 2 or ft.shape[1] != self.spec.in_trunk or ya.shape != (self.N, ft.shape[0]):
+            raise ValueError(f"set_sample_grid needs trunk features [P_all, {self.spec.in_trunk}] and y "
+                             f"[{self.N}, P_all]")
+        if ft.shape[0] < self.P:
+            raise ValueError(f"the grid has {ft.shape[0]} rows < the plan's P={self.P}")
+        self._grid = (ft, ya)
+
+    def set_trunk_rows(self, ind):
+        """vihmc_plan_set_trunk_rows: evaluate at grid rows ``ind`` ([P] ints in [0, P_all)) from now on."""
+        if getattr(self, "_grid", None) is None:
+            raise RuntimeError("set_trunk_rows needs set_sample_grid first")
+        ft, ya = self._grid
+        ii = np.asarray(ind, dtype=np.int64).reshape(-1)
+        if ii.size != self.P or (ii.size and (ii.min() < 0 or ii.max() >= ft.shape[0])):
+            raise ValueError(f"set_trunk_rows needs {self.P} indices in [0, {ft.shape[0]})")
+        it = torch.from_numpy(ii.astype(np.int32)).to(self.device)
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_plan_set_trunk_rows(self._plan, ft.data_ptr(), ya.data_ptr(), int(ft.shape[0]),
+                                                  it.data_ptr(), self._stream())
+        _lib.check(rc, "vihmc_plan_set_trunk_rows")
+        self._keep_ind = it                   # the gather is asynchronous on the stream
+
+    def sample_data(self, trunk_feat_all, y_all, p: int, rng=None):
+        """cfg.sample_data (main_VI_HMC_burgers.py:131-134): before every logp / logp_grad call draw
+        ``rng.sample(range(P_all), p)`` (default: Python's global ``random``, which the reference's
+        ``from random import sample`` uses) and evaluate at those trunk rows. One draw per call, shared by the
+        C chains of a batched call (the reference's per-chain calls draw once each: identical at C = 1).
+        Disables the fused trajectory (it would keep one draw for L steps). ``p=None`` switches it off."""
+        if p is None:
+            self._sample_rng, self._grid = None, None
+            self.fused_trajectory = True
+            return
+        if int(p) != self.P:
+            raise ValueError(f"the plan was built for P={self.P} trunk rows, cfg.p={p}")
+        self.set_sample_grid(trunk_feat_all, y_all)
+        self._sample_rng = random if rng is None else rng
+        self.fused_trajectory = False
+
+    def _redraw(self):
+        self.set_trunk_rows(self._sample_rng.sample(range(int(self._grid[0].shape[0])), self.P))
 
     def sensitivity(self, theta: torch.Tensor, pts=None, sigma=None) -> torch.Tensor:
         """vihmc_sensitivity: sigma^2 * mean over outputs of (d f / d theta)^2 for all D parameters, flat

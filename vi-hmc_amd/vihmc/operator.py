@@ -170,26 +170,34 @@ def define_model_log_prob(model, model_loss, tr_data, tau_list, tau_out, predict
         mu = np.zeros(spec.n_params, np.float32)
         grad_ind = np.arange(spec.n_params)
     grad_ind = np.asarray(grad_ind, np.int64)
-    if getattr(cfg, "sample_data", False) and not predict:
-        raise NotImplementedError("cfg.sample_data (random trunk subsampling per evaluation) is not supported")
     x1, x2, y = tr_data
     pm, ps = _prior_from_tau_list(cfg, tau_list, grad_ind.size)
     loss = model_loss
     if loss not in ("NLL", "regression"):
         raise NotImplementedError(f"model_loss {model_loss!r}")
-    eng = DeepONetEngine(spec, np.asarray(torch.as_tensor(x1).cpu()).reshape(-1, spec.in_branch),
-                         trunk_features(torch.as_tensor(x2).cpu()), np.asarray(torch.as_tensor(y).cpu()), mu,
-                         grad_ind, pm, ps, loss, tau_out, prior_scale, max_chains=max_chains, device=_device(device))
+    xb = np.asarray(torch.as_tensor(x1).cpu()).reshape(-1, spec.in_branch)
+    feats, yy = trunk_features(torch.as_tensor(x2).cpu()), np.asarray(torch.as_tensor(y).cpu())
+    # cfg.sample_data (:127-137): every non-predict evaluation sees cfg.p trunk rows drawn with random.sample
+    p_sub = int(cfg.p) if getattr(cfg, "sample_data", False) and not predict else None
+    if p_sub is not None and not 0 < p_sub <= feats.shape[0]:
+        raise ValueError(f"cfg.p={p_sub} must be in [1, {feats.shape[0]}] (the trunk grid size)")
+
+    def build(w, dev):
+        e = DeepONetEngine(spec, xb, feats if p_sub is None else feats[:p_sub],
+                           yy if p_sub is None else yy[:, :p_sub], w, grad_ind, pm, ps, loss, tau_out, prior_scale,
+                           max_chains=max_chains, device=dev)
+        if p_sub is not None:
+            e.sample_data(feats, yy, p_sub)
+        return e
+
+    eng = build(mu, _device(device))
 
     def resample():
-        nonlocal eng
         if sigma is None:
             return
         w = torch.normal(torch.as_tensor(mu), torch.as_tensor(sigma)).numpy()
         eng.close()
-        new = DeepONetEngine(spec, np.asarray(torch.as_tensor(x1).cpu()).reshape(-1, spec.in_branch),
-                             trunk_features(torch.as_tensor(x2).cpu()), np.asarray(torch.as_tensor(y).cpu()), w,
-                             grad_ind, pm, ps, loss, tau_out, prior_scale, max_chains=max_chains, device=eng.device)
+        new = build(w, eng.device)
         eng.__dict__.update(new.__dict__)
         new._plan = None                      # ownership moved into `eng`
 
