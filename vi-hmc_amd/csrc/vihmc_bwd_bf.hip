@@ -57,10 +57,15 @@ constexpr int B2_SLOTS = 7;                            // staged float4 per stag
 constexpr int B2_WS_D = (BB_SUB * 25 + 63) / 64;       // wave-slots of D items (13)
 
 __device__ __forceinline__ float act_grad_bf(int act, float h) {
+#pragma clang fp contract(off)
     // derivative from the activation's output (tanh: 1 - h^2, relu: h > 0), as act_grad_from_out_l
-    if (act == ACT_TANH) return 1.f - h * h;
+    if (act == ACT_TANH) return 1.f - h * h;   // h * h rounded first (no fused multiply-add)
     if (act == ACT_RELU) return h > 0.f ? 1.f : 0.f;
     return 1.f;
+}
+__device__ __forceinline__ float tanh_grad(float h) {
+#pragma clang fp contract(off)
+    return 1.f - h * h;                                // h * h rounded first (no fused multiply-add)
 }
 }  // namespace
 
@@ -309,7 +314,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float hv = ((float)hq[2][r] + (float)hq[1][r]) + (float)hq[0][r];
-                        o[r] = acc[u][r] * (TANH ? 1.f - hv * hv : act_grad_bf(P.act, hv));
+                        o[r] = acc[u][r] * (TANH ? tanh_grad(hv) : act_grad_bf(P.act, hv));
                     }
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bf6::u32x4, o), drs, off, 0, 0);
                 }

@@ -77,6 +77,31 @@ hipError_t launch_bwd(const BwdArgs& a, int nti, hipStream_t s);
 bool bwd_bf_ok(const BwdArgs& a);                       // k_bwd_bf handles every problem of the launch
 hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s);
 
+// Whole-network backward in one launch for chunks of 64 rows (vihmc_bwd_chain.hip): every layer of both nets,
+// the deltas on chip, the same partial slabs as the per-layer k_bwd_bf2 launches. W_j from the bf16x6 forward's
+// pre-split weight image of layer j (index j - 1 of the net's images).
+constexpr int BWD_CHAIN_MAXL = 12;
+struct BwdChainLayer {
+    const float* H; int64_t h_cs; int32_t ldh;    // h_{j-1} rows (j >= 1) or the net input (j = 0)
+    int32_t n_in, n_out;
+    int32_t act;                                  // activation of layer j - 1 (j >= 1)
+    int64_t part_off; int32_t part_stride;        // layer j's partial slabs inside the net's dwpart
+};
+struct BwdChainNet {
+    BwdChainLayer L[BWD_CHAIN_MAXL];
+    int32_t nl, M, n_wg;                          // n_wg = ceil(M / 64) workgroups per chain
+    const float* D; int64_t d_cs; int32_t ldd;    // delta of the top layer (dZ) [M][ldd]
+    float* dwpart; int64_t dwpart_cs;
+    const unsigned char* wimg; int64_t wimg_cs;   // the net's weight images (layers 1 .. nl - 1)
+};
+struct BwdChainArgs {
+    BwdChainNet net[2];
+    int32_t C;
+};
+bool bwd_chain_ok(const BwdChainArgs& a);
+hipError_t launch_bwd_chain(const BwdChainArgs& a, hipStream_t s);
+int bwd_chain_rows();
+
 // ---------------------------------------------------------------------------------------------
 // Fused branch x trunk contraction with the Gaussian likelihood, owner form.
 //   S[q][o] = sum_k Q[q][k] * Own[o][k] + b0;  r = S - Y[q][o];  G = gscale * r
@@ -106,6 +131,7 @@ struct ContractProb {
                                           //    operands, six products (k_contract_bf)
     const unsigned char* qimg; int64_t qimg_cs;   // bf16x6: Q pre-split into blocks (launch_split_blocks)
     float gscale;
+    int32_t rev_chains;                   // side B: > 0 = chain count, workgroups take the chains last first
 };
 
 // launchers (vihmc_kernels.hip)

@@ -142,7 +142,11 @@ struct vihmc_plan {
     int64_t wimg_cs = 0;
     int fwd_wimg = 1;
     int fuse_scatter = 1;       // plan option: trajectory evaluations take theta already scattered by the leapfrog
-    int mlp_fast = 1;           // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
+    int mlp_fast = 1;
+    int contract_rev = 0;
+    int bwd_chain = 1;            // option bwd_chain: whole-network backward in one launch when the chunks are 64 rows
+    bool wimg_live = false;
+    bool last_bwd_chain = false;  // the last gradient evaluation ran k_bwd_chain (get_option bwd_chain: bit 1)       // this evaluation's forward staged the weight images (they hold this theta)           // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
     int graph_on = -1;          // -1: follow VIHMC_GRAPH
     // hidden-layer forward products as exact 3-way bf16 splits (6 bf16 MFMA products, fp32 accumulate;
@@ -444,6 +448,9 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             const int64_t r_b = p->nets[0].rows, r_t = p->nets[1].rows;
             int64_t R = std::max<int64_t>(sub, (cdiv((int64_t)C * rows_all, slots) + sub - 1) / sub * sub);
             while ((int64_t)C * (cdiv(r_b, R) + cdiv(r_t, R)) > slots && R < rows_all) R += sub;
+            // the whole-network backward (k_bwd_chain) runs 64-row chunks: taken whenever they still fit one round
+            const int64_t rc = bwd_chain_rows();
+            if (p->bwd_bf16x6 && R < rc && (int64_t)C * (cdiv(r_b, rc) + cdiv(r_t, rc)) <= slots) R = rc;
             n.rows_per_chunk = (int)R;
         }
         int64_t po = 0;
@@ -627,6 +634,7 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
             a.net[1].wimg = p->wimg + (int64_t)a.net[0].nl * FWD_WIMG;
             a.net[0].wimg_cs = a.net[1].wimg_cs = p->wimg_cs;
             if (!p->img_by_scatter) HIPCHK(launch_split_wimg(a, s));
+            p->wimg_live = true;
         }
         HIPCHK(launch_fwd_fused_bf(a, nwb, s));
         return 0;
@@ -755,6 +763,40 @@ int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* 
     return 0;
 }
 
+// k_bwd_chain's arguments when this plan's backward chunks are its 64 rows in every layer of both nets
+bool bwd_chain_args(vihmc_plan* p, int C, BwdChainArgs& a) {
+    a.C = C;
+    for (int net = 0; net < 2; ++net) {
+        Net& n = p->nets[net];
+        BwdChainNet& cn = a.net[net];
+        cn.nl = (int)n.L.size();
+        if (cn.nl > BWD_CHAIN_MAXL) return false;
+        cn.M = n.rows;
+        cn.n_wg = cdiv(n.rows, bwd_chain_rows());
+        cn.D = n.delta[0];
+        cn.d_cs = n.delta_cs;
+        cn.ldd = n.L.back().ldo;
+        cn.dwpart = n.dwpart;
+        cn.dwpart_cs = n.dwpart_cs;
+        cn.wimg = p->wimg + (net ? (int64_t)(p->nets[0].L.size() - 1) * FWD_WIMG : 0);
+        cn.wimg_cs = p->wimg_cs;
+        for (int j = 0; j < cn.nl; ++j) {
+            const LayerPk& L = n.L[j];
+            if (L.rows_per_chunk != bwd_chain_rows() || L.n_chunks != cn.n_wg) return false;
+            BwdChainLayer& q = cn.L[j];
+            q.H = j == 0 ? n.input : n.act + n.h_off[j - 1];
+            q.h_cs = j == 0 ? 0 : n.act_cs;
+            q.ldh = L.ldi;
+            q.n_in = L.n_in;
+            q.n_out = L.n_out;
+            q.act = j >= 1 ? n.L[j - 1].act : 0;
+            q.part_off = L.part_off;
+            q.part_stride = (int32_t)L.part_stride;
+        }
+    }
+    return bwd_chain_ok(a);
+}
+
 int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
                        hipStream_t s, const LeapArgs* leap) {
     const ScatterImg si = scatter_img(p);
@@ -764,6 +806,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     // the pre-split contraction images (bf16x6 sides, gradient evaluations) are written by the fused forward
     // when it runs; otherwise k_split_blocks makes them below
     p->img_by_fwd = false;
+    p->wimg_live = false;
     if (int rc = deeponet_forward_layers(p, C, s, want_grad && p->contract_bf16x6 && p->W == 100)) return rc;
     int stats_waves = 0;
     {
@@ -801,6 +844,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         q.qimg = p->qsplitB;
         q.qimg_cs = p->qsplitB_cs;
         q.xcd_group = ((int64_t)C * p->qchunksB) % 8 == 0 ? 1 : 0;
+        q.rev_chains = p->contract_rev ? C : 0;
         q.b0 = p->packed;
         q.b0_cs = p->dp;
         q.out = p->partB;
@@ -834,7 +878,11 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         // the recorded time includes the maxl - 1 kernel boundaries between them
         hipEvent_t bwd_stop = nullptr;
         if (int rc = p->timing_begin(VIHMC_T_BWD, s, &bwd_stop, maxl)) return rc;
-        for (int i = 0; i < maxl; ++i) {
+        BwdChainArgs ca{};
+        const bool chain = p->bwd_chain && p->bwd_bf16x6 && p->wimg_live && bwd_chain_args(p, C, ca);
+        if (chain) HIPCHK(launch_bwd_chain(ca, s));
+        p->last_bwd_chain = chain;
+        for (int i = 0; i < (chain ? 0 : maxl); ++i) {
             BwdArgs ba{};
             ba.C = C;
             int nti = 1;
@@ -1375,7 +1423,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, contract_rev, bwd_chain"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1388,6 +1436,8 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "fuse_scatter") p->fuse_scatter = value ? 1 : 0;
     else if (k == "img_scatter") p->img_by_scatter = value && p->smap_img;   // 0: split the images per evaluation
     else if (k == "mlp_fast") p->mlp_fast = value ? 1 : 0;
+    else if (k == "contract_rev") p->contract_rev = value ? 1 : 0;
+    else if (k == "bwd_chain") p->bwd_chain = value ? 1 : 0;
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     // captured graphs embed the kernel choice
     for (auto& g : p->graphs) (void)hipGraphExecDestroy(g.second);
@@ -1406,6 +1456,8 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "fuse_scatter") *value = p->fuse_scatter;
     else if (k == "img_scatter") *value = p->img_by_scatter ? 1 : 0;
     else if (k == "mlp_fast") *value = p->mlp_fast && p->kind == 1 && mlp_bnn_fast_ok(p->mlp);
+    else if (k == "contract_rev") *value = p->contract_rev;
+    else if (k == "bwd_chain") *value = p->bwd_chain | (p->last_bwd_chain ? 2 : 0);
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
 }

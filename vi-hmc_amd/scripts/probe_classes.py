@@ -25,12 +25,16 @@ def main():
     ap.add_argument("--chains", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--opt", action="append", default=[], help="plan option key=value (repeatable)")
     args = ap.parse_args()
     spec = DeepONetSpec()
     prob = deeponet_problem(seed=0)
     C = args.chains
     eng = DeepONetEngine(spec, prob.branch_in, trunk_features(prob.trunk_in), prob.y, prob.mu, prob.grad_ind, 0.0, 0.1,
                          "NLL", 1.0, max_chains=C, device="cuda:0")
+    for kv in args.opt:
+        k, v = kv.split("=")
+        eng.option(k, int(v))
     th = torch.tensor(np.tile(prob.mu[prob.grad_ind], (C, 1)), device="cuda:0")
     th += 0.001 * torch.randn_like(th)
     for _ in range(5):
