@@ -383,21 +383,15 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         };
         if (ntj == 7) dw_run(std::integral_constant<int, 7>{});
         else dw_run(std::integral_constant<int, 0>{});
+        // the tiled partial slab (bwd_tile_off): each accumulator quad as it stands, one 1-KB store per tile
         float* part = P.part + c * P.part_cs + (int64_t)wg * P.part_stride;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
             const int tn = s2 == 0 ? rta : rtb;
 #pragma unroll
             for (int t = 0; t < 7; ++t) {
-                const int j = 16 * t + lr;
-                if (t >= ntj || j > NI4 || (s2 == 1 && (t < cb0 || t >= cb1))) continue;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int n = 16 * tn + 4 * lg + r;
-                    if (n >= P.n_out) continue;
-                    if (j == NI4) part[(int64_t)P.n_out * NI4 + n] = acc[s2][t][r];     // db
-                    else part[(int64_t)n * NI4 + j] = (j < P.n_in) ? acc[s2][t][r] : 0.f;
-                }
+                if (t >= ntj || (s2 == 1 && (t < cb0 || t >= cb1))) continue;
+                if (tn < 6 || lg == 0) *reinterpret_cast<f32x4*>(part + bwd_tile_off(tn, t, ntj, lane)) = acc[s2][t];
             }
         }
     }

@@ -66,6 +66,22 @@ __device__ __forceinline__ float act_grad(int act, float h) {
 }
 }  // namespace
 
+#ifndef CH_STAMP
+#define CH_STAMP 0        // timing-only instrumentation (variant builds): in-kernel phase stamps
+#endif
+#if CH_STAMP
+// every 8th workgroup (the first 16 of them): per wave and layer, s_memtime after barrier A [0], after A2 [1], when
+// the compute phase is done [2], after barrier B [3], when the write phase is done [4]; per workgroup s_memtime /
+// s_memrealtime at start and end (scripts/diag/stamps_chain.py)
+constexpr int CHS_WG = 16;
+__device__ unsigned long long ch_stamps[CHS_WG][12][BWD_CHAIN_MAXL][5];
+__device__ unsigned long long ch_real[CHS_WG][2][2];
+#define VIHMC_CH_STAMP(J, K) \
+    if (samp && lane == 0) ch_stamps[sidx][wave][(J)][(K)] = __builtin_amdgcn_s_memtime();
+#else
+#define VIHMC_CH_STAMP(J, K)
+#endif
+
 __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
     int b = blockIdx.x;
@@ -80,6 +96,14 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
     const int M = N.M;
     const int nl = N.nl;
     const unsigned char* wimg = N.wimg + c * N.wimg_cs;
+#if CH_STAMP
+    const bool samp = (blockIdx.x % 8) == 0 && blockIdx.x / 8 < CHS_WG;
+    const int sidx = blockIdx.x / 8;
+    if (samp && tid == 0) {
+        ch_real[sidx][0][0] = __builtin_amdgcn_s_memtime();
+        ch_real[sidx][0][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 
     // rows [r0, r0 + 64) of a [M][ld] fp32 matrix, float4 item e = row * q + c4 -> (global byte offset, LDS plane
     // offset); rows past M read 0 through the buffer resource
@@ -154,6 +178,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
             wtr[u] = (uint32_t)(CH_W + (8 * lg + (lr >> 2)) * CH_PITCH + 2 * img_pos(16 * (t0 + u) + 4 * (lr & 3)));
         for (int j = nl - 1; j >= 0; --j) {
             __syncthreads();                           // A: delta_j, h_{j-1}, W_j in LDS
+            VIHMC_CH_STAMP(j, 0)
             const bool dx = j >= 1;
             bf16x8 wf[2][3][3];                        // [u][kb][plane]
             float wt[2] = {0.f, 0.f};
@@ -177,6 +202,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                 }
             }
             __syncthreads();                           // A2: the W buffer is free (the dW waves refill it)
+            VIHMC_CH_STAMP(j, 1)
             // the next layer's h rows (h_{j-2}, or the net input when j = 1) into registers, stored after B
             f32x4 hx[CH_HSLOTS];
             uint32_t hl[CH_HSLOTS];
@@ -240,7 +266,12 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                     }
                 }
             }
+#if CH_STAMP
+            if (dx) asm volatile("" :: "v"(o[0][0]), "v"(o[1][0]));
+#endif
+            VIHMC_CH_STAMP(j, 2)
             __syncthreads();                           // B: every read of delta_j / h_{j-1} done
+            VIHMC_CH_STAMP(j, 3)
             if (dx) {
 #pragma unroll
                 for (int s = 0; s < 2; ++s)
@@ -256,6 +287,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                 for (int v = 0; v < CH_HSLOTS; ++v) store_planes(sm + CH_HP + hl[v], hx[v]);
                 db_column(4 * hq_n, tid);
             }
+            VIHMC_CH_STAMP(j, 4)
         }
     } else {
         // ---------------- dW role (and the staging of the next layer) ----------------
@@ -268,10 +300,12 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
         const int tro = bf6::tr_lane_off(lr, lg);
         for (int j = nl - 1; j >= 0; --j) {
             __syncthreads();                           // A
+            VIHMC_CH_STAMP(j, 0)
             const BwdChainLayer& L = N.L[j];
             const int NI4 = (L.n_in + 3) & ~3;
             const int ntj = __builtin_amdgcn_readfirstlane((NI4 + 16) >> 4);
             __syncthreads();                           // A2: the dX waves hold their W fragments
+            VIHMC_CH_STAMP(j, 1)
             if (j >= 2) dma_image(j - 1, g, 4);       // the next layer's image (layers >= 1)
             // weight gradient of layer j over the 64 rows (k = the rows, two 32-row blocks)
             f32x4 acc[2][7];
@@ -299,29 +333,44 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                     if (t >= cb0 && t < cb1) acc[1][t] = six(da[1], hb[t & 1], acc[1][t]);
                 }
             }
+#if CH_STAMP
+            asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][6]));
+#endif
+            VIHMC_CH_STAMP(j, 2)
             if (j >= 2) bf6::wait_vmcnt0();            // the image DMA landed
             __syncthreads();                           // B
-            // the partial slab of layer j (k_bwd_bf2's layout)
+            VIHMC_CH_STAMP(j, 3)
+            // the tiled partial slab of layer j (bwd_tile_off, as k_bwd_bf2): one 1-KB store per tile
             float* part = N.dwpart + c * N.dwpart_cs + L.part_off + (int64_t)wg * L.part_stride;
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const int tn = s2 == 0 ? rta : rtb;
 #pragma unroll
                 for (int t = 0; t < 7; ++t) {
-                    const int jj = 16 * t + lr;
-                    if (t >= ntj || jj > NI4 || (s2 == 1 && (t < cb0 || t >= cb1))) continue;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int n = 16 * tn + 4 * lg + r;
-                        if (n >= 100) continue;
-                        if (jj == NI4) part[(int64_t)100 * NI4 + n] = acc[s2][t][r];
-                        else part[(int64_t)n * NI4 + jj] = (jj < L.n_in) ? acc[s2][t][r] : 0.f;
-                    }
+                    if (t >= ntj || (s2 == 1 && (t < cb0 || t >= cb1))) continue;
+                    if (tn < 6 || lg == 0) *reinterpret_cast<f32x4*>(part + bwd_tile_off(tn, t, ntj, lane)) = acc[s2][t];
                 }
             }
+            VIHMC_CH_STAMP(j, 4)
         }
     }
+#if CH_STAMP
+    __syncthreads();
+    if (samp && tid == 0) {
+        ch_real[sidx][1][0] = __builtin_amdgcn_s_memtime();
+        ch_real[sidx][1][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
+
+#if CH_STAMP
+extern "C" int vihmc_debug_ch_stamps(void* stamps, size_t stamp_bytes, void* real, size_t real_bytes) {
+    if (stamp_bytes != sizeof(ch_stamps) || real_bytes != sizeof(ch_real)) return -1;
+    hipError_t e = hipMemcpyFromSymbol(stamps, HIP_SYMBOL(ch_stamps), stamp_bytes, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(real, HIP_SYMBOL(ch_real), real_bytes, 0, hipMemcpyDeviceToHost);
+    return (int)e;
+}
+#endif
 
 bool bwd_chain_ok(const BwdChainArgs& a) {
     for (int net = 0; net < 2; ++net) {
@@ -347,5 +396,8 @@ hipError_t launch_bwd_chain(const BwdChainArgs& a, hipStream_t s) {
 }
 
 int bwd_chain_rows() { return CH_ROWS; }
+
+// timing-only / instrumentation switches this translation unit was built with (0 = product build)
+int diag_switches_bwd_chain() { return CH_STAMP << 8; }
 
 }  // namespace vihmc

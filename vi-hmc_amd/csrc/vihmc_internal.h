@@ -162,7 +162,17 @@ hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, 
 struct ReduceJob {
     const float* src; int64_t in_cs; int64_t part_stride; int32_t n_parts; int32_t len;
     float* dst; int64_t dst_cs;
+    // tiled = 1: the slabs hold the bf16x6 backward's dW accumulator tiles as they stand (bwd_tile_off), len = the
+    // tiled slab's floats; the sums are scattered to dst = [n_out][ldi] weights + [n_out] bias (the db column NI4)
+    int32_t tiled, ntj, n_out, n_in, ldi;
 };
+// Tiled dW partial slab of the bf16x6 backward kernels: 16x16 tiles (row tile tn of the outputs n, column tile t of
+// the inputs j, t < ntj), lane-major float4 quads (lane l = 16 lg + lr holds rows n = 16 tn + 4 lg + r, column
+// j = 16 t + lr): tile (tn < 6, t) at (tn ntj + t) 256 floats, row tile 6 (n 96..111) keeps only its lg = 0 lanes.
+constexpr int bwd_tile_floats(int ntj) { return 6 * ntj * 256 + ntj * 64; }
+__host__ __device__ inline int bwd_tile_off(int tn, int t, int ntj, int lane) {
+    return tn < 6 ? (tn * ntj + t) * 256 + 4 * lane : 6 * ntj * 256 + t * 64 + 4 * lane;
+}
 // Likelihood statistics of the contraction (k_contract_stats): ll from the per-wave (sum r^2, sum G) pairs and
 // d ll / d b0 into packed slot 0 of gp. Optionally run as one extra grid slice of the weight-gradient reduce.
 struct StatsJob {
@@ -245,6 +255,7 @@ int diag_switches_fused();
 int diag_switches_contract_bf();
 int diag_switches_bwd_bf();
 int diag_switches_layers();
+int diag_switches_bwd_chain();
 int diag_switches();
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, int nw, hipStream_t s);     // bf16x6, 12 (or 4) waves

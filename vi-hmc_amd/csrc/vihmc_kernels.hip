@@ -144,7 +144,100 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
     }
     const ReduceJob J = jobs[blockIdx.y];
     const int c = blockIdx.z;
-    const bool vec = ((J.len | J.part_stride | J.in_cs | J.dst_cs) & 3) == 0 &&
+    if (J.tiled) {
+        // float4 quads of the tiled slabs (one accumulator quad of a dW tile each), summed over the slabs in the
+        // row-major paths' fixed orders -- so both layouts give bitwise equal gradients -- then scattered to the
+        // row-major destination
+        __shared__ float4 tsum[3][64];
+        const bool grouped = J.n_parts >= REDUCE_GROUP_MIN;
+        const int x = grouped ? (int)(threadIdx.x & 63) : (int)threadIdx.x, g = grouped ? (int)(threadIdx.x >> 6) : 0;
+        const int q = grouped ? (int)blockIdx.x * 64 + x : (int)blockIdx.x * 256 + x;
+        if (grouped && (int)blockIdx.x * 256 >= J.len) return;   // block-uniform
+        const bool ok = 4 * q < J.len;
+        if (!grouped && !ok) return;
+        const float* sp = J.src + c * J.in_cs + (ok ? 4 * q : 0);
+        const int64_t st = J.part_stride;
+        const int n = ok ? J.n_parts : 0;
+        float4 s = {0.f, 0.f, 0.f, 0.f};
+        if (grouped) {
+            int p = g;
+            for (; p + 28 < n; p += 32) {
+                float4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(sp + (p + 4 * u) * st);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    s.x += v[u].x;
+                    s.y += v[u].y;
+                    s.z += v[u].z;
+                    s.w += v[u].w;
+                }
+            }
+            for (; p < n; p += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(sp + p * st);
+                s.x += v.x;
+                s.y += v.y;
+                s.z += v.z;
+                s.w += v.w;
+            }
+            if (g > 0) tsum[g - 1][x] = s;
+            __syncthreads();
+            if (g != 0 || !ok) return;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s.x += tsum[k][x].x;
+                s.y += tsum[k][x].y;
+                s.z += tsum[k][x].z;
+                s.w += tsum[k][x].w;
+            }
+        } else {
+            int p = 0;
+            for (; p + 8 <= n; p += 8) {
+                float4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(sp + (p + u) * st);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    s.x += v[u].x;
+                    s.y += v[u].y;
+                    s.z += v[u].z;
+                    s.w += v[u].w;
+                }
+            }
+            for (; p < n; ++p) {
+                const float4 v = *reinterpret_cast<const float4*>(sp + p * st);
+                s.x += v.x;
+                s.y += v.y;
+                s.z += v.z;
+                s.w += v.w;
+            }
+        }
+        // quad -> (row tile, column tile, lane) -> rows n = 16 tn + 4 lg + r, column j = 16 t + lr
+        const int f = 4 * q, big = 6 * J.ntj * 256;
+        int tn, t, lane;
+        if (f < big) {
+            const int T = f >> 8;
+            tn = T / J.ntj;
+            t = T - tn * J.ntj;
+            lane = (f & 255) >> 2;
+        } else {
+            tn = 6;
+            t = (f - big) >> 6;
+            lane = ((f - big) & 63) >> 2;
+        }
+        const int j = 16 * t + (lane & 15), ni4 = (J.n_in + 3) & ~3;
+        float* d = J.dst + c * J.dst_cs;
+        const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int nn = 16 * tn + 4 * (lane >> 4) + r;
+            if (nn >= J.n_out) continue;
+            if (j < ni4) d[(int64_t)nn * J.ldi + j] = j < J.n_in ? sv[r] : 0.f;
+            else if (j == ni4) d[(int64_t)J.n_out * J.ldi + nn] = sv[r];
+        }
+        return;
+    }
+    const bool vec =((J.len | J.part_stride | J.in_cs | J.dst_cs) & 3) == 0 &&
                      ((reinterpret_cast<uintptr_t>(J.src) | reinterpret_cast<uintptr_t>(J.dst)) & 15) == 0;
     if (vec && J.n_parts >= REDUCE_GROUP_MIN) {
         // many slabs (the weight-gradient partials of a one-chain plan: ~160 row chunks per trunk layer): the block's

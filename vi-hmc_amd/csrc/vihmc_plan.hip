@@ -113,7 +113,8 @@ struct vihmc_plan {
     int64_t stats_cs = 0;
     int nwavesA = 0;
     ReduceJob* jobsB = nullptr;
-    ReduceJob* jobsW = nullptr;
+    ReduceJob* jobsW = nullptr;      // dW partial reduces: row-major slabs (fp32 backward)
+    ReduceJob* jobsWt = nullptr;     // ... tiled slabs for the layers the bf16x6 backward kernels run
     int n_jobsW = 0, max_lenW = 0, lenB = 0;
 
     std::vector<int32_t> fmap_host;    // flat parameter index -> packed offset (sensitivity output map)
@@ -214,7 +215,8 @@ struct vihmc_plan {
 
 namespace vihmc {
 int diag_switches() {
-    return diag_switches_fused() | diag_switches_contract_bf() | diag_switches_bwd_bf() | diag_switches_layers();
+    return diag_switches_fused() | diag_switches_contract_bf() | diag_switches_bwd_bf() | diag_switches_layers() |
+           diag_switches_bwd_chain();
 }
 }  // namespace vihmc
 
@@ -463,7 +465,8 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             L.rows_per_chunk = n.rows_per_chunk;
             if (j == 0 && L.n_in >= 64) L.rows_per_chunk = std::min(n.rows_per_chunk, 128);
             L.n_chunks = cdiv(n.rows, L.rows_per_chunk);
-            L.part_stride = r4((int64_t)L.n_out * L.ldi + L.n_out);
+            // row-major (fp32 backward) or tiled (bf16x6 backward kernels, bwd_tile_off) slabs: room for either
+            L.part_stride = r4(std::max<int64_t>((int64_t)L.n_out * L.ldi + L.n_out, bwd_tile_floats((L.ldi + 16) >> 4)));
             L.part_off = po;
             po += L.part_stride * L.n_chunks;
         }
@@ -527,10 +530,37 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             const ReduceJob both[2] = {jb, ja};
             if (int rc = p->upload(&p->jobsA, both, 2)) return rc;
         }
-        std::vector<ReduceJob> jw;
+        // two job lists over the same slabs: row-major (fp32 backward) and, for the layers the bf16x6 kernels run
+        // (bwd_bf_ok per launch: layer i from the top of both nets), tiled
+        std::vector<ReduceJob> jw, jt;
+        std::vector<char> tiled[2];
+        for (int net = 0; net < 2; ++net) tiled[net].assign(p->nets[net].L.size(), 0);
+        const int maxl = (int)std::max(p->nets[0].L.size(), p->nets[1].L.size());
+        for (int i = 0; i < maxl; ++i) {
+            BwdArgs ba{};
+            int js[2] = {-1, -1};
+            for (int net = 0; net < 2; ++net) {
+                const Net& n = p->nets[net];
+                const int j = (int)n.L.size() - 1 - i;
+                if (j < 0) continue;
+                js[net] = j;
+                const LayerPk& L = n.L[j];
+                BwdProb& q = ba.p[ba.nprob++];
+                q.ldd = q.ldw = L.ldo;
+                q.ldh = L.ldi;
+                q.n_out = L.n_out;
+                q.n_in = L.n_in;
+                q.has_dx = j >= 1;
+                q.rows_per_wg = L.rows_per_chunk;
+            }
+            if (bwd_bf_ok(ba))
+                for (int net = 0; net < 2; ++net)
+                    if (js[net] >= 0) tiled[net][js[net]] = 1;
+        }
         for (int net = 0; net < 2; ++net) {
             Net& n = p->nets[net];
-            for (auto& L : n.L) {
+            for (size_t li = 0; li < n.L.size(); ++li) {
+                const LayerPk& L = n.L[li];
                 ReduceJob j{};
                 j.src = n.dwpart + L.part_off;
                 j.in_cs = n.dwpart_cs;
@@ -541,10 +571,21 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
                 j.dst_cs = p->dp;
                 p->max_lenW = std::max(p->max_lenW, j.len);
                 jw.push_back(j);
+                if (tiled[net][li]) {
+                    j.tiled = 1;
+                    j.ntj = (L.ldi + 16) >> 4;
+                    j.len = bwd_tile_floats(j.ntj);
+                    j.n_out = L.n_out;
+                    j.n_in = L.n_in;
+                    j.ldi = L.ldi;
+                    p->max_lenW = std::max(p->max_lenW, j.len);
+                }
+                jt.push_back(j);
             }
         }
         p->n_jobsW = (int)jw.size();
         if (int rc = p->upload(&p->jobsW, jw.data(), (int64_t)jw.size())) return rc;
+        if (int rc = p->upload(&p->jobsWt, jt.data(), (int64_t)jt.size())) return rc;
     }
     // weight images maintained by the scatter (after the activation layout, which fused_args reads)
     if (p->wimg)
@@ -924,7 +965,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
             }
         }
         if (bwd_stop) HIPCHK(hipEventRecord(bwd_stop, s));
-        HIPCHK(launch_reduce(p->jobsW, p->n_jobsW, p->max_lenW, C, s, &stats_job));
+        HIPCHK(launch_reduce(p->bwd_bf16x6 ? p->jobsWt : p->jobsW, p->n_jobsW, p->max_lenW, C, s, &stats_job));
     }
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
                                p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, s,
@@ -1474,7 +1515,8 @@ const char* vihmc_version(void) {
     static std::string v = "vihmc 0.2.0 gfx950 diag=" + std::to_string(vihmc::diag_switches_fused()) + "," +
                            std::to_string(vihmc::diag_switches_contract_bf()) + "," +
                            std::to_string(vihmc::diag_switches_bwd_bf()) + "," +
-                           std::to_string(vihmc::diag_switches_layers());
+                           std::to_string(vihmc::diag_switches_layers()) + "," +
+                           std::to_string(vihmc::diag_switches_bwd_chain());
     return v.c_str();
 }
 
