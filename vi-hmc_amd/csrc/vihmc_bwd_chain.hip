@@ -5,19 +5,18 @@
 // torch autograd through F.linear and tanh), layer j = nl-1 .. 0 of each net:
 //   delta_{j-1}[m][i] = (sum_n delta_j[m][n] W_j[n][i]) * act'(h_{j-1}[m][i])        (j >= 1)
 //   part_j[n][i] = sum_m delta_j[m][n] h_{j-1}[m][i],  part_j[n_out][n] = sum_m delta_j[m][n]
-// with the same partial-slab layout as k_bwd_bf2 (reduced by the same k_reduce jobs), so the two paths are
-// interchangeable per evaluation and bitwise equal: every product and every accumulation order is k_bwd_bf2's.
+// with k_bwd_bf2's tiled partial slabs (reduced by the same k_reduce jobs), so the two paths are interchangeable
+// per evaluation and bitwise equal: every product and every accumulation order is k_bwd_bf2's.
 //
 // One 768-thread workgroup (8 dX + 4 dW waves, 3 per SIMD) per 64-row chunk of one net of one chain -- the
-// plan's chunk when a single chain's rows fill the chip in one round (C = 1: 16 + 160 workgroups). LDS (151 KB):
+// plan's chunk when a single chain's rows fill the chip in one round (C = 1: 16 + 160 workgroups). LDS (85 KB):
 //   2 sub-tiles x [delta_j planes [3][32][224 B] | h_{j-1} planes [3][32][224 B] | delta_j fp32 tail [32][4]]
-//   W_j: the forward's pre-split weight image (k_split_wimg: planes [3][100 n][112 permuted i]), one DMA copy
-//        per layer. dX reads it with transposed reads whose per-lane addresses undo the permutation and give
-//        the k order of the delta row reads; its n tail (rows 96..99) is rebuilt exactly from the planes.
-// Per layer: [A] the dX waves take their W fragments into registers; [A2] the dW waves start the DMA of the
-// next layer's image, the dX waves the loads of its h rows, then compute delta_{j-1} (kept in registers) while
-// the dW waves compute the weight gradient of both sub-tiles; [B] the dX waves split delta_{j-1} and the next h
-// rows into the planes, the dW waves store the partial slab; loop.
+// W_j^T never touches LDS: each dX wave keeps the fragments of its two input tiles in registers, loaded from the
+// pre-split W^T image (BWD_WTIMG, kept current by the scatter) right after its last MFMA of the layer before, so
+// they land while the workgroup writes the next deltas.
+// Per layer: [A] the dX waves issue the loads of the next h rows, compute delta_{j-1} (kept in registers) and
+// load the next W^T fragments, while the dW waves compute the weight gradient of both sub-tiles; [B] the dX waves
+// split delta_{j-1} and the next h rows into the planes, the dW waves store the partial slab; loop.
 #include "vihmc_internal.h"
 #include "vihmc_bf16x6.h"
 #include <type_traits>
@@ -28,9 +27,7 @@ namespace {
 using bf6::f32x4;
 using bf6::bf16x8;
 using bf6::bf16x4;
-using bf6::lds_bf16x4;
 using bf6::split4;
-using bf6::cat8;
 using bf6::six;
 using bf6::tr_frag;
 
@@ -42,20 +39,10 @@ constexpr int CH_DP = 0;
 constexpr int CH_HP = 3 * CH_PLANE;
 constexpr int CH_DT = 6 * CH_PLANE;
 constexpr int CH_BUF = CH_DT + CH_SUB * 16;            // 43520 per sub-tile
-constexpr int CH_W = 2 * CH_BUF;                       // 87040: the W image planes
-constexpr int CH_WPLANE = 100 * 224;                   // plane stride of the forward's image (fwd_img_plane_stride)
-constexpr int CH_WPIECES = (3 * CH_WPLANE + 1023) / 1024;   // 66 DMA pieces of 1 KB
-constexpr int CH_LDS = CH_W + CH_WPIECES * 1024;       // 154624
-static_assert(CH_LDS <= 160 * 1024 && CH_WPIECES * 1024 <= FWD_WIMG, "LDS / image");
+constexpr int CH_LDS = 2 * CH_BUF;                     // 87040
 static_assert(CH_BUF + 2 * CH_PLANE < 65536, "LDS store offsets fit the ds_write immediate");
 constexpr int CH_THREADS = 768;
 constexpr int CH_HSLOTS = 4;                           // h float4 per dX lane: 64 rows x <= 32 float4 / 512
-
-// image position of input column col (k_split_wimg's permuted order; fwd_img_plane_off)
-__device__ __forceinline__ int img_pos(int col) {
-    const int t = col >> 4, g = (col >> 2) & 3, e = col & 3;
-    return t < 6 ? (t >> 1) * 32 + g * 8 + (t & 1) * 4 + e : col;
-}
 
 // h * h rounded before the subtraction (no fused multiply-add), as k_bwd_bf2 computes it
 __device__ __forceinline__ float act_grad(int act, float h) {
@@ -70,8 +57,8 @@ __device__ __forceinline__ float act_grad(int act, float h) {
 #define CH_STAMP 0        // timing-only instrumentation (variant builds): in-kernel phase stamps
 #endif
 #if CH_STAMP
-// every 8th workgroup (the first 16 of them): per wave and layer, s_memtime after barrier A [0], after A2 [1], when
-// the compute phase is done [2], after barrier B [3], when the write phase is done [4]; per workgroup s_memtime /
+// every 8th workgroup (the first 16 of them): per wave and layer, s_memtime after barrier A [0], when the compute
+// phase is done [2], after barrier B [3], when the write phase is done [4] ([1] = [0]); per workgroup s_memtime /
 // s_memrealtime at start and end (scripts/diag/stamps_chain.py)
 constexpr int CHS_WG = 16;
 __device__ unsigned long long ch_stamps[CHS_WG][12][BWD_CHAIN_MAXL][5];
@@ -95,7 +82,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
     const int r0 = wg * CH_ROWS;
     const int M = N.M;
     const int nl = N.nl;
-    const unsigned char* wimg = N.wimg + c * N.wimg_cs;
+    const unsigned char* wtimg = N.wtimg + c * N.wtimg_cs;
 #if CH_STAMP
     const bool samp = (blockIdx.x % 8) == 0 && blockIdx.x / 8 < CHS_WG;
     const int sidx = blockIdx.x / 8;
@@ -130,12 +117,8 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
             *reinterpret_cast<unsigned short*>(o + 2 * CH_PLANE) = 0;
         }
     };
-    auto dma_image = [&](int j, int w0, int nw) {       // W_j's image (index j - 1) -> the W buffer
-        const unsigned char* src = wimg + (int64_t)(j - 1) * FWD_WIMG;
-        for (int k = w0; k < CH_WPIECES; k += nw) bf6::glds16_asm(src + k * 1024 + lane * 16, sm + CH_W + k * 1024);
-    };
 
-    // ---------------- prologue (all waves): delta of the top layer, h rows and W image of the top layer ------
+    // ---------------- prologue (all waves): delta of the top layer and its h rows ----------------
     {
         const int jt = nl - 1;
         const BwdChainLayer& L = N.L[jt];
@@ -144,7 +127,6 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
         const float* H = L.H + c * L.h_cs + (int64_t)r0 * L.ldh;
         const __amdgpu_buffer_rsrc_t drs = bf6::make_rsrc(D, (uint32_t)((M - r0) * N.ldd * 4));
         const __amdgpu_buffer_rsrc_t hrs = bf6::make_rsrc(H, (uint32_t)((M - r0) * L.ldh * 4));
-        if (jt >= 1 && wave >= 8) dma_image(jt, wave - 8, 4);
         for (int e = tid; e < CH_ROWS * 25; e += CH_THREADS) {
             uint32_t voff, loff;
             int c4, row;
@@ -161,136 +143,137 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
             store_planes(sm + CH_HP + loff, x);
         }
         db_column(4 * hq, tid);
-        if (jt >= 1 && wave >= 8) bf6::wait_vmcnt0();
     }
 
     if (wave < 8) {
         // ---------------- dX role: i-tiles {2 p2, 2 p2 + 1} x row half h of both sub-tiles ----------------
+        // instantiated per tile count (TWO) and activation (every hidden activation tanh, or any), so no branch
+        // splits the loads from the MFMAs; every global load of the loop is unconditional (clamped layer index),
+        // so hipcc's counted waits stay exact across the loop edge (the W^T fragments wait for themselves only)
         const int h = wave & 1, p2 = wave >> 1;
         const int t0 = 2 * __builtin_amdgcn_readfirstlane(p2);
-        const bool two = t0 + 1 < 7;                   // wave-uniform (p2 = 3: i-tile 6 only)
-        // transposed image reads: lane (qq = lr >> 2, pp = lr & 3) of group lg supplies image row 32 kb + 8 lg + qq
-        // (+ 4: the second read) at the position of input column 16 t + 4 pp, so result lane (lr, lg) holds
-        // W[32 kb + 8 lg + jj][16 t + lr], jj = 0..7: the k order of the delta rows' b128 reads
-        uint32_t wtr[2];
+        auto dx_run = [&](auto two_c, auto tanh_c) __attribute__((always_inline)) {
+            constexpr bool TWO = decltype(two_c)::value;
+            constexpr bool TANH = decltype(tanh_c)::value;
+            constexpr int NU = TWO ? 2 : 1;
+            // W_j^T fragments: lane (lr, lg) holds W^T[16 t + lr][32 kb + 8 lg + jj] (jj = 0..7, the k order of the
+            // delta rows' b128 reads) of every plane, and the exact fp32 n tail W^T[16 t + lr][96 + lg]
+            bf16x8 wf[NU][3][3];
+            float wt[NU];
+            auto load_w = [&](int jj) __attribute__((always_inline)) {
+                const unsigned char* ti = wtimg + (int64_t)(jj - 1) * BWD_WTIMG;
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-            wtr[u] = (uint32_t)(CH_W + (8 * lg + (lr >> 2)) * CH_PITCH + 2 * img_pos(16 * (t0 + u) + 4 * (lr & 3)));
-        for (int j = nl - 1; j >= 0; --j) {
-            __syncthreads();                           // A: delta_j, h_{j-1}, W_j in LDS
-            VIHMC_CH_STAMP(j, 0)
-            const bool dx = j >= 1;
-            bf16x8 wf[2][3][3];                        // [u][kb][plane]
-            float wt[2] = {0.f, 0.f};
-            if (dx) {
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    if (u == 1 && !two) break;
+                for (int u = 0; u < NU; ++u) {
+                    const int row = 16 * (t0 + u) + lr;
 #pragma unroll
                     for (int kb = 0; kb < 3; ++kb)
 #pragma unroll
-                        for (int p = 0; p < 3; ++p) {
-                            const unsigned char* a = sm + wtr[u] + p * CH_WPLANE + 32 * kb * CH_PITCH;
-                            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));
-                            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 4 * CH_PITCH));
-                            wf[u][kb][p] = cat8(lo, hi);
-                        }
-                    // n tail: W[96 + lg][16 t + lr], rebuilt exactly from the planes
-                    const __bf16* pl = reinterpret_cast<const __bf16*>(sm + CH_W + (96 + lg) * CH_PITCH) +
-                                       img_pos(16 * (t0 + u) + lr);
-                    wt[u] = ((float)pl[CH_WPLANE] + (float)pl[CH_WPLANE / 2]) + (float)pl[0];   // (x2 + x1) + x0
+                        for (int p = 0; p < 3; ++p)
+                            wf[u][kb][p] = *reinterpret_cast<const bf16x8*>(ti + p * BWD_WTPLANE + row * BWD_WTPITCH +
+                                                                            2 * (32 * kb + 8 * lg));
+                    wt[u] = *reinterpret_cast<const float*>(ti + BWD_WTTAIL + 4 * (row * 4 + lg));
                 }
-            }
-            __syncthreads();                           // A2: the W buffer is free (the dW waves refill it)
-            VIHMC_CH_STAMP(j, 1)
-            // the next layer's h rows (h_{j-2}, or the net input when j = 1) into registers, stored after B
-            f32x4 hx[CH_HSLOTS];
-            uint32_t hl[CH_HSLOTS];
-            int hq_n = 0;
-            if (dx) {
-                const BwdChainLayer& Ln = N.L[j - 1];
-                hq_n = (Ln.n_in + 3) >> 2;
-                const float* H = Ln.H + c * Ln.h_cs + (int64_t)r0 * Ln.ldh;
-                const __amdgpu_buffer_rsrc_t hrs = bf6::make_rsrc(H, (uint32_t)((M - r0) * Ln.ldh * 4));
-                const int tot = CH_ROWS * hq_n;
+            };
+            load_w(max(nl - 1, 1));
+            for (int j = nl - 1; j >= 0; --j) {
+                __syncthreads();                       // A: delta_j, h_{j-1} in LDS
+                VIHMC_CH_STAMP(j, 0)
+                VIHMC_CH_STAMP(j, 1)
+                const bool dx = j >= 1;
+                // the next layer's h rows (h_{j-2}, or the net input when j = 1) into registers, stored after B
+                f32x4 hx[CH_HSLOTS];
+                uint32_t hl[CH_HSLOTS];
+                const BwdChainLayer& Ln = N.L[max(j - 1, 0)];
+                const int hq_n = (Ln.n_in + 3) >> 2;
+                {
+                    const float* H = Ln.H + c * Ln.h_cs + (int64_t)r0 * Ln.ldh;
+                    const __amdgpu_buffer_rsrc_t hrs = bf6::make_rsrc(H, (uint32_t)((M - r0) * Ln.ldh * 4));
+                    const int tot = CH_ROWS * hq_n;
 #pragma unroll
-                for (int v = 0; v < CH_HSLOTS; ++v) {
-                    // wrapped: a lane past the end moves an item another lane moves too (same value, same address)
-                    const int e = (tid + 512 * v) % tot;
-                    uint32_t voff, loff;
-                    int c4, row;
-                    item_offsets(e, hq_n, Ln.ldh, voff, loff, c4, row);
-                    hl[v] = loff;
-                    hx[v] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hrs, voff, 0, 0));
-                }
-            }
-            f32x4 o[2][2];                             // [sub][u] delta_{j-1} of rows 32 sub + 16 h + lr
-            if (dx) {
-                const int act = N.L[j].act;
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const unsigned char* buf = sm + s * CH_BUF;
-                    const unsigned char* drow = buf + CH_DP + (16 * h + lr) * CH_PITCH + 16 * lg;
-                    const float dtl = reinterpret_cast<const float*>(buf + CH_DT)[(16 * h + lr) * 4 + lg];
-                    f32x4 ac[2];
-                    ac[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[0], dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                    ac[1] = two ? __builtin_amdgcn_mfma_f32_16x16x4f32(wt[1], dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0)
-                                : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                    for (int kb = 0; kb < 3; ++kb) {
-                        bf16x8 db[3];
-#pragma unroll
-                        for (int p = 0; p < 3; ++p) db[p] = *reinterpret_cast<const bf16x8*>(drow + p * CH_PLANE + 64 * kb);
-                        ac[0] = six(wf[0][kb], db, ac[0]);
-                        if (two) ac[1] = six(wf[1][kb], db, ac[1]);
+                    for (int v = 0; v < CH_HSLOTS; ++v) {
+                        // wrapped: a lane past the end moves an item another lane moves too (same value and address)
+                        const int e = (tid + 512 * v) % tot;
+                        uint32_t voff, loff;
+                        int c4, row;
+                        item_offsets(e, hq_n, Ln.ldh, voff, loff, c4, row);
+                        hl[v] = loff;
+                        hx[v] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hrs, voff, 0, 0));
                     }
+                }
+                f32x4 o[2][NU];                        // [sub][u] delta_{j-1} of rows 32 sub + 16 h + lr
+                if (dx) {
+                    const int act = N.L[j].act;
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        if (u == 1 && !two) {
-                            o[s][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-                            break;
+                    for (int s = 0; s < 2; ++s) {
+                        const unsigned char* buf = sm + s * CH_BUF;
+                        const unsigned char* drow = buf + CH_DP + (16 * h + lr) * CH_PITCH + 16 * lg;
+                        const float dtl = reinterpret_cast<const float*>(buf + CH_DT)[(16 * h + lr) * 4 + lg];
+                        f32x4 ac[NU];
+#pragma unroll
+                        for (int u = 0; u < NU; ++u)
+                            ac[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(wt[u], dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+                        for (int kb = 0; kb < 3; ++kb) {
+                            bf16x8 db[3];
+#pragma unroll
+                            for (int p = 0; p < 3; ++p) db[p] = *reinterpret_cast<const bf16x8*>(drow + p * CH_PLANE + 64 * kb);
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) ac[u] = six(wf[u][kb], db, ac[u]);
                         }
-                        f32x4 acc = ac[u];
                         // epilogue: act'(h_{j-1}) from the exact h planes
-                        const int col = 16 * (t0 + u) + 4 * lg;
-                        const unsigned char* hrow = buf + CH_HP + (16 * h + lr) * CH_PITCH + 2 * col;
-                        bf16x4 hq[3];
 #pragma unroll
-                        for (int p = 0; p < 3; ++p) hq[p] = *reinterpret_cast<const bf16x4*>(hrow + p * CH_PLANE);
+                        for (int u = 0; u < NU; ++u) {
+                            const int col = 16 * (t0 + u) + 4 * lg;
+                            const unsigned char* hrow = buf + CH_HP + (16 * h + lr) * CH_PITCH + 2 * col;
+                            bf16x4 hq[3];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const float hv = ((float)hq[2][r] + (float)hq[1][r]) + (float)hq[0][r];
-                            acc[r] = acc[r] * act_grad(act, hv);
+                            for (int p = 0; p < 3; ++p) hq[p] = *reinterpret_cast<const bf16x4*>(hrow + p * CH_PLANE);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const float hv = ((float)hq[2][r] + (float)hq[1][r]) + (float)hq[0][r];
+                                ac[u][r] = ac[u][r] * (TANH ? act_grad(ACT_TANH, hv) : act_grad(act, hv));
+                            }
+                            o[s][u] = ac[u];
                         }
-                        o[s][u] = acc;
                     }
                 }
-            }
+                // the next layer's fragments, in flight through B; the scheduling barrier keeps hipcc from hoisting
+                // them above this layer's MFMAs (which would need a second set of 72 fragment registers)
+                __builtin_amdgcn_sched_barrier(0);
+                load_w(max(j - 1, 1));
 #if CH_STAMP
-            if (dx) asm volatile("" :: "v"(o[0][0]), "v"(o[1][0]));
+                asm volatile("" :: "v"(o[0][0]), "v"(o[1][0]));
 #endif
-            VIHMC_CH_STAMP(j, 2)
-            __syncthreads();                           // B: every read of delta_j / h_{j-1} done
-            VIHMC_CH_STAMP(j, 3)
-            if (dx) {
+                VIHMC_CH_STAMP(j, 2)
+                __syncthreads();                       // B: every read of delta_j / h_{j-1} done
+                VIHMC_CH_STAMP(j, 3)
+                if (dx) {
 #pragma unroll
-                for (int s = 0; s < 2; ++s)
+                    for (int s = 0; s < 2; ++s)
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        if (u == 1 && !two) break;
-                        const int col = 16 * (t0 + u) + 4 * lg;
-                        unsigned char* buf = sm + s * CH_BUF;
-                        store_planes(buf + CH_DP + (16 * h + lr) * CH_PITCH + 2 * col, o[s][u]);
-                        if (col == 96) *reinterpret_cast<f32x4*>(buf + CH_DT + (16 * h + lr) * 16) = o[s][u];
-                    }
+                        for (int u = 0; u < NU; ++u) {
+                            const int col = 16 * (t0 + u) + 4 * lg;
+                            unsigned char* buf = sm + s * CH_BUF;
+                            store_planes(buf + CH_DP + (16 * h + lr) * CH_PITCH + 2 * col, o[s][u]);
+                            if (col == 96) *reinterpret_cast<f32x4*>(buf + CH_DT + (16 * h + lr) * 16) = o[s][u];
+                        }
 #pragma unroll
-                for (int v = 0; v < CH_HSLOTS; ++v) store_planes(sm + CH_HP + hl[v], hx[v]);
-                db_column(4 * hq_n, tid);
+                    for (int v = 0; v < CH_HSLOTS; ++v) store_planes(sm + CH_HP + hl[v], hx[v]);
+                    db_column(4 * hq_n, tid);
+                }
+                VIHMC_CH_STAMP(j, 4)
             }
-            VIHMC_CH_STAMP(j, 4)
+        };
+        const bool tanh_all = N.tanh_all != 0;
+        if (t0 + 1 < 7) {
+            if (tanh_all) dx_run(std::true_type{}, std::true_type{});
+            else dx_run(std::true_type{}, std::false_type{});
+        } else {
+            if (tanh_all) dx_run(std::false_type{}, std::true_type{});
+            else dx_run(std::false_type{}, std::false_type{});
         }
     } else {
-        // ---------------- dW role (and the staging of the next layer) ----------------
+        // ---------------- dW role ----------------
         // the tile assignment of k_bwd_bf2's dW role: waves 10, 11 take row tiles {0, 1} and {2, 3} whole, waves
         // 8, 9 row tile 4 or 5 whole plus row tile 6 over column tiles 0..3 or 4..6
         const int g = __builtin_amdgcn_readfirstlane(wave - 8);
@@ -298,21 +281,17 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
         const int rtb = g == 2 ? 1 : g == 3 ? 3 : 6;
         const int cb0 = g == 1 ? 4 : 0, cb1 = g == 0 ? 4 : 7;
         const int tro = bf6::tr_lane_off(lr, lg);
-        for (int j = nl - 1; j >= 0; --j) {
-            __syncthreads();                           // A
-            VIHMC_CH_STAMP(j, 0)
-            const BwdChainLayer& L = N.L[j];
-            const int NI4 = (L.n_in + 3) & ~3;
-            const int ntj = __builtin_amdgcn_readfirstlane((NI4 + 16) >> 4);
-            __syncthreads();                           // A2: the dX waves hold their W fragments
-            VIHMC_CH_STAMP(j, 1)
-            if (j >= 2) dma_image(j - 1, g, 4);       // the next layer's image (layers >= 1)
-            // weight gradient of layer j over the 64 rows (k = the rows, two 32-row blocks)
-            f32x4 acc[2][7];
+        f32x4 acc[2][7];
+        // weight gradient over the 64 rows (k = the rows, two 32-row blocks); instantiated for 7 column tiles (all
+        // but an input layer), so the next tile's h reads stay in flight under this tile's MFMAs
+        auto dw_layer = [&](auto nt_c, int ntj) __attribute__((always_inline)) {
+            constexpr int NT = decltype(nt_c)::value;  // 0: ntj at run time
+            const int nt = NT ? NT : ntj;
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
                 for (int t = 0; t < 7; ++t) acc[s2][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
             for (int s = 0; s < 2; ++s) {
                 const unsigned char* buf = sm + s * CH_BUF;
                 bf16x8 da[2][3], hb[2][3];
@@ -324,8 +303,8 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                 }
 #pragma unroll
                 for (int t = 0; t < 7; ++t) {
-                    if (t >= ntj) break;
-                    if (t + 1 < ntj) {
+                    if (t >= nt) break;
+                    if (t + 1 < nt) {
 #pragma unroll
                         for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(buf + CH_HP + p * CH_PLANE, tro, 16 * (t + 1));
                     }
@@ -333,22 +312,35 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                     if (t >= cb0 && t < cb1) acc[1][t] = six(da[1], hb[t & 1], acc[1][t]);
                 }
             }
+        };
+        for (int j = nl - 1; j >= 0; --j) {
+            __syncthreads();                           // A
+            VIHMC_CH_STAMP(j, 0)
+            VIHMC_CH_STAMP(j, 1)
+            const BwdChainLayer& L = N.L[j];
+            const int NI4 = (L.n_in + 3) & ~3;
+            const int ntj = __builtin_amdgcn_readfirstlane((NI4 + 16) >> 4);
+            if (ntj == 7) dw_layer(std::integral_constant<int, 7>{}, 7);
+            else dw_layer(std::integral_constant<int, 0>{}, ntj);
 #if CH_STAMP
             asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][6]));
 #endif
             VIHMC_CH_STAMP(j, 2)
-            if (j >= 2) bf6::wait_vmcnt0();            // the image DMA landed
             __syncthreads();                           // B
             VIHMC_CH_STAMP(j, 3)
-            // the tiled partial slab of layer j (bwd_tile_off, as k_bwd_bf2): one 1-KB store per tile
-            float* part = N.dwpart + c * N.dwpart_cs + L.part_off + (int64_t)wg * L.part_stride;
+            // the tiled partial slab of layer j (bwd_tile_off, as k_bwd_bf2): one 1-KB store per tile through a
+            // buffer resource (row tile 6 keeps its lg = 0 lanes: the others get an out-of-range offset)
+            const __amdgpu_buffer_rsrc_t prs = bf6::make_rsrc(N.dwpart + c * N.dwpart_cs + L.part_off +
+                                                              (int64_t)wg * L.part_stride,
+                                                              (uint32_t)bwd_tile_floats(ntj) * 4u);
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const int tn = s2 == 0 ? rta : rtb;
 #pragma unroll
                 for (int t = 0; t < 7; ++t) {
                     if (t >= ntj || (s2 == 1 && (t < cb0 || t >= cb1))) continue;
-                    if (tn < 6 || lg == 0) *reinterpret_cast<f32x4*>(part + bwd_tile_off(tn, t, ntj, lane)) = acc[s2][t];
+                    const uint32_t off = (tn < 6 || lg == 0) ? (uint32_t)bwd_tile_off(tn, t, ntj, lane) * 4u : bf6::OOB;
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bf6::u32x4, acc[s2][t]), prs, off, 0, 0);
                 }
             }
             VIHMC_CH_STAMP(j, 4)
@@ -372,10 +364,45 @@ extern "C" int vihmc_debug_ch_stamps(void* stamps, size_t stamp_bytes, void* rea
 }
 #endif
 
+// W^T of every fused layer of every chain -> the backward's transposed image (BWD_WTIMG layout): one block per
+// (chain, net, layer); the three planes exactly as k_split_wimg / the scatter split them
+__global__ __launch_bounds__(256) void k_split_wtimg(FusedArgs args, unsigned char* timg, int64_t timg_cs) {
+    const int C = args.C;
+    int b = blockIdx.x;
+    const int c = b % C;
+    b /= C;
+    const int net = b < args.net[0].nl ? 0 : 1;
+    const int j = net ? b - args.net[0].nl : b;
+    const float* W = args.packed + c * args.dp + args.net[net].w_off[j];   // [100 n][100 i]
+    unsigned char* img = timg + c * timg_cs + (int64_t)b * BWD_WTIMG;
+    for (int e = threadIdx.x; e < 112 * 112; e += 256) {
+        const int i = e / 112, n = e - i * 112;
+        const float v = (i < 100 && n < 100) ? W[n * 100 + i] : 0.f;
+        const __bf16 a = (__bf16)v;
+        const float r = v - (float)a;
+        const __bf16 bb = (__bf16)r;
+        const __bf16 cc = (__bf16)(r - (float)bb);
+        __bf16* o = reinterpret_cast<__bf16*>(img + i * BWD_WTPITCH + 2 * n);
+        o[0] = a;
+        o[BWD_WTPLANE / 2] = bb;
+        o[BWD_WTPLANE] = cc;
+    }
+    float* tail = reinterpret_cast<float*>(img + BWD_WTTAIL);
+    for (int e = threadIdx.x; e < 112 * 4; e += 256) {
+        const int i = e >> 2, q = e & 3;
+        tail[e] = i < 100 ? W[(96 + q) * 100 + i] : 0.f;
+    }
+}
+
+hipError_t launch_split_wtimg(const FusedArgs& a, unsigned char* timg, int64_t timg_cs, hipStream_t s) {
+    hipLaunchKernelGGL(k_split_wtimg, dim3(a.C * (a.net[0].nl + a.net[1].nl)), dim3(256), 0, s, a, timg, timg_cs);
+    return hipGetLastError();
+}
+
 bool bwd_chain_ok(const BwdChainArgs& a) {
     for (int net = 0; net < 2; ++net) {
         const BwdChainNet& n = a.net[net];
-        if (n.nl < 2 || n.nl > BWD_CHAIN_MAXL || !n.wimg || (n.ldd & 3) || n.ldd < 100 || n.n_wg * CH_ROWS < n.M ||
+        if (n.nl < 2 || n.nl > BWD_CHAIN_MAXL || !n.wtimg || (n.ldd & 3) || n.ldd < 100 || n.n_wg * CH_ROWS < n.M ||
             (n.n_wg - 1) * CH_ROWS >= n.M)
             return false;
         for (int j = 0; j < n.nl; ++j) {
@@ -385,7 +412,7 @@ bool bwd_chain_ok(const BwdChainArgs& a) {
                 return false;
         }
     }
-    return fwd_img_plane_stride() == CH_WPLANE;
+    return true;
 }
 
 hipError_t launch_bwd_chain(const BwdChainArgs& a, hipStream_t s) {

@@ -78,8 +78,8 @@ bool bwd_bf_ok(const BwdArgs& a);                       // k_bwd_bf handles ever
 hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s);
 
 // Whole-network backward in one launch for chunks of 64 rows (vihmc_bwd_chain.hip): every layer of both nets,
-// the deltas on chip, the same partial slabs as the per-layer k_bwd_bf2 launches. W_j from the bf16x6 forward's
-// pre-split weight image of layer j (index j - 1 of the net's images).
+// the deltas on chip, the same partial slabs as the per-layer k_bwd_bf2 launches. W_j^T from the pre-split W^T
+// image of layer j (BWD_WTIMG layout, index j - 1 of the net's images).
 constexpr int BWD_CHAIN_MAXL = 12;
 struct BwdChainLayer {
     const float* H; int64_t h_cs; int32_t ldh;    // h_{j-1} rows (j >= 1) or the net input (j = 0)
@@ -90,9 +90,10 @@ struct BwdChainLayer {
 struct BwdChainNet {
     BwdChainLayer L[BWD_CHAIN_MAXL];
     int32_t nl, M, n_wg;                          // n_wg = ceil(M / 64) workgroups per chain
+    int32_t tanh_all;                             // every layer j >= 1 has a tanh below it (compile-time act')
     const float* D; int64_t d_cs; int32_t ldd;    // delta of the top layer (dZ) [M][ldd]
     float* dwpart; int64_t dwpart_cs;
-    const unsigned char* wimg; int64_t wimg_cs;   // the net's weight images (layers 1 .. nl - 1)
+    const unsigned char* wtimg; int64_t wtimg_cs; // the net's W^T images (layers 1 .. nl - 1)
 };
 struct BwdChainArgs {
     BwdChainNet net[2];
@@ -154,7 +155,17 @@ hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* fro
 // chain's image region, -1 = none; null maps: packed only.
 struct ScatterImg {
     unsigned char* img; int64_t img_cs; const int32_t* img_w; const int32_t* img_f; int32_t plane;  // plane stride (B)
+    // the backward's transposed images (BWD_WTIMG bytes per fused layer): W^T planes and the fp32 n tail
+    unsigned char* timg; int64_t timg_cs; const int32_t* timg_w; const int32_t* timg_f; int32_t tplane;
 };
+// Pre-split W^T of every fused layer (layers 1.. of both nets), for the whole-network backward's dX: planes
+// [3][112 i][112 n] bf16 (224-B rows, zero past n_in / n_out) and the fp32 n tail [112 i][4] = W[96 + q][i].
+constexpr int BWD_WTPITCH = 224;
+constexpr int BWD_WTPLANE = 112 * BWD_WTPITCH;           // 25088
+constexpr int BWD_WTTAIL = 3 * BWD_WTPLANE;              // 75264
+constexpr int BWD_WTIMG = 77824;                         // 76 KB per layer
+static_assert(BWD_WTTAIL + 112 * 16 <= BWD_WTIMG, "W^T image");
+hipError_t launch_split_wtimg(const struct FusedArgs& a, unsigned char* timg, int64_t timg_cs, hipStream_t s);
 hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, int K, const int32_t* smap_w,
                           const int32_t* smap_wt, hipStream_t s, const ScatterImg* si = nullptr);
 // Sum `n_parts` partial slabs of `len` floats (slab stride `part_stride`, chain stride `in_cs`) into

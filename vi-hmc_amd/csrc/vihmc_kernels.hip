@@ -83,6 +83,21 @@ __device__ __forceinline__ void scatter_one(float* packed, int64_t dp, const int
         const int32_t f = si.img_f[k];
         if (f >= 0) *reinterpret_cast<float*>(img + f) = v;
     }
+    if (si.timg_w != nullptr) {
+        unsigned char* img = si.timg + c * si.timg_cs;
+        const int32_t o = si.timg_w[k];
+        if (o >= 0) {
+            const __bf16 a = (__bf16)v;
+            const float r = v - (float)a;
+            const __bf16 b = (__bf16)r;
+            const __bf16 cc = (__bf16)(r - (float)b);
+            *reinterpret_cast<__bf16*>(img + o) = a;
+            *reinterpret_cast<__bf16*>(img + o + si.tplane) = b;
+            *reinterpret_cast<__bf16*>(img + o + 2 * si.tplane) = cc;
+        }
+        const int32_t f = si.timg_f[k];
+        if (f >= 0) *reinterpret_cast<float*>(img + f) = v;
+    }
 }
 
 __global__ void k_scatter(float* packed, int64_t dp, const float* theta, int K, const int32_t* smap_w,

@@ -141,13 +141,17 @@ struct vihmc_plan {
     // images' fp32 k tail)
     unsigned char* wimg = nullptr;
     int64_t wimg_cs = 0;
+    unsigned char* wtimg = nullptr;   // the backward's transposed images (BWD_WTIMG per fused layer), same upkeep
+    int64_t wtimg_cs = 0;
+    int32_t* smap_timg = nullptr;     // per sampled index: byte offset of its W^T-image plane element, or -1
+    int32_t* smap_timgf = nullptr;    // ... of its fp32 n-tail copy, or -1
     int fwd_wimg = 1;
     int fuse_scatter = 1;       // plan option: trajectory evaluations take theta already scattered by the leapfrog
-    int mlp_fast = 1;
-    int contract_rev = 0;
-    int bwd_chain = 1;            // option bwd_chain: whole-network backward in one launch when the chunks are 64 rows
-    bool wimg_live = false;
-    bool last_bwd_chain = false;  // the last gradient evaluation ran k_bwd_chain (get_option bwd_chain: bit 1)       // this evaluation's forward staged the weight images (they hold this theta)           // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
+    int mlp_fast = 1;             // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
+    int contract_rev = 0;         // plan option: side B takes the chains last first
+    int bwd_chain = 1;            // plan option: whole-network backward in one launch when the chunks are 64 rows
+    bool timg_live = false;       // the W^T images hold this evaluation's theta (scatter-kept or split this evaluation)
+    bool last_bwd_chain = false;  // the last gradient evaluation ran k_bwd_chain (get_option bwd_chain: bit 1)
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
     int graph_on = -1;          // -1: follow VIHMC_GRAPH
     // hidden-layer forward products as exact 3-way bf16 splits (6 bf16 MFMA products, fp32 accumulate;
@@ -259,40 +263,49 @@ void fused_args(vihmc_plan* p, int C, FusedArgs& a);
 // evaluation, or no images).
 int image_maps(vihmc_plan* p, const vihmc_deeponet_desc* d, const int64_t* idx) {
     if (!fused_forward_ok(p)) return 0;
-    std::vector<int32_t> fw(p->D, -1), ff(p->D, -1);
+    std::vector<int32_t> fw(p->D, -1), ff(p->D, -1), tw(p->D, -1), tf(p->D, -1);
     int img = 0;
     const vihmc_linear* tabs[2] = {d->branch, d->trunk};
     const int nl[2] = {d->n_branch_layers, d->n_trunk_layers};
     for (int net = 0; net < 2; ++net)
         for (int j = 1; j < nl[net]; ++j, ++img) {
             const vihmc_linear& l = tabs[net][j];
-            const int64_t base = (int64_t)img * FWD_WIMG;
+            const int64_t base = (int64_t)img * FWD_WIMG, tbase = (int64_t)img * BWD_WTIMG;
             for (int r = 0; r < l.n_out; ++r) {
                 for (int c = 0; c < l.n_in; ++c) {
                     const int64_t f = l.w_off + (int64_t)r * l.n_in + c;
                     fw[f] = (int32_t)(base + fwd_img_plane_off(r, c));
                     if (c >= 96) ff[f] = (int32_t)(base + fwd_img_tail_off(r, c));
+                    // W^T image: row i = c, column n = r; n tail W[96 + q][i] at [i][q]
+                    tw[f] = (int32_t)(tbase + c * BWD_WTPITCH + 2 * r);
+                    if (r >= 96) tf[f] = (int32_t)(tbase + BWD_WTTAIL + 4 * (c * 4 + (r - 96)));
                 }
                 ff[l.b_off + r] = (int32_t)(base + fwd_img_bias_off(r));
             }
         }
-    std::vector<int32_t> sw(p->K), sf(p->K);
+    std::vector<int32_t> sw(p->K), sf(p->K), stw(p->K), stf(p->K);
     for (int k = 0; k < p->K; ++k) {
         sw[k] = fw[idx[k]];
         sf[k] = ff[idx[k]];
+        stw[k] = tw[idx[k]];
+        stf[k] = tf[idx[k]];
     }
     if (int rc = p->upload(&p->smap_img, sw.data(), p->K)) return rc;
     if (int rc = p->upload(&p->smap_imgf, sf.data(), p->K)) return rc;
+    if (int rc = p->upload(&p->smap_timg, stw.data(), p->K)) return rc;
+    if (int rc = p->upload(&p->smap_timgf, stf.data(), p->K)) return rc;
     FusedArgs a{};
     fused_args(p, p->maxC, a);
     HIPCHK(launch_split_wimg(a, nullptr));
+    HIPCHK(launch_split_wtimg(a, p->wtimg, p->wtimg_cs, nullptr));
     HIPCHK(hipDeviceSynchronize());
     p->img_by_scatter = true;
     return 0;
 }
 
 ScatterImg scatter_img(const vihmc_plan* p) {
-    return ScatterImg{p->wimg, p->wimg_cs, p->smap_img, p->smap_imgf, fwd_img_plane_stride()};
+    return ScatterImg{p->wimg, p->wimg_cs, p->smap_img, p->smap_imgf, fwd_img_plane_stride(),
+                      p->wtimg, p->wtimg_cs, p->smap_timg, p->smap_timgf, BWD_WTPLANE};
 }
 
 int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb, const float* tf, const float* y,
@@ -417,6 +430,8 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         // pre-split weight images of the bf16x6 fused forward (layers 1.. of both nets)
         p->wimg_cs = (int64_t)(p->nets[0].L.size() - 1 + p->nets[1].L.size() - 1) * FWD_WIMG;
         if (int rc = p->alloc(&p->wimg, p->wimg_cs * C)) return rc;
+        p->wtimg_cs = (int64_t)(p->nets[0].L.size() - 1 + p->nets[1].L.size() - 1) * BWD_WTIMG;
+        if (int rc = p->alloc(&p->wtimg, p->wtimg_cs * C)) return rc;
         p->qsplitA_cs = (int64_t)cdiv(p->N, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
         if (int rc = p->alloc(&p->qsplitA, p->qsplitA_cs * C)) return rc;
         p->qsplitB_cs = (int64_t)cdiv(p->P, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
@@ -674,8 +689,11 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
             a.net[0].wimg = p->wimg;
             a.net[1].wimg = p->wimg + (int64_t)a.net[0].nl * FWD_WIMG;
             a.net[0].wimg_cs = a.net[1].wimg_cs = p->wimg_cs;
-            if (!p->img_by_scatter) HIPCHK(launch_split_wimg(a, s));
-            p->wimg_live = true;
+            if (!p->img_by_scatter) {
+                HIPCHK(launch_split_wimg(a, s));
+                HIPCHK(launch_split_wtimg(a, p->wtimg, p->wtimg_cs, s));
+                p->timg_live = true;
+            }
         }
         HIPCHK(launch_fwd_fused_bf(a, nwb, s));
         return 0;
@@ -814,13 +832,15 @@ bool bwd_chain_args(vihmc_plan* p, int C, BwdChainArgs& a) {
         if (cn.nl > BWD_CHAIN_MAXL) return false;
         cn.M = n.rows;
         cn.n_wg = cdiv(n.rows, bwd_chain_rows());
+        cn.tanh_all = 1;
+        for (int j = 0; j + 1 < cn.nl; ++j) cn.tanh_all &= n.L[j].act == ACT_TANH ? 1 : 0;
         cn.D = n.delta[0];
         cn.d_cs = n.delta_cs;
         cn.ldd = n.L.back().ldo;
         cn.dwpart = n.dwpart;
         cn.dwpart_cs = n.dwpart_cs;
-        cn.wimg = p->wimg + (net ? (int64_t)(p->nets[0].L.size() - 1) * FWD_WIMG : 0);
-        cn.wimg_cs = p->wimg_cs;
+        cn.wtimg = p->wtimg + (net ? (int64_t)(p->nets[0].L.size() - 1) * BWD_WTIMG : 0);
+        cn.wtimg_cs = p->wtimg_cs;
         for (int j = 0; j < cn.nl; ++j) {
             const LayerPk& L = n.L[j];
             if (L.rows_per_chunk != bwd_chain_rows() || L.n_chunks != cn.n_wg) return false;
@@ -847,7 +867,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     // the pre-split contraction images (bf16x6 sides, gradient evaluations) are written by the fused forward
     // when it runs; otherwise k_split_blocks makes them below
     p->img_by_fwd = false;
-    p->wimg_live = false;
+    p->timg_live = p->img_by_scatter && p->wtimg;      // the scatter above kept the W^T images current
     if (int rc = deeponet_forward_layers(p, C, s, want_grad && p->contract_bf16x6 && p->W == 100)) return rc;
     int stats_waves = 0;
     {
@@ -920,7 +940,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         hipEvent_t bwd_stop = nullptr;
         if (int rc = p->timing_begin(VIHMC_T_BWD, s, &bwd_stop, maxl)) return rc;
         BwdChainArgs ca{};
-        const bool chain = p->bwd_chain && p->bwd_bf16x6 && p->wimg_live && bwd_chain_args(p, C, ca);
+        const bool chain = p->bwd_chain && p->bwd_bf16x6 && p->timg_live && bwd_chain_args(p, C, ca);
         if (chain) HIPCHK(launch_bwd_chain(ca, s));
         p->last_bwd_chain = chain;
         for (int i = 0; i < (chain ? 0 : maxl); ++i) {
