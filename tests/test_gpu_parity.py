@@ -96,24 +96,26 @@ def test_deeponet_burgers_every_launch_geometry(C, fwd_bf16x6, contract_bf16x6, 
 
 
 @pytest.mark.parametrize("name", ["deeponet_burgers", "deeponet_refshape"])
-def test_whole_network_backward_bitwise_equals_layer_launches(name, cuda_device):
-    """Single-chain plans run the backward of both nets in one launch (k_bwd_chain: deltas kept in LDS, W_j from
-    the forward's weight images); it must equal the nine per-layer k_bwd_bf2 launches bit for bit, and the golden."""
+def test_single_chain_kernels_bitwise_equal_batched_kernels(name, cuda_device):
+    """Single-chain plans run the backward of both nets in one launch (k_bwd_chain: deltas kept in LDS, W^T from
+    the scatter-kept transposed images); it must equal the nine per-layer k_bwd_bf2 launches bit for bit, and
+    match the golden."""
     c = deeponet_case(name)
     eng = engine_for(c, max_chains=1)
     res = {}
-    for on in (1, 0):
-        eng.option("bwd_chain", on)
+    for fs, bc in ((1, 1), (0, 0)):
+        eng.option("bwd_chain", bc)
         out = []
         for th in c.thetas:
             lp, g = eng.logp_grad(torch.tensor(th, device=cuda_device)[None])
             out.append((lp.cpu(), g.cpu()))
-        assert eng.get_option("bwd_chain") == (3 if on else 0)
-        res[on] = out
-    for (la, ga), (lb, gb) in zip(res[0], res[1]):
-        assert torch.equal(la, lb) and torch.equal(ga, gb)
+        assert eng.get_option("bwd_chain") == (3 if bc else 0)
+        res[(fs, bc)] = out
+    for key in ((0, 0),):
+        for (la, ga), (lb, gb) in zip(res[(1, 1)], res[key]):
+            assert torch.equal(la, lb) and torch.equal(ga, gb), key
     sub = c.g["grad_subsample"]
-    for t, (lp, g) in enumerate(res[1]):
+    for t, (lp, g) in enumerate(res[(1, 1)]):
         check_logp(float(lp[0]), float(c.g[f"logp{t}"]), f"{name} theta{t}")
         check_grad_sub(g[0].numpy(), sub, c.g[f"grad{t}_sub"], float(c.g[f"grad{t}_norm"]), f"{name} theta{t}")
 

@@ -270,6 +270,7 @@ int diag_switches_bwd_chain();
 int diag_switches();
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, int nw, hipStream_t s);     // bf16x6, 12 (or 4) waves
+
 size_t fwd_fused_lds_bytes();
 
 // BNN: one wave per chain, everything in registers / LDS.

@@ -493,7 +493,17 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         // side A: workgroups own 128 trunk rows and sweep the branch rows; split the sweep (partial
         // dZ_trunk slabs + fixed-order reduce) only when too few workgroups would fill the chip
         const int og_a = cdiv(p->P, CONTRACT_OWN_PER_WG), og_b = cdiv(p->N, CONTRACT_OWN_PER_WG);
-        const int qa = std::max(1, std::min(8, (int)std::lround(1024.0 / ((double)C * og_a))));
+        // q-split count: fewest resident rounds x chunks per workgroup (+2 chunks of per-workgroup prologue), one
+        // 1024-thread workgroup per CU (single chain: 3 splits of 11 chunks, 240 workgroups in one round)
+        int qa = 1;
+        {
+            const int64_t nch = cdiv(p->N, CONTRACT_SPLIT_ROWS);
+            int64_t best = INT64_MAX;
+            for (int q = 1; q <= 8; ++q) {
+                const int64_t cost = cdiv((int64_t)C * og_a * q, 256) * (cdiv(nch, q) + 2);
+                if (cost < best) best = cost, qa = q;
+            }
+        }
         // multiple of 32 rows: whole blocks of the pre-split image for k_contract_bf (and 16-row chunks)
         p->qperA = (int)(((int64_t)cdiv(p->N, qa) + CONTRACT_SPLIT_ROWS - 1) / CONTRACT_SPLIT_ROWS * CONTRACT_SPLIT_ROWS);
         p->qchunksA = cdiv(p->N, p->qperA);
