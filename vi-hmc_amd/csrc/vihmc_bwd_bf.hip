@@ -53,8 +53,8 @@ constexpr int BB_LDS = BB_WT + 100 * 16;               // 154880
 static_assert(BB_LDS <= 160 * 1024, "LDS");
 static_assert(BB_BUF + 2 * BB_PLANE < 65536, "LDS store offsets fit the ds_write immediate");
 constexpr int BB_THREADS = 1024;                       // 8 dX + 4 dW + 4 staging waves, 4 per SIMD
-constexpr int B2_SLOTS = 7;                            // staged float4 per staging lane (<= 800 D + 896 H)
-constexpr int B2_WS_D = (BB_SUB * 25 + 63) / 64;       // wave-slots of D items (13)
+constexpr int B2_SLOTS = 4;                            // staged D float4 per staging lane (800 per sub-tile / 256)
+constexpr int B2_HSLOTS = 2;                           // staged H float4 per dX lane (<= 32 x 28 per sub-tile / 512)
 
 __device__ __forceinline__ float act_grad_bf(int act, float h) {
 #pragma clang fp contract(off)
@@ -146,26 +146,21 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
     if (wave >= 12) __builtin_amdgcn_s_setprio(1);
     if (wave >= 12) {
         // ---------------- staging role ----------------
-        // wave-slot ws = 4 v + g (g = staging wave, v = slot): ws < 13 carries D items e = 64 ws + lane (800 of
-        // them: 32 rows x 25 float4), the others H items (32 rows x hq4 float4), wrapped modulo the item count: a
-        // lane past the end moves an item another lane moves too (the same value to the same LDS address), so no
-        // slot is ever skipped. Per slot the kind is wave-uniform and the offsets are constant over the sub-tiles.
+        // wave-slot ws = 4 v + g (g = staging wave, v = slot) carries D items e = 64 ws + lane (800 of them: 32 rows x
+        // 25 float4) wrapped modulo 800: a lane past the end moves an item another lane moves too (the same value to the
+        // same LDS address), so no slot is ever skipped; the offsets are constant over the sub-tiles. The h rows are
+        // the dX waves' (below): split between the two roles, neither is the period's critical path alone.
         const int g = __builtin_amdgcn_readfirstlane(wave - 12);
-        uint32_t voff[B2_SLOTS], loff[B2_SLOTS], toff[4];
-        bool tl[4];
+        uint32_t voff[B2_SLOTS], loff[B2_SLOTS], toff[B2_SLOTS];
+        bool tl[B2_SLOTS];
 #pragma unroll
         for (int v = 0; v < B2_SLOTS; ++v) {
-            const int ws = 4 * v + g;
-            const bool isd = ws < B2_WS_D;
-            const int q = isd ? 25 : hq4, ld = isd ? P.ldd : P.ldh;
-            const int e = ((isd ? ws : ws - B2_WS_D) * 64 + lane) % (BB_SUB * q);
-            const int r = e / q, c4 = e - r * q;
-            voff[v] = (uint32_t)(r * ld + 4 * c4) * 4u;
-            loff[v] = (uint32_t)((isd ? BB_DP : BB_HP) + r * BB_PITCH + 8 * c4);
-            if (v < 4) {
-                tl[v] = isd && c4 == 24;
-                toff[v] = (uint32_t)(BB_DT + r * 16);
-            }
+            const int e = ((4 * v + g) * 64 + lane) % (BB_SUB * 25);
+            const int r = e / 25, c4 = e - r * 25;
+            voff[v] = (uint32_t)(r * P.ldd + 4 * c4) * 4u;
+            loff[v] = (uint32_t)(BB_DP + r * BB_PITCH + 8 * c4);
+            tl[v] = c4 == 24;
+            toff[v] = (uint32_t)(BB_DT + r * 16);
         }
         // db column: H column NI4 of both buffers is the constant 1 (planes 1, 0, 0), never overwritten by the
         // H stores (columns < NI4), so the dW MFMAs produce part[n][NI4] = sum_m D[m][n] = db[n] exactly
@@ -184,14 +179,10 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         f32x4 pfa[B2_SLOTS], pfb[B2_SLOTS];
         auto load = [&](int sub, f32x4 (&pf)[B2_SLOTS]) __attribute__((always_inline)) {
             // resources based at the sub-tile's first row: rows past M read 0 (a partial last sub-tile)
+            const __amdgpu_buffer_rsrc_t rs = bf6::make_rsrc(D + (int64_t)sub * P.ldd, (uint32_t)((P.M - sub) * P.ldd * 4));
 #pragma unroll
-            for (int v = 0; v < B2_SLOTS; ++v) {
-                const bool isd = 4 * v + g < B2_WS_D;          // wave-uniform
-                const float* base = isd ? D + (int64_t)sub * P.ldd : H + (int64_t)sub * P.ldh;
-                const int ld = isd ? P.ldd : P.ldh;
-                const __amdgpu_buffer_rsrc_t rs = bf6::make_rsrc(base, (uint32_t)((P.M - sub) * ld * 4));
+            for (int v = 0; v < B2_SLOTS; ++v)
                 pf[v] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[v], 0, 0));
-            }
         };
         auto store = [&](int buf, const f32x4 (&pf)[B2_SLOTS]) __attribute__((always_inline)) {
 #pragma unroll
@@ -202,7 +193,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 *reinterpret_cast<bf16x4*>(base) = p0;
                 *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;
                 *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;
-                if (v < 4 && tl[v]) *reinterpret_cast<f32x4*>(smw + buf * BB_BUF + toff[v]) = pf[v];
+                if (tl[v]) *reinterpret_cast<f32x4*>(smw + buf * BB_BUF + toff[v]) = pf[v];
             }
         };
         // Loop unrolled by two so set A is always the newest in flight at the loop head, and every load issued
@@ -254,17 +245,51 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         // offset instead of a branch around the store
         const __amdgpu_buffer_rsrc_t drs =
             bf6::make_rsrc(P.Dout + c * P.o_cs, (uint32_t)((int64_t)P.M * P.ldh * 4));
+        // h-row staging (the staging waves move the deltas): item e = tid + 512 v of the sub-tile's 32 x hq4 float4,
+        // wrapped like the staging role's; sub-tile s is loaded into set s & 1 two sub-tiles before its store
+        uint32_t hvoff[B2_HSLOTS], hloff[B2_HSLOTS];
+#pragma unroll
+        for (int v = 0; v < B2_HSLOTS; ++v) {
+            const int e = (tid + 512 * v) % (BB_SUB * hq4);
+            const int r = e / hq4, c4 = e - r * hq4;
+            hvoff[v] = (uint32_t)(r * P.ldh + 4 * c4) * 4u;
+            hloff[v] = (uint32_t)(BB_HP + r * BB_PITCH + 8 * c4);
+        }
+        const int slast = r0 + max(nsub - 1, 0) * BB_SUB;
+        auto hsub_at = [&](int k) { return min(r0 + k * BB_SUB, slast); };
+        auto hload = [&](int sub, f32x4 (&hs)[B2_HSLOTS]) __attribute__((always_inline)) {
+            const __amdgpu_buffer_rsrc_t rs = bf6::make_rsrc(H + (int64_t)sub * P.ldh, (uint32_t)((P.M - sub) * P.ldh * 4));
+#pragma unroll
+            for (int v = 0; v < B2_HSLOTS; ++v)
+                hs[v] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, hvoff[v], 0, 0));
+        };
+        auto hstore = [&](int buf, const f32x4 (&hs)[B2_HSLOTS]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int v = 0; v < B2_HSLOTS; ++v) {
+                bf16x4 p0, p1, p2;
+                split4(hs[v], p0, p1, p2);
+                unsigned char* base = smw + buf * BB_BUF + hloff[v];
+                *reinterpret_cast<bf16x4*>(base) = p0;
+                *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;
+                *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;
+            }
+        };
         auto dx_run = [&](auto two_c, auto tanh_c) __attribute__((always_inline)) {
             constexpr bool TWO = decltype(two_c)::value;
             constexpr bool TANH = decltype(tanh_c)::value;
             constexpr int NU = TWO ? 2 : 1;
+            f32x4 hsa[B2_HSLOTS], hsb[B2_HSLOTS];       // per instantiation: no register set live across the dispatch
+            if (nsub > 0) {
+                hload(hsub_at(0), hsa);
+                hload(hsub_at(1), hsb);
+                hstore(0, hsa);
+                hload(hsub_at(2), hsa);
+            }
             bf16x8 wra[3][3];                          // [kb][plane] W^T fragments of the first i-tile (registers)
             float wta = 0.f, wtb = 0.f;
-            for (int i = 0; i < nsub; ++i) {
+            auto dx_sub = [&](int i) __attribute__((always_inline)) {
                 const int sub = r0 + i * BB_SUB;
-                __syncthreads();
-                VIHMC_BB_STAMP(i, 0)
-                if (!P.has_dx) continue;
+                if (!P.has_dx) return;
                 if (i == 0) {
 #pragma unroll
                     for (int kb = 0; kb < 3; ++kb)
@@ -276,11 +301,6 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 }
                 const unsigned char* buf = smw + (i & 1) * BB_BUF;
                 const unsigned char* drow = buf + BB_DP + (16 * h + lr) * BB_PITCH + 16 * lg;
-                bf16x8 db[3][3];
-#pragma unroll
-                for (int kb = 0; kb < 3; ++kb)
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) db[kb][p] = *reinterpret_cast<const bf16x8*>(drow + p * BB_PLANE + 64 * kb);
                 const float dtl = reinterpret_cast<const float*>(buf + BB_DT)[(16 * h + lr) * 4 + lg];
                 f32x4 acc[2];
                 acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wta, dtl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
@@ -288,13 +308,16 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                              : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int kb = 0; kb < 3; ++kb) {
-                    acc[0] = six(wra[kb], db[kb], acc[0]);
+                    bf16x8 db[3];                      // the delta fragments of this k-block (12 VGPRs at a time)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) db[p] = *reinterpret_cast<const bf16x8*>(drow + p * BB_PLANE + 64 * kb);
+                    acc[0] = six(wra[kb], db, acc[0]);
                     if (TWO) {
                         // only the first i-tile's W^T in registers (VGPR budget); the second re-read from LDS
                         bf16x8 wb[3];
 #pragma unroll
                         for (int p = 0; p < 3; ++p) wb[p] = *reinterpret_cast<const bf16x8*>(wrow1 + p * BB_WPLANE + 64 * kb);
-                        acc[1] = six(wb, db[kb], acc[1]);
+                        acc[1] = six(wb, db, acc[1]);
                     }
                 }
 #if BB_STAMP
@@ -318,6 +341,27 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                     }
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bf6::u32x4, o), drs, off, 0, 0);
                 }
+            };
+            // unrolled by two (static register sets, every load unconditional: see the staging role)
+            int i = 0;
+            for (; i + 1 < nsub; i += 2) {
+                __syncthreads();                       // buffer 0 holds sub-tile i
+                VIHMC_BB_STAMP(i, 0)
+                dx_sub(i);
+                hstore(1, hsb);                        // h of sub-tile i + 1 into the free buffer
+                hload(hsub_at(i + 3), hsb);
+                VIHMC_BB_STAMP(i, 2)
+                __syncthreads();                       // buffer 1 holds sub-tile i + 1
+                VIHMC_BB_STAMP(i + 1, 0)
+                dx_sub(i + 1);
+                if (i + 2 < nsub) hstore(0, hsa);
+                hload(hsub_at(i + 4), hsa);
+                VIHMC_BB_STAMP(i + 1, 2)
+            }
+            if (i < nsub) {
+                __syncthreads();
+                VIHMC_BB_STAMP(i, 0)
+                dx_sub(i);
                 VIHMC_BB_STAMP(i, 2)
             }
         };
