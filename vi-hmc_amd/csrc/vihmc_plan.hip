@@ -424,7 +424,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     const int64_t NP = (int64_t)p->N * p->P;
     if (int rc = p->upload(&p->y, y, NP)) return rc;
     p->ldgT = (int)((p->N + 31) / 32 * 32);
-    p->gT_cs = r64((int64_t)p->P * p->ldgT);
+    p->gT_cs = r64((int64_t)(p->P + 1) * p->ldgT);      // the bf16x6 blocked layout uses (P rounded even) rows
     if (int rc = p->alloc(&p->gT, p->gT_cs * C)) return rc;
     if (p->W == 100) {
         // pre-split weight images of the bf16x6 fused forward (layers 1.. of both nets)
@@ -773,6 +773,11 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img) {
     return 0;
 }
 
+// rows per 16-row block of the bf16x6 G^T hand-off, even: every block (16 x 64 B per row) starts on a 128-B line,
+// so side A's 1-KB tile stores are whole lines (an odd count left every other block's tiles straddling two
+// partial lines, which the memory side read back: +200 MB of fetch per side-A launch at 16 chains)
+inline int gt_block_rows(const vihmc_plan* p) { return (p->P + 1) & ~1; }
+
 ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
     Net& b = p->nets[0];
     Net& t = p->nets[1];
@@ -794,7 +799,7 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
         q.out_chunk_stride = p->qchunksA > 1 ? (int64_t)p->P * p->ldz : 0;
         q.gout = p->gT;
         q.gout_cs = p->gT_cs;
-        q.ldg = p->contract_bf16x6 && p->W == 100 ? p->P : p->ldgT;   // bf16x6: chunk-blocked rows
+        q.ldg = p->contract_bf16x6 && p->W == 100 ? gt_block_rows(p) : p->ldgT;   // bf16x6: 16-row blocked
     } else {
         q.out = out ? out : p->lik_buf;   // dummy when not writing S
         q.out_cs = out ? (int64_t)p->N * p->P : 0;
@@ -908,7 +913,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         q.q_cs = t.act_cs;
         q.ldq = p->ldz;
         q.Y = p->gT;           // G^T written by side A: no S recompute on this side
-        q.ldy = p->contract_bf16x6 && p->W == 100 ? p->P : p->ldgT;
+        q.ldy = p->contract_bf16x6 && p->W == 100 ? gt_block_rows(p) : p->ldgT;
         q.y_cs = p->gT_cs;
         q.load_g = 1;
         q.bf16x6 = p->W == 100 ? p->contract_bf16x6 : 0;
