@@ -210,7 +210,7 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value);
 
 void        vihmc_plan_destroy(vihmc_plan* p);
 const char* vihmc_last_error(void);
-/* "vihmc <ver> gfx950 diag=<fwd>,<contract_bf>,<bwd_bf>,<layers>": the timing-only ablation / stamp switches the
+/* "vihmc <ver> gfx950 diag=<fwd>,<contract_bf>,<bwd_bf>,<layers>,<bwd_chain>": the timing-only ablation / stamp switches the
  * library was built with (all 0 in a product build). Plan creation fails in a build with any of them on
  * unless VIHMC_ALLOW_DIAG=1 (A/B timing of variant builds only: results are wrong by design). */
 const char* vihmc_version(void);

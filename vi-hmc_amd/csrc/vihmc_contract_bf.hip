@@ -387,10 +387,8 @@ __global__ __launch_bounds__(CBB_THREADS, 1) void k_contract_bf_b(ContractProb P
         b = (gx * 8 + xcd) * P.o_tiles + og;
     }
     const int per_chain = P.o_tiles * P.q_chunks;
-    const int cb = b / per_chain;
-    b -= cb * per_chain;
-    // the chains side A wrote last first (their G^T the likeliest still in the memory-side cache)
-    const int c = P.rev_chains ? P.rev_chains - 1 - cb : cb;
+    const int c = b / per_chain;
+    b -= c * per_chain;
     const int qc = b / P.o_tiles;
     const int og = b - qc * P.o_tiles;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;

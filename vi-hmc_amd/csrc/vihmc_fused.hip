@@ -375,18 +375,12 @@ __device__ __forceinline__ void bf_split_operand(const float4 (&h)[7], bf16x8 (&
 #ifndef FWD_DMA_ONLY
 #define FWD_DMA_ONLY 0     // timing builds: the register-staging path compiled out with FWD_TAILF32 = 0 too
 #endif
-#ifndef FWD_TF_SCHED
-#define FWD_TF_SCHED 0     // 1: sched_barrier between tile pairs (fewer spills, 257-262 vs 256 us: not kept)
-#endif
 constexpr int FWD_WTAIL = 3 * BPLANE * 2 + 112 * 4;   // byte offset of the fp32 W tail [100][4] in an image
 constexpr int QI_PITCH = 224;                           // contraction block image (vihmc_contract_bf.hip): plane
 constexpr int QI_PLANE = CONTRACT_SPLIT_ROWS * QI_PITCH;  // rows of 112 bf16, 3 planes, then the fp32 tail [32][4]
 static_assert(3 * QI_PLANE + CONTRACT_SPLIT_ROWS * 16 <= CONTRACT_SPLIT_BLOCK, "block image");
 constexpr int QI_HALF = 16 * QI_PITCH;                  // a wave's 16 rows of one plane (3584 B)
 constexpr int QI_WAVE = 3 * QI_HALF + 16 * 16;          // + its tail rows: 11008 B of LDS per wave
-#ifndef FWD_IMG_LDS
-#define FWD_IMG_LDS 1   // 0: the image written straight from registers (8-B stores per lane and tile)
-#endif
 
 __device__ __forceinline__ int tf_row(int t, int lr) { return t < 6 ? 16 * t + lr : 96 + (lr >> 2); }
 
@@ -423,9 +417,6 @@ __device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, co
         const f32x4 a1 = tf_tile(wb, wtail, 2 * p + 1, lr, lg, hp, h6);
         hn[2 * p] = bf_epi<ACT>(bias, 2 * p, lg, a0, orsrc, ooff);
         hn[2 * p + 1] = bf_epi<ACT>(bias, 2 * p + 1, lg, a1, orsrc, ooff);
-#if FWD_TF_SCHED
-        __builtin_amdgcn_sched_barrier(0);     // keep the scheduler from hoisting later tiles (VGPR pressure)
-#endif
     }
     // tile 6: register 0 of lane (lr, lg) = pre-activation of h[lr][96 + lg]
     const f32x4 a6 = tf_tile(wb, wtail, 6, lr, lg, hp, h6);
@@ -509,26 +500,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
     // (global_load_lds, 1 KB per wave-instruction, no VGPRs / VALU); the barrier drains it (vmcnt(0))
     const bool dma = FWD_TAILF32 || FWD_DMA_ONLY || N.wimg != nullptr;  // FWD_TAILF32: images only (host-checked)
     const unsigned char* wimgc = dma ? N.wimg + c * N.wimg_cs : nullptr;
-#ifndef FWD_ASM_DMA
-#define FWD_ASM_DMA 1   // 1: the weight-image DMA from inline asm (hipcc does not track it): with the builtin, hipcc
-                        // waited vmcnt(0) -- this wave's h stores included -- before the bias reads of every tile
-                        // pair, not knowing the DMA target disjoint; the wave then waits for the DMA itself at the
-                        // end of the layer, before the barrier that publishes it
-#endif
-#ifndef FWD_DMA_CNT0
-#define FWD_DMA_CNT0 0  // 1: drain vmcnt(0) at the end of each layer (A/B)
-#endif
-#if FWD_ASM_DMA
 #define VIHMC_FB_DMA(J, BUF)                                                                          \
     for (int k = wave; k < FWD_WIMG / 1024; k += NW)                                                  \
         bf6::glds16_asm(wimgc + (int64_t)(J) * FWD_WIMG + k * 1024 + lane * 16, fsmb + (BUF) * FWD_WIMG + k * 1024);
-#else
-#define VIHMC_FB_DMA(J, BUF)                                                                          \
-    for (int k = wave; k < FWD_WIMG / 1024; k += NW)                                                  \
-        __builtin_amdgcn_global_load_lds(                                                             \
-            reinterpret_cast<const void*>(wimgc + (int64_t)(J) * FWD_WIMG + k * 1024 + lane * 16),   \
-            (__attribute__((address_space(3))) void*)(fsmb + (BUF) * FWD_WIMG + k * 1024), 16, 0, 0);
-#endif
     if (dma) {
         VIHMC_FB_DMA(0, 0)
     } else {
@@ -585,8 +559,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         }
         // layer j+1's image landed before the next barrier. The DMA was issued ahead of this layer's seven h stores
         // (six b128 + the tile-6 b32), so a counted wait leaves those stores in flight (vmcnt(0) waited for them)
-        if (FWD_ASM_DMA && dma) {
-            if (FWD_TAILF32 && !FWD_DMA_CNT0) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        if (dma) {
+            if (FWD_TAILF32) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
             else bf6::wait_vmcnt0();
         }
     }
@@ -608,7 +582,6 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
         split3(h[6].x, y0, y1, y2);                       // column 96 + lg: its planes and the fp32 tail
         unsigned char* blk = N.qimg + c * N.qimg_cs + (int64_t)(min(row, N.rows - 1) / CONTRACT_SPLIT_ROWS) *
                                                           CONTRACT_SPLIT_BLOCK;
-#if FWD_IMG_LDS
         // through LDS (the weight buffers are free after the last layer): each wave lays its 16 rows out as in
         // the image -- three 16-row plane slices and the tail slice, 11,008 B -- then copies them out in whole
         // 1-KB wave stores (direct 8-B stores per lane and tile measured slower)
@@ -656,25 +629,6 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
             if (row0 + r < N.rows)
                 *reinterpret_cast<u32x4*>(blk + off) = *reinterpret_cast<const u32x4*>(reg + i * 16);
         }
-#else
-        if (rok) {
-            unsigned char* rp = blk + (row % CONTRACT_SPLIT_ROWS) * QI_PITCH;
-#pragma unroll
-            for (int t = 0; t < 6; ++t) {
-                bf16x4 a, b, cc;
-                split_tile(t, a, b, cc);
-                unsigned char* o = rp + 2 * (16 * t + 4 * lg);
-                *reinterpret_cast<bf16x4*>(o) = a;
-                *reinterpret_cast<bf16x4*>(o + QI_PLANE) = b;
-                *reinterpret_cast<bf16x4*>(o + 2 * QI_PLANE) = cc;
-            }
-            unsigned char* o = rp + 2 * (96 + lg);
-            *reinterpret_cast<__bf16*>(o) = y0;
-            *reinterpret_cast<__bf16*>(o + QI_PLANE) = y1;
-            *reinterpret_cast<__bf16*>(o + 2 * QI_PLANE) = y2;
-            reinterpret_cast<float*>(blk + 3 * QI_PLANE + (row % CONTRACT_SPLIT_ROWS) * 16)[lg] = h[6].x;
-        }
-#endif
     }
 #undef VIHMC_FB_LOAD
 #undef VIHMC_FB_STORE

@@ -132,7 +132,6 @@ struct ContractProb {
                                           //    operands, six products (k_contract_bf)
     const unsigned char* qimg; int64_t qimg_cs;   // bf16x6: Q pre-split into blocks (launch_split_blocks)
     float gscale;
-    int32_t rev_chains;                   // side B: > 0 = chain count, workgroups take the chains last first
 };
 
 // launchers (vihmc_kernels.hip)

@@ -754,14 +754,9 @@ hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in
                  inv_mass, K, sc ? *sc : ScatterArgs{});
 }
 
-// the plan's layers are exactly MlpBnn's widths (then the compile-time form runs); VIHMC_MLP_FIX=0: never
+// the plan's layers are exactly MlpBnn's widths (then the compile-time form runs)
 static bool mlp_is_bnn(const MlpArgs& a, int maxw) {
-    static const bool on = [] {
-        const char* e = std::getenv("VIHMC_MLP_FIX");
-        return !e || std::atoi(e) != 0;
-    }();
-    if (!on || a.n_layers != MlpBnn::NL || maxw != 10 || a.in_dim != MlpBnn::dim(0) ||
-        a.out_dim != MlpBnn::dim(MlpBnn::NL))
+    if (a.n_layers != MlpBnn::NL || maxw != 10 || a.in_dim != MlpBnn::dim(0) || a.out_dim != MlpBnn::dim(MlpBnn::NL))
         return false;
     for (int l = 0; l < MlpBnn::NL; ++l)
         if (a.L[l].n_in != MlpBnn::dim(l) || a.L[l].n_out != MlpBnn::dim(l + 1)) return false;
@@ -786,11 +781,7 @@ hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int ma
     MlpTrajArgs tt = t;
     tt.ws_floats = (int32_t)(ws / sizeof(float));
     const size_t cache = sizeof(float) * ((size_t)a.N * (a.in_dim + a.out_dim) + 4 * (size_t)a.K);
-    static const bool cache_on = [] {
-        const char* e = std::getenv("VIHMC_MLP_CACHE");
-        return !e || std::atoi(e) != 0;
-    }();
-    tt.cache = cache_on && shm + cache <= 160 * 1024 ? 1 : 0;
+    tt.cache = shm + cache <= 160 * 1024 ? 1 : 0;
     if (tt.cache) shm += cache;
     if (mlp_is_bnn(a, maxw)) VIHMC_LAUNCH((k_mlp_traj<0, MlpBnn>), dim3(C), dim3(64), shm, s, a, maxw, tt);
     VIHMC_LAUNCH(k_mlp_traj<0>, dim3(C), dim3(64), shm, s, a, maxw, tt);

@@ -148,7 +148,6 @@ struct vihmc_plan {
     int fwd_wimg = 1;
     int fuse_scatter = 1;       // plan option: trajectory evaluations take theta already scattered by the leapfrog
     int mlp_fast = 1;             // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
-    int contract_rev = 0;         // plan option: side B takes the chains last first
     int bwd_chain = 1;            // plan option: whole-network backward in one launch when the chunks are 64 rows
     bool timg_live = false;       // the W^T images hold this evaluation's theta (scatter-kept or split this evaluation)
     bool last_bwd_chain = false;  // the last gradient evaluation ran k_bwd_chain (get_option bwd_chain: bit 1)
@@ -920,7 +919,6 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         q.qimg = p->qsplitB;
         q.qimg_cs = p->qsplitB_cs;
         q.xcd_group = ((int64_t)C * p->qchunksB) % 8 == 0 ? 1 : 0;
-        q.rev_chains = p->contract_rev ? C : 0;
         q.b0 = p->packed;
         q.b0_cs = p->dp;
         q.out = p->partB;
@@ -1499,7 +1497,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, contract_rev, bwd_chain"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1512,7 +1510,6 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "fuse_scatter") p->fuse_scatter = value ? 1 : 0;
     else if (k == "img_scatter") p->img_by_scatter = value && p->smap_img;   // 0: split the images per evaluation
     else if (k == "mlp_fast") p->mlp_fast = value ? 1 : 0;
-    else if (k == "contract_rev") p->contract_rev = value ? 1 : 0;
     else if (k == "bwd_chain") p->bwd_chain = value ? 1 : 0;
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     // captured graphs embed the kernel choice
@@ -1532,7 +1529,6 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "fuse_scatter") *value = p->fuse_scatter;
     else if (k == "img_scatter") *value = p->img_by_scatter ? 1 : 0;
     else if (k == "mlp_fast") *value = p->mlp_fast && p->kind == 1 && mlp_bnn_fast_ok(p->mlp);
-    else if (k == "contract_rev") *value = p->contract_rev;
     else if (k == "bwd_chain") *value = p->bwd_chain | (p->last_bwd_chain ? 2 : 0);
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;

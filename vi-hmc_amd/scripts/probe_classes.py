@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default="")
     ap.add_argument("--opt", action="append", default=[], help="plan option key=value (repeatable)")
+    ap.add_argument("--config4", action="store_true",
+                    help="config 4's evaluation: one data shard of N/2 functions, every parameter sampled")
     args = ap.parse_args()
     spec = DeepONetSpec()
     prob = deeponet_problem(seed=0)
