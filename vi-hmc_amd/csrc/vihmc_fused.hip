@@ -429,8 +429,10 @@ __device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, co
     hn[6].x = v;
 }
 
-template <int NW>
-__global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
+// ND > 0 (images only): ND extra waves that only issue the weight-image DMA. With four compute waves (one chain) each
+// of them otherwise issues 17 one-KB DMA pieces per layer (~100 cycles each among its MFMAs).
+template <int NW, int ND = 0>
+__global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
     constexpr int FTHREADS = NW * 64;
     constexpr int FSLOTS = (FBLK4 + FTHREADS - 1) / FTHREADS;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsmb[];      // 2 x BBUF
@@ -445,6 +447,26 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
     const int rowc = min(row, N.rows - 1);
     const bool rok = row < N.rows;
     const float* Wc = args.packed + c * args.dp;
+    if (ND > 0 && wave >= NW) {
+        // DMA waves: image 0 before the first barrier, image j + 1 after barrier j, each drained before the barrier
+        // that publishes it; the same barrier sequence as the compute waves (zero fill, one per layer, epilogue)
+        const unsigned char* wimgd = N.wimg + c * N.wimg_cs;
+        for (int k = wave - NW; k < FWD_WIMG / 1024; k += ND)
+            bf6::glds16_asm(wimgd + k * 1024 + lane * 16, fsmb + k * 1024);
+        bf6::wait_vmcnt0();
+        __syncthreads();
+        for (int j = 0; j < N.nl; ++j) {
+            __syncthreads();
+            if (j + 1 < N.nl) {
+                for (int k = wave - NW; k < FWD_WIMG / 1024; k += ND)
+                    bf6::glds16_asm(wimgd + (int64_t)(j + 1) * FWD_WIMG + k * 1024 + lane * 16,
+                                    fsmb + ((j + 1) & 1) * FWD_WIMG + k * 1024);
+            }
+            bf6::wait_vmcnt0();
+        }
+        if (N.qimg != nullptr) __syncthreads();
+        return;
+    }
 
     // zero the never-written tail columns 100..111 of every plane row and the bias pad, both buffers
     // (register staging only: the pre-split images carry their zeros)
@@ -501,6 +523,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused_bf(FusedArgs args) {
     const bool dma = FWD_TAILF32 || FWD_DMA_ONLY || N.wimg != nullptr;  // FWD_TAILF32: images only (host-checked)
     const unsigned char* wimgc = dma ? N.wimg + c * N.wimg_cs : nullptr;
 #define VIHMC_FB_DMA(J, BUF)                                                                          \
+    if (ND == 0)                                                                                      \
     for (int k = wave; k < FWD_WIMG / 1024; k += NW)                                                  \
         bf6::glds16_asm(wimgc + (int64_t)(J) * FWD_WIMG + k * 1024 + lane * 16, fsmb + (BUF) * FWD_WIMG + k * 1024);
     if (dma) {
@@ -708,7 +731,9 @@ hipError_t launch_fwd_fused_bf(const FusedArgs& a, int nw, hipStream_t s) {
     dim3 g(a.C * (a.net[0].nblk + a.net[1].nblk));
     // 4 waves (64 rows per workgroup) for chain counts whose 12-wave grid would leave most CUs idle (single chain:
     // 176 workgroups instead of 60)
-    if (nw == 4) hipLaunchKernelGGL(k_fwd_fused_bf<4>, g, dim3(4 * 64), fwd_fused_bf_lds_bytes(), s, a);
+    if (nw == 4 && FWD_TAILF32 && a.net[0].wimg && a.net[1].wimg)
+        hipLaunchKernelGGL((k_fwd_fused_bf<4, 4>), g, dim3(8 * 64), fwd_fused_bf_lds_bytes(), s, a);
+    else if (nw == 4) hipLaunchKernelGGL(k_fwd_fused_bf<4>, g, dim3(4 * 64), fwd_fused_bf_lds_bytes(), s, a);
     else hipLaunchKernelGGL(k_fwd_fused_bf<FWD_BF_NW>, g, dim3(FWD_BF_NW * 64), fwd_fused_bf_lds_bytes(), s, a);
     return hipGetLastError();
 }
