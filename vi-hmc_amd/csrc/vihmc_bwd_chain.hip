@@ -56,6 +56,9 @@ __device__ __forceinline__ float act_grad(int act, float h) {
 #ifndef CH_STAMP
 #define CH_STAMP 0        // timing-only instrumentation (variant builds): in-kernel phase stamps
 #endif
+#ifndef CH_ABL
+#define CH_ABL 0          // timing-only ablation (wrong results): 1 = no dW MFMAs, 2 = no dX bf16 MFMAs
+#endif
 #if CH_STAMP
 // every 8th workgroup (the first 16 of them): per wave and layer, s_memtime after barrier A [0], when the compute
 // phase is done [2], after barrier B [3], when the write phase is done [4] ([1] = [0]); per workgroup s_memtime /
@@ -218,7 +221,10 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
 #pragma unroll
                             for (int p = 0; p < 3; ++p) db[p] = *reinterpret_cast<const bf16x8*>(drow + p * CH_PLANE + 64 * kb);
 #pragma unroll
-                            for (int u = 0; u < NU; ++u) ac[u] = six(wf[u][kb], db, ac[u]);
+                            for (int u = 0; u < NU; ++u) {
+                                if (CH_ABL == 2) asm volatile("" :: "v"(wf[u][kb][0]), "v"(db[0]), "v"(db[1]), "v"(db[2]));
+                                else ac[u] = six(wf[u][kb], db, ac[u]);
+                            }
                         }
                         // epilogue: act'(h_{j-1}) from the exact h planes
 #pragma unroll
@@ -307,6 +313,10 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                     if (t + 1 < nt) {
 #pragma unroll
                         for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(buf + CH_HP + p * CH_PLANE, tro, 16 * (t + 1));
+                    }
+                    if (CH_ABL == 1) {
+                        asm volatile("" :: "v"(da[0][0]), "v"(da[1][0]), "v"(hb[t & 1][0]), "v"(hb[t & 1][1]), "v"(hb[t & 1][2]));
+                        continue;
                     }
                     acc[0][t] = six(da[0], hb[t & 1], acc[0][t]);
                     if (t >= cb0 && t < cb1) acc[1][t] = six(da[1], hb[t & 1], acc[1][t]);
@@ -425,6 +435,6 @@ hipError_t launch_bwd_chain(const BwdChainArgs& a, hipStream_t s) {
 int bwd_chain_rows() { return CH_ROWS; }
 
 // timing-only / instrumentation switches this translation unit was built with (0 = product build)
-int diag_switches_bwd_chain() { return CH_STAMP << 8; }
+int diag_switches_bwd_chain() { return (CH_STAMP << 8) | CH_ABL; }
 
 }  // namespace vihmc

@@ -65,6 +65,9 @@ constexpr int CB_GLDS = CB_BLOCK / 1024;           // 22 wave-wide 16-B-per-lane
 
 }  // namespace
 
+#ifndef CB_DMA_ASM
+#define CB_DMA_ASM 0    // the D waves' chunk copies by asm LDS-DMA (no hipcc vmcnt(0) before their LDS reads)
+#endif
 #ifndef CB_STAMP
 #define CB_STAMP 0      // timing-only instrumentation (variant builds): in-kernel phase stamps, see below
 #endif
@@ -110,11 +113,17 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
     // of before its first LDS read) runs side A 3 % faster but the evaluation not at all: r03, 378 vs 390 us for side A,
     // 1.489 vs 1.488 ms per evaluation -- the other kernels slowed by as much (the chip is at its power limit)
 #define VIHMC_CB_BAR() __syncthreads();
+#if CB_DMA_ASM
+#define VIHMC_CB_GLDS(CI, BUF)                                                                              \
+    for (int k = wave - 8; k < CB_GLDS; k += CBA_DW)                                                        \
+        bf6::glds16_asm(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16, smc + (BUF) * CB_QIMG + k * 1024);
+#else
 #define VIHMC_CB_GLDS(CI, BUF)                                                                              \
     for (int k = wave - 8; k < CB_GLDS; k += CBA_DW)                                                        \
         __builtin_amdgcn_global_load_lds(                                                                   \
             reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
             (__attribute__((address_space(3))) void*)(smc + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
+#endif
     if (wave < 8) {
         // ---------------- S role ----------------
         const float* Own = P.Own + c * P.own_cs;
@@ -271,6 +280,9 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
     for (int t = 0; t < 7; ++t) dacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int tro = bf6::tr_lane_off(lr, lg);
     for (int i = 0; i <= nchunks; ++i) {
+#if CB_DMA_ASM
+        bf6::wait_vmcnt0();                            // this wave's copies of chunk i (invisible to hipcc) landed
+#endif
         VIHMC_CB_BAR()
         VIHMC_CB_STAMP(i, 0)
         // chunk i+1 -> buffer (i+1)%3 (last read by this role in iteration i-1, by S in i-2); the copies
@@ -278,6 +290,9 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
         if (i + 1 < nchunks) {
             VIHMC_CB_GLDS(i + 1, (i + 1) % CB_NQBUF)
         }
+#if CB_STAMP == 2
+        VIHMC_CB_STAMP(i, 2)                           // D waves: mid = the copies issued
+#endif
         if (i >= 1) {
             const unsigned char* img = smc + ((i - 1) % CB_NQBUF) * CB_QIMG;
             const unsigned char* gimg = smc + CB_NQBUF * CB_QIMG + ((i - 1) & 1) * CB_GIMG + w * (CB_GIMG / 8);
@@ -293,7 +308,9 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
             }
 #if CB_STAMP
             asm volatile("" :: "v"(ga[0]), "v"(ga[2]));
+#if CB_STAMP == 1
             VIHMC_CB_STAMP(i, 2)
+#endif
 #endif
 #pragma unroll
             for (int t = 0; t < 7; ++t) {

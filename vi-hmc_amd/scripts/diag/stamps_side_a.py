@@ -30,7 +30,7 @@ WG, CH = 24, 40
 def main():
     spec = DeepONetSpec()
     prob = deeponet_problem(seed=0)
-    C = 16
+    C = int(os.environ.get("STAMP_CHAINS", "16"))
     eng = DeepONetEngine(spec, prob.branch_in, trunk_features(prob.trunk_in), prob.y, prob.mu, prob.grad_ind, 0.0, 0.1,
                          "NLL", 1.0, max_chains=C, device="cuda:0")
     th = torch.tensor(np.tile(prob.mu[prob.grad_ind], (C, 1)), device="cuda:0")
@@ -51,10 +51,14 @@ def main():
     cyc = rl[ok, 1, 0] - rl[ok, 0, 0]
     us = (rl[ok, 1, 1] - rl[ok, 0, 1]) / 100.0
     print(f"workgroups sampled: {ok.sum()}  duration {us.mean():.1f} us  shader clock {np.mean(cyc / us) / 1e3:.3f} GHz "
-          f"(min {np.min(cyc / us) / 1e3:.3f}, max {np.max(cyc / us) / 1e3:.3f})")
-    nch = 33   # 32 chunks + the D role's trailing iteration
+          f"(min {np.min(cyc / us) / 1e3:.3f}, max {np.max(cyc / us) / 1e3:.3f}), cycles {np.mean(cyc):.0f}")
     per, s_work, d_work, skew, s_late, d_late, s_mid, d_mid = [], [], [], [], [], [], [], []
+    pro, epi, nchs = [], [], []
     for g in np.nonzero(ok)[0]:
+        nch = int((st[g, 8, :, 0] > 0).sum())   # the D role's iterations: the chunks + its trailing one
+        pro.append(st[g, :, 0, 0].min() - rl[g, 0, 0])
+        epi.append(rl[g, 1, 0] - st[g, :, nch - 1, 0].max())
+        nchs.append(nch)
         bar = st[g, :, :nch, 0]
         end = st[g, :, :nch, 1]
         mid = st[g, :, :nch, 2]
@@ -69,7 +73,10 @@ def main():
             d_mid.append(np.mean(mid[8:, i] - bar[8:, i]))
             d_late.append(np.max(end[8:, i]) - t0)
     f = lambda a: f"{np.mean(a):7.0f} (p10 {np.percentile(a, 10):6.0f}, p90 {np.percentile(a, 90):6.0f})"  # noqa: E731
-    print("cycles per chunk (shader clock), steady-state chunks 1..31:")
+    print(f"chunks per workgroup (D role iterations) {np.mean(nchs):.1f}")
+    print(f"  prologue (start -> first barrier exit) {f(pro)}")
+    print(f"  epilogue (last barrier exit -> end)     {f(epi)}")
+    print("cycles per chunk (shader clock), steady-state chunks:")
     print(f"  barrier period              {f(per)}")
     print(f"  barrier-exit skew            {f(skew)}")
     print(f"  S role work (mean wave)      {f(s_work)}")
