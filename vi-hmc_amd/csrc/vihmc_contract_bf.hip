@@ -65,9 +65,6 @@ constexpr int CB_GLDS = CB_BLOCK / 1024;           // 22 wave-wide 16-B-per-lane
 
 }  // namespace
 
-#ifndef CB_DMA_ASM
-#define CB_DMA_ASM 0    // the D waves' chunk copies by asm LDS-DMA (no hipcc vmcnt(0) before their LDS reads)
-#endif
 #ifndef CB_STAMP
 #define CB_STAMP 0      // timing-only instrumentation (variant builds): in-kernel phase stamps, see below
 #endif
@@ -107,23 +104,17 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
     const int nchunks = q_hi > q_lo ? (q_hi - q_lo + CB_QC - 1) / CB_QC : 0;
 
     // Q chunks: blocks of the pre-split image (vihmc_split_blocks), copied global -> LDS by the D waves
-    // with wave-wide DMA (global_load_lds_dwordx4: 1 KB per instruction, no VGPRs, no VALU)
+    // with wave-wide DMA (global_load_lds_dwordx4: 1 KB per instruction, no VGPRs, no VALU), issued by asm:
+    // with the builtin, hipcc waited vmcnt(0) -- for the copies just issued -- before the D waves' first LDS
+    // read of every chunk; the asm copies are retired by the wave's own vmcnt(0) before the next barrier.
+    // r03: side A 0.366 vs 0.385 ms at 16 chains, neutral at one chain (profiles/r03_side_a/asm_dma_*).
+    // Moving the copies to the S waves (4 buffers, two chunks ahead) and a one-role kernel with G kept in
+    // registers (8 waves, both products in every wave) were bitwise equal and slower: profiles/r03_side_a/.
     const unsigned char* qblk = P.qimg + c * P.qimg_cs + (int64_t)(q_lo / CB_QC) * CB_BLOCK;
-    // side A's image by the builtin LDS-DMA. The asm form (the wait for chunk i+1 at the end of the D iteration instead
-    // of before its first LDS read) runs side A 3 % faster but the evaluation not at all: r03, 378 vs 390 us for side A,
-    // 1.489 vs 1.488 ms per evaluation -- the other kernels slowed by as much (the chip is at its power limit)
 #define VIHMC_CB_BAR() __syncthreads();
-#if CB_DMA_ASM
 #define VIHMC_CB_GLDS(CI, BUF)                                                                              \
     for (int k = wave - 8; k < CB_GLDS; k += CBA_DW)                                                        \
         bf6::glds16_asm(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16, smc + (BUF) * CB_QIMG + k * 1024);
-#else
-#define VIHMC_CB_GLDS(CI, BUF)                                                                              \
-    for (int k = wave - 8; k < CB_GLDS; k += CBA_DW)                                                        \
-        __builtin_amdgcn_global_load_lds(                                                                   \
-            reinterpret_cast<const void*>(qblk + (int64_t)(CI) * CB_BLOCK + k * 1024 + lane * 16),          \
-            (__attribute__((address_space(3))) void*)(smc + (BUF) * CB_QIMG + k * 1024), 16, 0, 0);
-#endif
     if (wave < 8) {
         // ---------------- S role ----------------
         const float* Own = P.Own + c * P.own_cs;
@@ -269,9 +260,6 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
     }
 
     // ---------------- D role ----------------
-    // The chunk-0 DMA is issued here, on the D waves' own path: issued before the role split, hipcc's wait
-    // analysis (one per kernel, not per role) carried a pending LDS-DMA into the S role's loop head and waited
-    // vmcnt -- i.e. for the S waves' own G^T stores and target loads -- before their LDS reads of every chunk.
     if (nchunks > 0) {
         VIHMC_CB_GLDS(0, 0)
     }
@@ -280,9 +268,7 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
     for (int t = 0; t < 7; ++t) dacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int tro = bf6::tr_lane_off(lr, lg);
     for (int i = 0; i <= nchunks; ++i) {
-#if CB_DMA_ASM
         bf6::wait_vmcnt0();                            // this wave's copies of chunk i (invisible to hipcc) landed
-#endif
         VIHMC_CB_BAR()
         VIHMC_CB_STAMP(i, 0)
         // chunk i+1 -> buffer (i+1)%3 (last read by this role in iteration i-1, by S in i-2); the copies
