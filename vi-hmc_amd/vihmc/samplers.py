@@ -309,21 +309,24 @@ class HMCRunner:
         sub = eps / (2 * (M - 1))
         g0_cached = g if self.reuse else None
         gm = lp0_end = None
+        # one fused kernel per update (torch.add with alpha; eps is a host float here) instead of a scale and
+        # an add: config 4's per-step updates between the engine evaluations are launch-bound
+        half = 0.5 * eps
         for _ in range(L):
             for m in range(M):
                 if m == 0 and g0_cached is not None:
                     gm = g0_cached
                 else:
                     _, gm = evs[m].logp_grad(th)
-                p = p + (0.5 * eps) * gm
+                p = torch.add(p, gm, alpha=half) if not torch.is_tensor(eps) else p + half * gm
                 if m < M - 1:
-                    th = th + sub * p
+                    th = torch.add(th, p, alpha=sub) if not torch.is_tensor(eps) else th + sub * p
             for m in reversed(range(M)):
                 if not (m == M - 1 and self.reuse):      # same theta as the forward pass' last shard
                     lp0_end, gm = evs[m].logp_grad(th)
-                p = p + (0.5 * eps) * gm
+                p = torch.add(p, gm, alpha=half) if not torch.is_tensor(eps) else p + half * gm
                 if m > 0:
-                    th = th + sub * p
+                    th = torch.add(th, p, alpha=sub) if not torch.is_tensor(eps) else th + sub * p
             g0_cached = gm if self.reuse else None
         lp_sum = lp0_end.clone()
         for m in range(1, M):
