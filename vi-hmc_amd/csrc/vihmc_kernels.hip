@@ -100,14 +100,16 @@ __device__ __forceinline__ void scatter_one(float* packed, int64_t dp, const int
     }
 }
 
-__global__ void k_scatter(float* packed, int64_t dp, const float* theta, int K, const int32_t* smap_w,
-                          const int32_t* smap_wt, ScatterImg si) {
+// one element per thread (a grid-stride loop left each thread's scattered stores' index loads serial: 10 us for
+// config 4's 172,401 parameters)
+__global__ __launch_bounds__(256) void k_scatter(float* packed, int64_t dp, const float* theta, int K,
+                                                 const int32_t* smap_w, const int32_t* smap_wt, ScatterImg si) {
     const int c = blockIdx.y;
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x)
-        scatter_one(packed, dp, smap_w, smap_wt, si, c, k, theta[(int64_t)c * K + k]);
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < K) scatter_one(packed, dp, smap_w, smap_wt, si, c, k, theta[(int64_t)c * K + k]);
 }
 
-__device__ double block_sum_256(double v, double* sh) {
+__device__ double block_sum(double v, double* sh) {
     v = wave_sum(v);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) sh[w] = v;
@@ -128,8 +130,8 @@ __device__ void contract_stats_body(const StatsJob& J, int c) {
         ssq += st[2 * i];
         gs += st[2 * i + 1];
     }
-    ssq = block_sum_256(ssq, sh);
-    gs = block_sum_256(gs, sh);
+    ssq = block_sum(ssq, sh);
+    gs = block_sum(gs, sh);
     if (threadIdx.x == 0) {
         double ll;
         if (J.loss == 0) {
@@ -353,43 +355,62 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
 constexpr int GATHER_SPLIT = GATHER_SPLIT_N;
 static_assert(GATHER_SPLIT <= GATHER_SPLIT_MAX, "lp_part slots");
 
+// 1024 threads, GATHER_U elements a thread per pass with every load of the pass issued before the first use: a
+// one-element loop waited out the dependent smap -> gp gather latency per element (12.5 us for config 4's
+// 172,401 parameters in 64 slices; one pass now)
+constexpr int GATHER_THREADS = 1024, GATHER_U = 4;
 template <bool LEAP>
-__global__ __launch_bounds__(256) void k_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap,
-                                                      const float* theta, int K, const float* prior_mu,
-                                                      const float* prior_inv_var, float prior_scale,
-                                                      float* grad, double* lp_part, LeapArgs lf) {
-    __shared__ double sh[8];
+__global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap,
+                                                                 const float* theta, int K, const float* prior_mu,
+                                                                 const float* prior_inv_var, float prior_scale,
+                                                                 float* grad, double* lp_part, LeapArgs lf) {
+    __shared__ double sh[GATHER_THREADS / 64];
     const int c = blockIdx.y;
     const int per = (K + gridDim.x - 1) / gridDim.x;
     const int k0 = blockIdx.x * per, k1 = min(K, k0 + per);
     const float inv_scale = 1.f / prior_scale;
+    const float* gpc = gp + c * gp_cs;
     double lp = 0.0;
-    for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) {
-        const int64_t o = (int64_t)c * K + k;
-        const float th = theta[o];
-        const float d = th - prior_mu[k];
-        const float iv = prior_inv_var[k];
-        lp += -0.5 * (double)d * (double)d * (double)iv;
-        // one explicit fma after a rounded product: the same rounding in both instantiations whatever the
-        // contraction pragma around them (the fused trajectory is bitwise the step-by-step path)
-        const float g = __builtin_fmaf(-__fmul_rn(d, iv), inv_scale, gp[c * gp_cs + smap[k]]);
-        if (grad) grad[o] = g;
-        if (LEAP) {
+    for (int kb = k0 + threadIdx.x; kb < k1; kb += GATHER_U * GATHER_THREADS) {
+        float thv[GATHER_U], muv[GATHER_U], ivv[GATHER_U], gpv[GATHER_U];
+#pragma unroll
+        for (int u = 0; u < GATHER_U; ++u) {
+            const int k = min(kb + u * GATHER_THREADS, k1 - 1);
+            thv[u] = theta[(int64_t)c * K + k];
+            muv[u] = prior_mu[k];
+            ivv[u] = prior_inv_var[k];
+            gpv[u] = gpc[smap[k]];
+        }
+#pragma unroll
+        for (int u = 0; u < GATHER_U; ++u) {
+            const int k = kb + u * GATHER_THREADS;
+            if (k >= k1) break;
+            const int64_t o = (int64_t)c * K + k;
+            const float th = thv[u];
+            const float d = th - muv[u];
+            const float iv = ivv[u];
+            lp += -0.5 * (double)d * (double)d * (double)iv;
+            // one explicit fma after a rounded product: the same rounding in both instantiations whatever the
+            // contraction pragma around them (the fused trajectory is bitwise the step-by-step path)
+            const float g = __builtin_fmaf(-__fmul_rn(d, iv), inv_scale, gpv[u]);
+            if (grad) grad[o] = g;
+            if (LEAP) {
 #pragma clang fp contract(off)
-            const float e = lf.eps[c];
-            float pn = lf.p[o] + e * g;
-            if (lf.last) {
-                pn = pn - (0.5f * e) * g;
-            } else {
-                const float step = lf.inv_mass ? (e * lf.inv_mass[k]) * pn : e * pn;
-                const float tn = th + step;
-                lf.th[o] = tn;
-                if (lf.sc.packed) scatter_one(lf.sc.packed, lf.sc.dp, lf.sc.smap_w, lf.sc.smap_wt, lf.sc.si, c, k, tn);
+                const float e = lf.eps[c];
+                float pn = lf.p[o] + e * g;
+                if (lf.last) {
+                    pn = pn - (0.5f * e) * g;
+                } else {
+                    const float step = lf.inv_mass ? (e * lf.inv_mass[k]) * pn : e * pn;
+                    const float tn = th + step;
+                    lf.th[o] = tn;
+                    if (lf.sc.packed) scatter_one(lf.sc.packed, lf.sc.dp, lf.sc.smap_w, lf.sc.smap_wt, lf.sc.si, c, k, tn);
+                }
+                lf.p[o] = pn;
             }
-            lf.p[o] = pn;
         }
     }
-    lp = block_sum_256(lp, sh);
+    lp = block_sum(lp, sh);
     if (threadIdx.x == 0) lp_part[c * gridDim.x + blockIdx.x] = lp;
 }
 
@@ -712,7 +733,7 @@ hipError_t launch_init_packed(float* packed, int64_t dp, int C, const float* fro
 
 hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, int K, const int32_t* smap_w,
                           const int32_t* smap_wt, hipStream_t s, const ScatterImg* si) {
-    dim3 g((unsigned)std::min((K + 255) / 256, 256), C), blk(256);
+    dim3 g((unsigned)((K + 255) / 256), C), blk(256);
     VIHMC_LAUNCH(k_scatter, g, blk, 0, s, packed, dp, theta, K, smap_w, smap_wt, si ? *si : ScatterImg{});
 }
 
@@ -734,10 +755,10 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
                                double* lp_part, hipStream_t s, const LeapArgs* leap) {
     if (leap)
-        hipLaunchKernelGGL(k_gather_prior<true>, dim3(GATHER_SPLIT, C), dim3(256), 0, s, gp, gp_cs, smap, theta, K,
+        hipLaunchKernelGGL(k_gather_prior<true>, dim3(GATHER_SPLIT, C), dim3(GATHER_THREADS), 0, s, gp, gp_cs, smap, theta, K,
                            prior_mu, prior_inv_var, prior_scale, grad, lp_part, *leap);
     else
-        hipLaunchKernelGGL(k_gather_prior<false>, dim3(GATHER_SPLIT, C), dim3(256), 0, s, gp, gp_cs, smap, theta, K,
+        hipLaunchKernelGGL(k_gather_prior<false>, dim3(GATHER_SPLIT, C), dim3(GATHER_THREADS), 0, s, gp, gp_cs, smap, theta, K,
                            prior_mu, prior_inv_var, prior_scale, grad, lp_part, LeapArgs{});
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || logp == nullptr) return e;   // no log-prob wanted (inner leapfrog steps)

@@ -30,10 +30,16 @@ def main():
                     help="config 4's evaluation: one data shard of N/2 functions, every parameter sampled")
     args = ap.parse_args()
     spec = DeepONetSpec()
-    prob = deeponet_problem(seed=0)
     C = args.chains
-    eng = DeepONetEngine(spec, prob.branch_in, trunk_features(prob.trunk_in), prob.y, prob.mu, prob.grad_ind, 0.0, 0.1,
-                         "NLL", 1.0, max_chains=C, device="cuda:0")
+    if args.config4:        # bench.py leg_split_c1's first shard
+        prob = deeponet_problem(seed=0, k=None)
+        half = prob.N // 2
+        eng = DeepONetEngine(spec, prob.branch_in[:half], trunk_features(prob.trunk_in), prob.y[:half], prob.mu,
+                             prob.grad_ind, 0.0, 0.1, "NLL", 1.0, prior_scale=2.0, max_chains=C, device="cuda:0")
+    else:
+        prob = deeponet_problem(seed=0)
+        eng = DeepONetEngine(spec, prob.branch_in, trunk_features(prob.trunk_in), prob.y, prob.mu, prob.grad_ind, 0.0,
+                             0.1, "NLL", 1.0, max_chains=C, device="cuda:0")
     for kv in args.opt:
         k, v = kv.split("=")
         eng.option(k, int(v))
