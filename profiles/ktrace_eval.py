@@ -1,5 +1,5 @@
 """Per-dispatch kernel durations of ONE evaluation from a rocprofv3 kernel trace (profiles/scripts/ktrace.sh):
-the last complete evaluation (k_scatter ... k_logp_finalize) in dispatch order.
+the last complete evaluation (k_scatter ... the gradient gather) in dispatch order.
 Usage: python profiles/ktrace_eval.py gpurun_out/<tag>_kt"""
 import csv
 import glob

@@ -212,10 +212,17 @@ struct LeapArgs {
     ScatterArgs sc;         // scatter the new theta (not on the last step); packed == null: the next evaluation does
     int32_t scattered_in;   // this evaluation's theta is already scattered (skip its k_scatter)
 };
+// the log-prob finalisation fused into the gradient gather (logp == null: none); cnt: [maxC] zeroed counters
+struct FinalizeArgs {
+    float* logp;
+    const float* lik;
+    double prior_const;
+    uint32_t* cnt;
+};
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
                                const float* prior_mu, const float* prior_inv_var, double prior_const,
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
-                               double* lp_part, hipStream_t s, const LeapArgs* leap = nullptr);
+                               double* lp_part, uint32_t* fin_cnt, hipStream_t s, const LeapArgs* leap = nullptr);
 // the opening half step and first position step of a trajectory: p_out = p_in + (eps / 2) g_in,
 // th_out = th_in + eps p_out (eps inv_mass p_out)
 hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out, const float* g_in,

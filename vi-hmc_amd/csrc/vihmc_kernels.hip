@@ -363,7 +363,8 @@ template <bool LEAP>
 __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap,
                                                                  const float* theta, int K, const float* prior_mu,
                                                                  const float* prior_inv_var, float prior_scale,
-                                                                 float* grad, double* lp_part, LeapArgs lf) {
+                                                                 float* grad, double* lp_part, LeapArgs lf,
+                                                                 FinalizeArgs fin) {
     __shared__ double sh[GATHER_THREADS / 64];
     const int c = blockIdx.y;
     const int per = (K + gridDim.x - 1) / gridDim.x;
@@ -412,6 +413,28 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp
     }
     lp = block_sum(lp, sh);
     if (threadIdx.x == 0) lp_part[c * gridDim.x + blockIdx.x] = lp;
+    if (fin.logp == nullptr) return;
+    // log-prob finalisation by the chain's last block to finish (k_logp_finalize's fixed butterfly, so bitwise the
+    // separate launch it replaces): release the partial, count it, and the block that completes the count
+    // acquires every partial and resets the counter for the next evaluation (or graph replay)
+    __shared__ int is_last;
+    if (threadIdx.x == 0) {
+        __threadfence();
+        is_last = atomicAdd(fin.cnt + c, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!is_last || threadIdx.x >= 64) return;
+    __threadfence();
+    const int lane = threadIdx.x;
+    double t = lane < (int)gridDim.x ? __hip_atomic_load(lp_part + c * gridDim.x + lane, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) {
+        fin.logp[c] = (float)((double)fin.lik[c] + (t + fin.prior_const) / (double)prior_scale);
+        fin.cnt[c] = 0u;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out,
@@ -429,16 +452,6 @@ __global__ __launch_bounds__(256) void k_leap_open(const float* th_in, float* th
         th_out[o] = tn;
         if (sc.packed) scatter_one(sc.packed, sc.dp, sc.smap_w, sc.smap_wt, sc.si, c, k, tn);
     }
-}
-
-// One wave per chain: lane i holds partial i (nparts <= 64), summed by a fixed xor butterfly (deterministic).
-__global__ __launch_bounds__(64) void k_logp_finalize(const double* lp_part, int nparts, const float* lik,
-                                                      double prior_const, float prior_scale, float* logp) {
-    const int c = blockIdx.x, lane = threadIdx.x;
-    double lp = lane < nparts ? lp_part[c * nparts + lane] : 0.0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) lp += __shfl_xor(lp, o, 64);
-    if (lane == 0) logp[c] = (float)((double)lik[c] + (lp + prior_const) / (double)prior_scale);
 }
 
 // =============================================================================================
@@ -753,18 +766,18 @@ hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_wa
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,
                                const float* prior_mu, const float* prior_inv_var, double prior_const,
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
-                               double* lp_part, hipStream_t s, const LeapArgs* leap) {
-    if (leap)
-        hipLaunchKernelGGL(k_gather_prior<true>, dim3(GATHER_SPLIT, C), dim3(GATHER_THREADS), 0, s, gp, gp_cs, smap, theta, K,
-                           prior_mu, prior_inv_var, prior_scale, grad, lp_part, *leap);
-    else
-        hipLaunchKernelGGL(k_gather_prior<false>, dim3(GATHER_SPLIT, C), dim3(GATHER_THREADS), 0, s, gp, gp_cs, smap, theta, K,
-                           prior_mu, prior_inv_var, prior_scale, grad, lp_part, LeapArgs{});
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || logp == nullptr) return e;   // no log-prob wanted (inner leapfrog steps)
+                               double* lp_part, uint32_t* fin_cnt, hipStream_t s, const LeapArgs* leap) {
     static_assert(GATHER_SPLIT <= 64, "one lane per partial");
-    VIHMC_LAUNCH(k_logp_finalize, dim3(C), dim3(64), 0, s, lp_part, GATHER_SPLIT, lik, prior_const, prior_scale,
-                 logp);
+    // logp == null: no log-prob wanted (inner leapfrog steps); else the last block of each chain finalises it
+    const FinalizeArgs fin{logp, lik, prior_const, fin_cnt};
+    if (logp && !fin_cnt) return hipErrorInvalidValue;
+    if (leap)
+        hipLaunchKernelGGL(k_gather_prior<true>, dim3(GATHER_SPLIT, C), dim3(GATHER_THREADS), 0, s, gp, gp_cs, smap,
+                           theta, K, prior_mu, prior_inv_var, prior_scale, grad, lp_part, *leap, fin);
+    else
+        hipLaunchKernelGGL(k_gather_prior<false>, dim3(GATHER_SPLIT, C), dim3(GATHER_THREADS), 0, s, gp, gp_cs, smap,
+                           theta, K, prior_mu, prior_inv_var, prior_scale, grad, lp_part, LeapArgs{}, fin);
+    return hipGetLastError();
 }
 
 hipError_t launch_leap_open(const float* th_in, float* th_out, const float* p_in, float* p_out, const float* g_in,

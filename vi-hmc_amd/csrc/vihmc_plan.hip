@@ -84,6 +84,7 @@ struct vihmc_plan {
     double prior_const = 0.0;
     float* lik_buf = nullptr;
     double* lp_part = nullptr;            // [maxC][GATHER_SPLIT_MAX] partial log-priors
+    uint32_t* fin_cnt = nullptr;          // [maxC] blocks of the gradient gather done (its last block finalises)
 
     // DeepONet
     int N = 0, P = 0, W = 0, ldz = 0;
@@ -527,6 +528,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         if (int rc = p->alloc(&p->stats, p->stats_cs * C)) return rc;
         if (int rc = p->alloc(&p->lik_buf, C)) return rc;
         if (int rc = p->alloc(&p->lp_part, (int64_t)C * GATHER_SPLIT_MAX)) return rc;
+        if (int rc = p->alloc(&p->fin_cnt, C)) return rc;
     }
     // reduce jobs
     {
@@ -1001,7 +1003,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         HIPCHK(launch_reduce(p->bwd_bf16x6 ? p->jobsWt : p->jobsW, p->n_jobsW, p->max_lenW, C, s, &stats_job));
     }
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
-                               p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, s,
+                               p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, p->fin_cnt, s,
                                want_grad ? leap : nullptr));
     return 0;
 }
@@ -1266,7 +1268,7 @@ int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, con
         for (int st = 0; st < L; ++st) {
             LeapArgs lf{p_out, theta_out, eps, inv_mass, st == L - 1 ? 1 : 0, fuse && st < L - 1 ? sc : ScatterArgs{},
                         fuse ? 1 : 0};
-            // only the end point's log-prob is returned: the intermediate evaluations skip k_logp_finalize
+            // only the end point's log-prob is returned: the intermediate evaluations skip the log-prob finalisation
             if (int rc = deeponet_eval(p, theta_out, C, st == L - 1 ? logp_out : nullptr, g_out, nullptr, s, &lf))
                 return rc;
         }
