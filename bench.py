@@ -139,7 +139,9 @@ def cpu_throughput(procs, seconds, L, step_size):
 KCLASS = {0: ("contract_a", "k_contract_bf", "side-A contraction: S = Z_b Z_t^T + b, Gaussian NLL, G, dZ_trunk"),
           1: ("contract_b", "k_contract_bf_b", "side-B contraction: dZ_branch = G Z_trunk"),
           2: ("bwd", "k_bwd_bf2", "layer backward (dX and dW of both MLPs), one launch per layer"),
-          3: ("fwd", "k_fwd_fused_bf", "fused hidden-layer forward of both MLPs (layers 1..8)")}
+          3: ("fwd", "k_fwd_fused_bf", "fused hidden-layer forward of both MLPs (layers 1..8)"),
+          6: ("gram", "k_gram_a + k_gram_b + k_gram_c (+ k_gram_aug)",
+              "Gram-form gradient-only contraction of the inner leapfrog steps: y Zt^, y^T Zb^, Gram terms")}
 T_EVAL = 4
 CAL_STEPS = 2          # untimed HMC iterations with every kernel class under HIP events
 
@@ -153,8 +155,9 @@ def mfma_peak(bf16x6: int) -> float:
 def class_table(eng, spec, prob, C, evals):
     """Per-class HIP-event times recorded over `evals` evaluations -> per-launch roofline numbers."""
     fl = spec.flops_by_kernel(prob.N, prob.P)
+    fl["gram"] = spec.flops_gram(prob.N, prob.P)
     forms = {"contract_a": eng.get_option("contract_bf16x6"), "contract_b": eng.get_option("contract_bf16x6"),
-             "bwd": eng.get_option("bwd_bf16x6"), "fwd": eng.get_option("fwd_bf16x6")}
+             "bwd": eng.get_option("bwd_bf16x6"), "fwd": eng.get_option("fwd_bf16x6"), "gram": 1}
     ev_ms, ev_n = eng.timing_class(T_EVAL)
     eval_ms = ev_ms / max(ev_n, 1)
     out = {}
@@ -425,13 +428,14 @@ def main():
     value = leapfrog / T
     key, kname, what = KCLASS[dom_cls]
     fl = spec.flops_by_kernel(prob.N, prob.P)
+    fl["gram"] = spec.flops_gram(prob.N, prob.P)
     per_eval = cal[key]["launches_per_eval"]
     flops_launch = C * fl[key] / per_eval
     avg_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = flops_launch / avg_s / 1e12 if k_n else None
     evals_per_s = world * grad_evals / T
     form_key = {"contract_a": "contract_bf16x6", "contract_b": "contract_bf16x6", "bwd": "bwd_bf16x6",
-                "fwd": "fwd_bf16x6"}[key]
+                "fwd": "fwd_bf16x6", "gram": "contract_bf16x6"}[key]
     bf = eng.get_option(form_key)
     peak = mfma_peak(bf)
     traffic, tsrc = load_traffic(kname, C)

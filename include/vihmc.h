@@ -113,6 +113,12 @@ int vihmc_mlp_plan_create(vihmc_plan** out, const vihmc_mlp_desc* d,
  * main_VI_HMC_burgers.py:86-178 / main_VI_HMC.py:96-151. grad may be NULL (value only). */
 int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, void* stream);
 
+/* d log p / d theta_c only (no log-prob): the leapfrog's inner gradient evaluations (hamiltorch's params_grad
+ * between the position updates, SURVEY.md App. A.2, whose log-prob value is discarded). DeepONet plans with
+ * width 100 and C >= the plan option "gram_min_chains" use the Gram-form contraction (vihmc_gram.hip: no N x P
+ * residual, plan option "gram"); vihmc_trajectory uses the same path for its inner steps. */
+int vihmc_grad(vihmc_plan* p, const float* theta, int C, float* grad, void* stream);
+
 /* Forward only: logp [C] and the network output out [C, N, P] (DeepONet) or [C, N, out_dim] (BNN).
  * Replaces log_prob_func(..., predict=True) -> (logp, output) (main_VI_HMC_burgers.py:175-176). */
 int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* out, void* stream);
@@ -182,7 +188,9 @@ enum {
     VIHMC_T_FWD = 3,          /* fused hidden-layer forward (k_fwd_fused_bf / k_fwd_fused) */
     VIHMC_T_EVAL = 4,         /* one whole DeepONet evaluation, first to last launch */
     VIHMC_T_MLP = 5,          /* BNN evaluation (k_mlp) */
-    VIHMC_T_COUNT = 6
+    VIHMC_T_GRAM = 6,         /* Gram-form gradient-only contraction (k_gram_aug, k_gram_a, k_gram_b, k_gram_c): one
+                                 event pair brackets the four launches */
+    VIHMC_T_COUNT = 7
 };
 int vihmc_timing_enable(vihmc_plan* p, int which, int on);
 int vihmc_timing_read(vihmc_plan* p, double* total_ms, int64_t* launches);
@@ -201,7 +209,9 @@ int vihmc_graph_enable(vihmc_plan* p, int on);
  * "contract_bf16x6" (default 1): the same for the side-A contraction (branch x trunk S, likelihood,
  * G, dZ_trunk; width 100) and side B. "bwd_bf16x6" (default 1): the same for the layer backward (dX,
  * dW, db of layers with 100 outputs); its default (environment VIHMC_BWD_BF16) also sizes the backward
- * row chunks at plan creation. "graph" = vihmc_graph_enable. Changing an option drops captured graphs.
+ * row chunks at plan creation. "graph" = vihmc_graph_enable. "gram" (default 1): gradient-only DeepONet
+ * evaluations (vihmc_grad, the inner steps of vihmc_trajectory) in Gram form; "gram_min_chains" (default 2): the
+ * smallest chain count that uses it. Changing an option drops captured graphs.
  * Returns nonzero for an unknown key. */
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value);
 /* Current value of an option (contract_bf16x6 reads 1 only where the bf16x6 contraction applies,

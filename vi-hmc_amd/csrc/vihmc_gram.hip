@@ -1,0 +1,503 @@
+// Gradient-only contraction in Gram form (the leapfrog's inner evaluations, where no log-prob is returned).
+//
+// Replaces the autograd backward of torch.einsum("...i,...i->...", xb, xtr) + b and the Gaussian NLL
+// (Operator_network/VI_HMC/my_make_func.py:79-82, main_VI_HMC_burgers.py:157-163) when only the gradient is
+// needed. With the augmented outputs Zb^ = [Z_b | 1] (N x 101) and Zt^ = [Z_t | b0] (P x 101) the prediction is
+// S + b0 = Zb^ Zt^T and G = gscale (Zb^ Zt^T - y), so
+//     dZb^ = G Zt^ = gscale (Zb^ Gt - y Zt^),      Gt = Zt^T Zt^   (101 x 101)
+//     dZt^ = G^T Zb^ = gscale (Zt^ Gb - y^T Zb^),  Gb = Zb^T Zb^
+// and d ll / d b0 = sum G = sum_p dZt^[p][100]. The N x P residual is never formed: the two products with the
+// data y (shared by every chain, pre-split once per plan) are plain GEMMs over all chains, and the Gram terms are
+// W x W. Per chain 2 N P W + O((N + P) W^2) MACs instead of 3 N P W, no G^T hand-off, no per-element VALU.
+// The log-likelihood value itself (sum r^2) is not computed here: with a good fit it is a small difference of
+// large Gram-form terms, so evaluations that return the log-prob keep the residual form (k_contract_bf).
+//
+// Products are bf16x6 (vihmc_bf16x6.h): every operand pre-split into three bf16 planes, six MFMA products per
+// 32-long k-block, fp32 accumulation -- fp32-level accuracy, no splits inside the loops.
+//
+// Kernels (one evaluation, C chains):
+//   k_gram_aug   feature 100 of the pre-split output images: 1 (branch rows < N), b0 (trunk rows < P)
+//   k_gram_a     T_b = y Zt^ over the trunk image (split-K partial slabs), Gt = Zt^T Zt^ (split-K, the last
+//                slab of a chain sums them in fixed order), Gb = Zb^T Zb^ (written negated, pre-split, as the
+//                B blocks of k_gram_b's extension)
+//   k_gram_b     dZt = -gscale (y^T Zb^ - Zt^ Gb) over the branch image + 4 extension blocks; d ll / d b0 slots
+//   k_gram_c     dZb = gscale (Zb^ Gt - sum_s T_b slab s)
+// Images: the contraction's pre-split blocks (k_split_blocks' layout, written by the fused forward): block =
+// 3 planes [32 rows][112 features] bf16, 224-B rows. The B operand (rows = k) is read with ds_read_b64_tr_b16
+// (bf6::tr_frag), which delivers k rows 4lg..4lg+3 and 16+4lg..+3 of a 32-row block; the pre-split data images
+// YA = y[n][p] and YB = y^T[p][n] store each 32-long k block in that order, so a lane's A fragment is one 16-B load.
+#include "vihmc_internal.h"
+#include "vihmc_bf16x6.h"
+
+namespace vihmc {
+
+namespace {
+using bf6::bf16x4;
+using bf6::bf16x8;
+using bf6::f32x4;
+using bf6::six;
+
+constexpr int GR_PL = CONTRACT_SPLIT_ROWS * bf6::PITCH;   // 7168 B per plane of a block
+constexpr int GR_BLK = 3 * GR_PL;                         // 21504 B of planes per block (the fp32 tail is not used)
+constexpr int GR_PIECES = GR_BLK / 1024;                  // 21 one-KB DMA pieces per block
+static_assert(GR_PIECES * 1024 == GR_BLK, "whole DMA pieces");
+constexpr int GR_NBUF = 3;
+constexpr int GR_LDS = GR_NBUF * GR_BLK;                  // 64.5 KB
+constexpr int GR_CW = 8;                                  // compute waves (32 rows each)
+constexpr int GR_THREADS = 64 * (GR_CW + 1);              // + one DMA wave
+
+// position of k (0..31) inside a 32-long block of the A images: lane group lg holds k = 4lg..4lg+3, 16+4lg..+3
+__host__ __device__ inline int kpos(int k) { return k < 16 ? 8 * (k >> 2) + (k & 3) : 8 * ((k - 16) >> 2) + 4 + (k & 3); }
+
+// the DMA wave of a block ring: block i -> buffer i % 3, copies of block i+2 issued after the barrier of
+// iteration i (every wave is past block i-1 = buffer (i+2) % 3), then wait for block i+1 (21 newer copies may stay
+// in flight) so the next barrier publishes it. SRC(i) gives block i's global address.
+#define GRAM_DMA_PIECES(SRC, BUF)                                                                             \
+    for (int k = 0; k < GR_PIECES; ++k) bf6::glds16_asm((SRC) + k * 1024 + lane * 16, lds + (BUF) * GR_BLK + k * 1024);
+
+template <typename F>
+__device__ __forceinline__ void dma_role(unsigned char* lds, int lane, int nb, F src) {
+    if (nb > 0) { GRAM_DMA_PIECES(src(0), 0) }
+    if (nb > 1) { GRAM_DMA_PIECES(src(1), 1) }
+    if (nb > 1) asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = 0; i < nb; ++i) {
+        __syncthreads();
+        if (i + 2 < nb) {
+            GRAM_DMA_PIECES(src(i + 2), (i + 2) % GR_NBUF)
+            asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+}
+
+__device__ __forceinline__ void load_b(const unsigned char* buf, int tro, int t, bf16x8 (&b)[3]) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) b[pl] = bf6::tr_frag(buf + pl * GR_PL, tro, 16 * t);
+}
+
+// unit of a workgroup with XCD-contiguous unit ranges (workgroup b runs on XCD b % 8): the first `upx` slots of
+// every XCD take units [x upx, (x + 1) upx) of the grouped list, the next `gpx` slots round-robin units of the
+// second list; -1 = idle slot
+__device__ __forceinline__ void unit_of(int b, int upx, int n1, int n2, int& list, int& u) {
+    const int x = b & 7, k = b >> 3;
+    if (k < upx) {
+        list = 0;
+        u = x * upx + k;
+        if (u >= n1) list = -1;
+    } else {
+        list = 1;
+        u = (k - upx) * 8 + x;
+        if (u >= n2) list = -1;
+    }
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
+    const int c = blockIdx.y;
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    const int f = 2 * 100;                                    // byte offset of feature 100 in a plane row
+    if (r < A.N) {
+        unsigned char* row = A.bimg + c * A.bimg_cs + (int64_t)(r / 32) * CONTRACT_SPLIT_BLOCK + (r % 32) * bf6::PITCH;
+        *reinterpret_cast<__bf16*>(row + f) = (__bf16)1.0f;
+        *reinterpret_cast<__bf16*>(row + GR_PL + f) = (__bf16)0.0f;
+        *reinterpret_cast<__bf16*>(row + 2 * GR_PL + f) = (__bf16)0.0f;
+    } else if (r < A.N + A.P) {
+        const int q = r - A.N;
+        const float b0 = A.b0[c * A.b0_cs];
+        const __bf16 a = (__bf16)b0;
+        const float rr = b0 - (float)a;
+        const __bf16 bb = (__bf16)rr;
+        unsigned char* row = A.timg + c * A.timg_cs + (int64_t)(q / 32) * CONTRACT_SPLIT_BLOCK + (q % 32) * bf6::PITCH;
+        *reinterpret_cast<__bf16*>(row + f) = a;
+        *reinterpret_cast<__bf16*>(row + GR_PL + f) = bb;
+        *reinterpret_cast<__bf16*>(row + 2 * GR_PL + f) = (__bf16)(rr - (float)bb);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// k_gram_a: list 0 = T_b units (g = ng * S + s major, chain minor: the 16 chains sharing one YA slab on one XCD),
+// list 1 = Gram units (C * S Gram-t slabs, then C Gram-b).
+//   T_b unit (ng, s, c): rows n0 = 256 ng + 32 w of wave w, trunk blocks [s SL, (s+1) SL): acc[2][7] tiles, stored
+//     tile-major to tb_part[c][s][ng][w][rt][t] (256 floats = 64 lanes x float4 each).
+//   Gram-t (c, s): wave w < 7 computes row tile w (features v = 16w..16w+15) of Zt^T Zt^ over the slab; its A
+//     operand is the B fragment of column tile w. Stored to gt_part[c][s][w][t]; the last slab of chain c to finish
+//     sums the S slabs in order s = 0.. into gt[c] ([112 v][112 w] fp32) and resets the counter.
+//   Gram-b (c): the same over all branch blocks; -Gb written pre-split as 4 blocks (rows v, k of the extension).
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    int list, u;
+    unit_of(blockIdx.x, A.upx_a, A.NG * A.S * A.C, A.C * A.S + A.C, list, u);
+    if (list < 0) return;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    // decode the unit
+    int c, s = 0, ng = 0, kind;          // kind 0 = T_b, 1 = Gram-t, 2 = Gram-b
+    if (list == 0) {
+        const int g = u / A.C;
+        c = u - g * A.C;
+        ng = g / A.S;
+        s = g - ng * A.S;
+        kind = 0;
+    } else if (u < A.C * A.S) {
+        c = u / A.S;
+        s = u - c * A.S;
+        kind = 1;
+    } else {
+        c = u - A.C * A.S;
+        kind = 2;
+    }
+    const unsigned char* src0;
+    int nb, kb0 = 0;
+    if (kind == 2) {
+        src0 = A.bimg + c * A.bimg_cs;
+        nb = A.nblkN;
+    } else {
+        kb0 = s * A.SL;
+        nb = min(A.SL, A.nblkP - kb0);
+        src0 = A.timg + c * A.timg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
+    }
+    const int tro = bf6::tr_lane_off(lr, lg);
+    if (wave == GR_CW) {
+        dma_role(lds, lane, nb, [&](int i) { return src0 + (int64_t)i * CONTRACT_SPLIT_BLOCK; });
+    } else if (kind == 0) {
+        // ---------------- T_b = y Zt^ (A = YA rows, 16-B loads one block ahead in two register sets) ----------
+        const int n0 = 256 * ng + 32 * wave;
+        const __bf16* ya = A.ya + (int64_t)(n0 + lr) * A.ya_ld + (int64_t)kb0 * 32 + 8 * lg;
+        const int64_t rt16 = 16 * (int64_t)A.ya_ld;
+        bf16x8 a0[2][3], a1[2][3];
+        auto load_a = [&](bf16x8 (&a)[2][3], int i) __attribute__((always_inline)) {
+            const int ii = min(i, nb - 1);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    a[rt][pl] = *reinterpret_cast<const bf16x8*>(ya + pl * A.ya_plane + rt * rt16 + 32 * ii);
+        };
+        f32x4 acc[2][7];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
+            __syncthreads();
+            load_a(an, i + 1);
+            __builtin_amdgcn_sched_barrier(0);     // issue the next block's A loads here, a whole block ahead
+            const unsigned char* buf = lds + (i % GR_NBUF) * GR_BLK;
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                bf16x8 b[3];
+                load_b(buf, tro, t, b);
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b, acc[rt][t]);
+            }
+        };
+        load_a(a0, 0);
+        int i = 0;
+        for (; i + 1 < nb; i += 2) {
+            step(i, a0, a1);
+            step(i + 1, a1, a0);
+        }
+        if (i < nb) step(i, a0, a1);
+        float* dst = A.tb_part + c * A.tb_cs + ((int64_t)((s * A.NG + ng) * GR_CW + wave) * 14) * 256 + 4 * lane;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(dst + (rt * 7 + t) * 256) = acc[rt][t];
+    } else {
+    // ---------------- Gram rows: wave w < 7 = row tile w ----------------
+    f32x4 acc[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int w = min(wave, 6);
+    for (int i = 0; i < nb; ++i) {
+        __syncthreads();
+        if (wave < 7) {
+            const unsigned char* buf = lds + (i % GR_NBUF) * GR_BLK;
+            bf16x8 a[3];
+            load_b(buf, tro, w, a);
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                bf16x8 b[3];
+                load_b(buf, tro, t, b);
+                acc[t] = six(a, b, acc[t]);
+            }
+        }
+    }
+    if (kind == 2) {
+        // -Gb pre-split into the extension blocks: element (v, x) -> block v / 32, row v % 32, feature x
+        if (wave < 7) {
+            unsigned char* gb = A.gbimg + c * A.gbimg_cs;
+#pragma unroll
+            for (int t = 0; t < 7; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int v = 16 * w + 4 * lg + r, x = 16 * t + lr;
+                    const float val = -acc[t][r];
+                    const __bf16 p0 = (__bf16)val;
+                    const float rr = val - (float)p0;
+                    const __bf16 p1 = (__bf16)rr;
+                    unsigned char* e = gb + (v / 32) * CONTRACT_SPLIT_BLOCK + (v % 32) * bf6::PITCH + 2 * x;
+                    *reinterpret_cast<__bf16*>(e) = p0;
+                    *reinterpret_cast<__bf16*>(e + GR_PL) = p1;
+                    *reinterpret_cast<__bf16*>(e + 2 * GR_PL) = (__bf16)(rr - (float)p1);
+                }
+        }
+    } else if (wave < 7) {
+        // Gram-t slab s of chain c
+        float* part = A.gt_part + c * A.gt_cs;
+#pragma unroll
+        for (int t = 0; t < 7; ++t)
+            *reinterpret_cast<f32x4*>(part + ((s * 7 + w) * 7 + t) * 256 + 4 * lane) = acc[t];
+    }
+    }
+    if (kind != 1) return;
+    // every wave (the DMA wave too) reaches the barriers below
+    const float* part = A.gt_part + c * A.gt_cs;
+    __shared__ int is_last;
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();
+        is_last = atomicAdd(A.cnt + c, 1u) == (unsigned)(A.S - 1);
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    // fixed-order sum of the S slabs -> gt[c][v][x]
+    float* gt = A.gt + c * A.gt_cs2;
+    for (int e = tid; e < 49 * 256; e += GR_CW * 64) {
+        const int tile = e >> 8, within = e & 255, l = within >> 2, r = within & 3;
+        float sum = 0.f;
+        for (int ss = 0; ss < A.S; ++ss)
+            sum += __hip_atomic_load(part + ss * 49 * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int vt = tile / 7, t = tile - vt * 7;
+        gt[(16 * vt + 4 * (l >> 4) + r) * 112 + 16 * t + (l & 15)] = sum;
+    }
+    if (tid == 0) A.cnt[c] = 0u;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// k_gram_b: unit (pt, c), pt-major (the chains sharing one YB slab on one XCD). Waves own 32 trunk rows
+// p0 = 256 pt + 32 w; k runs over the branch blocks (A = YB rows, 16-B loads) and then 4 extension blocks
+// (A = Zt^ rows from the trunk image, k = feature v; B = -Gb blocks). dZt = -gscale acc (p < P, w < 100);
+// column 100 summed into the d ll / d b0 slot (pt * 8 + w) of the chain.
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    int list, u;
+    unit_of(blockIdx.x, A.upx_b, A.PT * A.C, 0, list, u);
+    if (list < 0) return;
+    const int pt = u / A.C, c = u - pt * A.C;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int nbm = A.nblkN, nb = nbm + 4;
+    if (wave == GR_CW) {
+        const unsigned char* bsrc = A.bimg + c * A.bimg_cs;
+        const unsigned char* gsrc = A.gbimg + c * A.gbimg_cs;
+        dma_role(lds, lane, nb, [&](int i) {
+            return i < nbm ? bsrc + (int64_t)i * CONTRACT_SPLIT_BLOCK : gsrc + (int64_t)(i - nbm) * CONTRACT_SPLIT_BLOCK;
+        });
+        return;
+    }
+    const int tro = bf6::tr_lane_off(lr, lg);
+    const int p0 = 256 * pt + 32 * wave;
+    const __bf16* yb = A.yb + (int64_t)(p0 + lr) * A.yb_ld + 8 * lg;
+    const int64_t rt16 = 16 * (int64_t)A.yb_ld;
+    bf16x8 a0[2][3], a1[2][3];
+    auto load_a = [&](bf16x8 (&a)[2][3], int i) __attribute__((always_inline)) {
+        const int ii = min(i, nbm - 1);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+                a[rt][pl] = *reinterpret_cast<const bf16x8*>(yb + pl * A.yb_plane + rt * rt16 + 32 * ii);
+    };
+    f32x4 acc[2][7];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
+        __syncthreads();
+        load_a(an, i + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned char* buf = lds + (i % GR_NBUF) * GR_BLK;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            bf16x8 b[3];
+            load_b(buf, tro, t, b);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b, acc[rt][t]);
+        }
+    };
+    load_a(a0, 0);
+    int i = 0;
+    for (; i + 1 < nbm; i += 2) {
+        step(i, a0, a1);
+        step(i + 1, a1, a0);
+    }
+    if (i < nbm) step(i, a0, a1);
+    // extension: acc -= Zt^ Gb (B blocks hold -Gb); A lane (lr, lg) = Zt^[p][32e + 4lg + j] (j < 4) and
+    // [32e + 16 + 4lg + j - 4] (j >= 4), two 8-B loads per plane from the trunk image row; rows past P read 0
+    const unsigned char* trow[2];
+    bool pval[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const int p = p0 + 16 * rt + lr;
+        pval[rt] = p < A.P;
+        const int pc = min(p, A.P - 1);
+        trow[rt] = A.timg + c * A.timg_cs + (int64_t)(pc / 32) * CONTRACT_SPLIT_BLOCK + (pc % 32) * bf6::PITCH;
+    }
+    for (int e = 0; e < 4; ++e) {
+        __syncthreads();
+        bf16x8 a[2][3];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const unsigned char* q = trow[rt] + pl * GR_PL + 2 * (32 * e + 4 * lg);
+                bf16x4 lo = *reinterpret_cast<const bf16x4*>(q);
+                bf16x4 hi = e < 3 ? *reinterpret_cast<const bf16x4*>(q + 32) : bf16x4{};
+                if (!pval[rt]) lo = bf16x4{}, hi = bf16x4{};
+                a[rt][pl] = bf6::cat8(lo, hi);
+            }
+        const unsigned char* buf = lds + ((nbm + e) % GR_NBUF) * GR_BLK;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            bf16x8 b[3];
+            load_b(buf, tro, t, b);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b, acc[rt][t]);
+        }
+    }
+    // dZt = -gscale acc
+    const float sc = -A.gscale;
+    float* out = A.dzt + c * A.dzt_cs;
+    float db = 0.f;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int x = 16 * t + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int p = p0 + 16 * rt + 4 * lg + r;
+                const float v = sc * acc[rt][t][r];
+                if (x < 100 && p < A.P) out[(int64_t)p * A.ldz + x] = v;
+                if (t == 6 && lr == 4) db += v;     // x == 100: sum_n G[n][p] (rows past P are 0)
+            }
+        }
+    // lanes 4, 20, 36, 52 hold the wave's column-100 sums
+    db += __shfl_xor(db, 16, 64);
+    db += __shfl_xor(db, 32, 64);
+    if (lane == 4) {
+        double* st = A.stats + c * A.stats_cs + 2 * (int64_t)(pt * GR_CW + wave);
+        st[0] = 0.0;
+        st[1] = (double)db;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// k_gram_c: unit (c, 32-row group m): dZb[n][x] = gscale (sum_{v <= 100} Zb^[n][v] Gt[v][x] - sum_s T_b[s][n][x]).
+// 256 threads; wave wv handles the group's accumulator tiles (rt, t) = wv, wv + 4, ... of 14, lane layout of the
+// T_b slabs (rows 4lg + r, column lr). Gt (101 x 112) and Zb^T (101 x 32) staged in LDS.
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gram_c(GramArgs A) {
+    __shared__ __attribute__((aligned(16))) float gts[101 * 112];
+    __shared__ __attribute__((aligned(16))) float zbt[101 * 32];
+    const int ngroups = (A.N + 31) / 32;
+    const int c = blockIdx.x / ngroups, m = blockIdx.x - c * ngroups;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const float* gt = A.gt + c * A.gt_cs2;
+    for (int e = tid; e < 101 * 28; e += 256) {
+        const int v = e / 28, q = e - v * 28;
+        *reinterpret_cast<f32x4*>(gts + v * 112 + 4 * q) = *reinterpret_cast<const f32x4*>(gt + v * 112 + 4 * q);
+    }
+    const float* zb = A.zb + c * A.zb_cs;
+    for (int e = tid; e < 32 * 101; e += 256) {
+        const int row = e / 101, v = e - row * 101, n = 32 * m + row;
+        float z = 0.f;
+        if (n < A.N) z = v < 100 ? zb[(int64_t)n * A.ldz + v] : 1.f;
+        zbt[v * 32 + row] = z;
+    }
+    __syncthreads();
+    const int n32 = 32 * m, ng = n32 / 256, w8 = (n32 % 256) / 32;
+    const float* tb = A.tb_part + c * A.tb_cs + ((int64_t)(ng * GR_CW + w8) * 14) * 256 + 4 * lane;
+    const int64_t sstride = (int64_t)A.NG * GR_CW * 14 * 256;
+    float* out = A.dzb + c * A.dzb_cs;
+    for (int tile = wv; tile < 14; tile += 4) {
+        const int rt = tile / 7, t = tile - rt * 7;
+        f32x4 ts = {0.f, 0.f, 0.f, 0.f};
+        for (int ss = 0; ss < A.S; ++ss) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(tb + ss * sstride + tile * 256);
+            ts += v;
+        }
+        f32x4 gz = {0.f, 0.f, 0.f, 0.f};
+        const int x = 16 * t + lr;
+        for (int v = 0; v < 101; ++v) {
+            const f32x4 z = *reinterpret_cast<const f32x4*>(zbt + v * 32 + 16 * rt + 4 * lg);
+            const float g = gts[v * 112 + x];
+            gz += z * g;
+        }
+        if (x < 100) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n32 + 16 * rt + 4 * lg + r;
+                if (n < A.N) out[(int64_t)n * A.ldz + x] = A.gscale * (gz[r] - ts[r]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Pre-split data images (once per plan / data change): YA = y [n][p] (k = p blocks in kpos order), YB = y^T [p][n]
+// (k = n blocks). Padding rows / columns stay zero (the plan zeroes the allocation).
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld,
+                                                   __bf16* yb, int64_t yb_plane, int yb_ld) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (int64_t)N * P) return;
+    const int n = (int)(e / P), p = (int)(e - (int64_t)n * P);
+    const float x = y[e];
+    const __bf16 a = (__bf16)x;
+    const float r = x - (float)a;
+    const __bf16 b = (__bf16)r;
+    const __bf16 cc = (__bf16)(r - (float)b);
+    const int64_t ia = (int64_t)n * ya_ld + 32 * (p / 32) + kpos(p % 32);
+    ya[ia] = a;
+    ya[ia + ya_plane] = b;
+    ya[ia + 2 * ya_plane] = cc;
+    const int64_t ib = (int64_t)p * yb_ld + 32 * (n / 32) + kpos(n % 32);
+    yb[ib] = a;
+    yb[ib + yb_plane] = b;
+    yb[ib + 2 * yb_plane] = cc;
+}
+
+hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld, __bf16* yb,
+                            int64_t yb_plane, int yb_ld, hipStream_t s) {
+    const int64_t n = (int64_t)N * P;
+    hipLaunchKernelGGL(k_gram_yimg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, y, N, P, ya, ya_plane, ya_ld, yb,
+                       yb_plane, yb_ld);
+    return hipGetLastError();
+}
+
+int gram_lds_bytes() { return GR_LDS; }
+
+hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
+    GramArgs a = a0;
+    if (a.ya_ld % 8 || a.yb_ld % 8 || a.NG * 256 < a.N || a.PT * 256 < a.P || a.nblkN * 32 < a.N ||
+        a.nblkP * 32 < a.P || a.S * a.SL < a.nblkP || a.C < 1)
+        return hipErrorInvalidValue;
+    const int n1 = a.NG * a.S * a.C, n2 = a.C * a.S + a.C;
+    a.upx_a = (n1 + 7) / 8;
+    const int gpx = (n2 + 7) / 8;
+    a.upx_b = (a.PT * a.C + 7) / 8;
+    hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gram_a, dim3(8 * (a.upx_a + gpx)), dim3(GR_THREADS), GR_LDS, s, a);
+    hipLaunchKernelGGL(k_gram_b, dim3(8 * a.upx_b), dim3(GR_THREADS), GR_LDS, s, a);
+    hipLaunchKernelGGL(k_gram_c, dim3(a.C * ((a.N + 31) / 32)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace vihmc

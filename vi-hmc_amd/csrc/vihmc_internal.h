@@ -134,6 +134,34 @@ struct ContractProb {
     float gscale;
 };
 
+// ---------------------------------------------------------------------------------------------
+// Gradient-only contraction in Gram form (vihmc_gram.hip): dZ_b and dZ_t from y Zt^, y^T Zb^ and the two
+// 101 x 101 Gram matrices of the augmented outputs Zb^ = [Z_b | 1], Zt^ = [Z_t | b0]; no residual, no G^T.
+// ---------------------------------------------------------------------------------------------
+struct GramArgs {
+    unsigned char* bimg; int64_t bimg_cs; int32_t nblkN;   // branch outputs, pre-split blocks (qsplitA)
+    unsigned char* timg; int64_t timg_cs; int32_t nblkP;   // trunk outputs, pre-split blocks (qsplitB)
+    const __bf16* ya; int64_t ya_plane; int32_t ya_ld;     // y [NG*256 rows n][32 nblkP], 3 planes, kpos order
+    const __bf16* yb; int64_t yb_plane; int32_t yb_ld;     // y^T [PT*256 rows p][32 nblkN], 3 planes
+    float* tb_part; int64_t tb_cs;                         // [C][S][NG][8 waves][14 tiles][256]
+    float* gt_part; int64_t gt_cs;                         // [C][S][49 tiles][256]
+    float* gt; int64_t gt_cs2;                             // [C][112][112] Zt^T Zt^
+    unsigned char* gbimg; int64_t gbimg_cs;                // [C][4 blocks] -Zb^T Zb^ pre-split
+    uint32_t* cnt;                                         // [C] Gram-t slab counters (self-resetting)
+    const float* zb; int64_t zb_cs;                        // fp32 Z_b rows [N][ldz]
+    float* dzb; int64_t dzb_cs;                            // dZ_b [N][ldz]
+    float* dzt; int64_t dzt_cs;                            // dZ_t [P][ldz]
+    double* stats; int64_t stats_cs;                       // (0, sum G) pairs, PT * 8 per chain
+    const float* b0; int64_t b0_cs;
+    int32_t N, P, ldz, NG, S, SL, PT, C;
+    int32_t upx_a, upx_b;                                  // set by launch_gram
+    float gscale;
+};
+hipError_t launch_gram(const GramArgs& a, hipStream_t s);
+hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld, __bf16* yb,
+                            int64_t yb_plane, int yb_ld, hipStream_t s);
+int gram_lds_bytes();
+
 // launchers (vihmc_kernels.hip)
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s);
 // The grouped input-layer launch (branch K = 101 on the whole-tile KF = 104 path, trunk run-time K) applies:

@@ -150,6 +150,24 @@ struct vihmc_plan {
     int fuse_scatter = 1;       // plan option: trajectory evaluations take theta already scattered by the leapfrog
     int mlp_fast = 1;             // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
     int bwd_chain = 1;            // plan option: whole-network backward in one launch when the chunks are 64 rows
+    // Gram-form gradient-only contraction (vihmc_gram.hip) for the evaluations that return no log-prob (the
+    // trajectory's inner leapfrog steps, vihmc_grad): plan options "gram" (on / off) and "gram_min_chains"
+    int gram = 1, gram_min_chains = 2;
+    bool gram_alloc = false;      // W = 100 plan: images and work buffers allocated
+    __bf16* gya = nullptr;        // y [NG*256][32 nblkP], 3 planes (kpos order inside each 32-long p block)
+    __bf16* gyb = nullptr;        // y^T [PT*256][32 nblkN], 3 planes
+    int64_t gya_plane = 0, gyb_plane = 0;
+    int gya_ld = 0, gyb_ld = 0, gNG = 0, gS = 0, gSL = 0, gPT = 0;
+    float* gtb_part = nullptr;
+    int64_t gtb_cs = 0;
+    float* ggt_part = nullptr;
+    int64_t ggt_part_cs = 0;
+    float* ggt = nullptr;
+    unsigned char* ggb = nullptr;
+    uint32_t* gcnt = nullptr;
+    double* gstats = nullptr;
+    int64_t gstats_cs = 0;
+    bool last_gram = false;       // the last gradient evaluation ran the Gram form (get_option gram: bit 1)
     bool timg_live = false;       // the W^T images hold this evaluation's theta (scatter-kept or split this evaluation)
     bool last_bwd_chain = false;  // the last gradient evaluation ran k_bwd_chain (get_option bwd_chain: bit 1)
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
@@ -308,6 +326,93 @@ ScatterImg scatter_img(const vihmc_plan* p) {
                       p->wtimg, p->wtimg_cs, p->smap_timg, p->smap_timgf, BWD_WTPLANE};
 }
 
+// Gram-form buffers (W = 100 plans): the pre-split data images (built from p->y by gram_images, again whenever the
+// data changes) and the per-chain work buffers of vihmc_gram.hip. Split-K of the y Zt^ product: S slabs of SL trunk
+// blocks (8 at 16 chains: 512 T_b workgroups of 40 blocks).
+int gram_setup(vihmc_plan* p, int C) {
+    const int nblkN = cdiv(p->N, CONTRACT_SPLIT_ROWS), nblkP = cdiv(p->P, CONTRACT_SPLIT_ROWS);
+    p->gNG = cdiv(p->N, 256);
+    p->gPT = cdiv(p->P, 256);
+    p->gS = 8;
+    p->gSL = cdiv(nblkP, p->gS);
+    p->gS = cdiv(nblkP, p->gSL);
+    p->gya_ld = 32 * nblkP;
+    p->gyb_ld = 32 * nblkN;
+    p->gya_plane = (int64_t)p->gNG * 256 * p->gya_ld;
+    p->gyb_plane = (int64_t)p->gPT * 256 * p->gyb_ld;
+    if (int rc = p->alloc(&p->gya, 3 * p->gya_plane)) return rc;
+    if (int rc = p->alloc(&p->gyb, 3 * p->gyb_plane)) return rc;
+    p->gtb_cs = (int64_t)p->gS * p->gNG * 8 * 14 * 256;
+    if (int rc = p->alloc(&p->gtb_part, p->gtb_cs * C)) return rc;
+    p->ggt_part_cs = (int64_t)p->gS * 49 * 256;
+    if (int rc = p->alloc(&p->ggt_part, p->ggt_part_cs * C)) return rc;
+    if (int rc = p->alloc(&p->ggt, (int64_t)112 * 112 * C)) return rc;
+    if (int rc = p->alloc(&p->ggb, (int64_t)4 * CONTRACT_SPLIT_BLOCK * C)) return rc;
+    if (int rc = p->alloc(&p->gcnt, C)) return rc;
+    p->gstats_cs = 2 * (int64_t)p->gPT * 8;
+    if (int rc = p->alloc(&p->gstats, p->gstats_cs * C)) return rc;
+    p->gram_alloc = true;
+    return 0;
+}
+
+int gram_images(vihmc_plan* p, hipStream_t s) {
+    if (!p->gram_alloc) return 0;
+    HIPCHK(launch_gram_yimg(p->y, p->N, p->P, p->gya, p->gya_plane, p->gya_ld, p->gyb, p->gyb_plane, p->gyb_ld, s));
+    return 0;
+}
+
+bool gram_on(const vihmc_plan* p, int C) {
+    return p->gram && p->gram_alloc && p->W == 100 && p->contract_bf16x6 && C >= p->gram_min_chains;
+}
+
+GramArgs gram_args(vihmc_plan* p, int C) {
+    GramArgs a{};
+    a.bimg = p->qsplitA;
+    a.bimg_cs = p->qsplitA_cs;
+    a.nblkN = cdiv(p->N, CONTRACT_SPLIT_ROWS);
+    a.timg = p->qsplitB;
+    a.timg_cs = p->qsplitB_cs;
+    a.nblkP = cdiv(p->P, CONTRACT_SPLIT_ROWS);
+    a.ya = p->gya;
+    a.ya_plane = p->gya_plane;
+    a.ya_ld = p->gya_ld;
+    a.yb = p->gyb;
+    a.yb_plane = p->gyb_plane;
+    a.yb_ld = p->gyb_ld;
+    a.tb_part = p->gtb_part;
+    a.tb_cs = p->gtb_cs;
+    a.gt_part = p->ggt_part;
+    a.gt_cs = p->ggt_part_cs;
+    a.gt = p->ggt;
+    a.gt_cs2 = 112 * 112;
+    a.gbimg = p->ggb;
+    a.gbimg_cs = 4 * CONTRACT_SPLIT_BLOCK;
+    a.cnt = p->gcnt;
+    const Net& b = p->nets[0];
+    const Net& t = p->nets[1];
+    a.zb = b.act + b.h_off.back();
+    a.zb_cs = b.act_cs;
+    a.dzb = b.delta[0];
+    a.dzb_cs = b.delta_cs;
+    a.dzt = t.delta[0];
+    a.dzt_cs = t.delta_cs;
+    a.stats = p->gstats;
+    a.stats_cs = p->gstats_cs;
+    a.b0 = p->packed;
+    a.b0_cs = p->dp;
+    a.N = p->N;
+    a.P = p->P;
+    a.ldz = p->ldz;
+    a.NG = p->gNG;
+    a.S = p->gS;
+    a.SL = p->gSL;
+    a.PT = p->gPT;
+    a.C = C;
+    const float v = std::max(p->lik.tau_out, 1e-6f);
+    a.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
+    return a;
+}
+
 int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb, const float* tf, const float* y,
                    const float* frozen, const int64_t* idx, const float* prior_mu, const float* prior_sd) {
     if (d->n_branch_layers < 1 || d->n_trunk_layers < 1) return fail("empty branch or trunk");
@@ -436,6 +541,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         if (int rc = p->alloc(&p->qsplitA, p->qsplitA_cs * C)) return rc;
         p->qsplitB_cs = (int64_t)cdiv(p->P, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
         if (int rc = p->alloc(&p->qsplitB, p->qsplitB_cs * C)) return rc;
+        if (int rc = gram_setup(p, C)) return rc;
     }
 
     // ---- per-chain work buffers ---------------------------------------------------------------------
@@ -616,6 +722,8 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     // weight images maintained by the scatter (after the activation layout, which fused_args reads)
     if (p->wimg)
         if (int rc = image_maps(p, d, idx)) return rc;
+    if (int rc = gram_images(p, nullptr)) return rc;
+    HIPCHK(hipDeviceSynchronize());
     return 0;
 }
 
@@ -885,8 +993,23 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     p->img_by_fwd = false;
     p->timg_live = p->img_by_scatter && p->wtimg;      // the scatter above kept the W^T images current
     if (int rc = deeponet_forward_layers(p, C, s, want_grad && p->contract_bf16x6 && p->W == 100)) return rc;
+    // gradient-only evaluations (no log-prob returned): the Gram-form contraction, which forms no residual
+    const bool gram = want_grad && logp == nullptr && gram_on(p, C);
+    p->last_gram = gram;
     int stats_waves = 0;
-    {
+    if (gram) {
+        Net& b = p->nets[0];
+        Net& t = p->nets[1];
+        if (!p->img_by_fwd) {
+            HIPCHK(launch_split_blocks(b.act + b.h_off.back(), b.act_cs, p->ldz, p->N, p->qsplitA, p->qsplitA_cs, C, s));
+            HIPCHK(launch_split_blocks(t.act + t.h_off.back(), t.act_cs, p->ldz, p->P, p->qsplitB, p->qsplitB_cs, C, s));
+        }
+        hipEvent_t stop = nullptr;
+        if (int rc = p->timing_begin(VIHMC_T_GRAM, s, &stop)) return rc;
+        HIPCHK(launch_gram(gram_args(p, C), s));
+        if (stop) HIPCHK(hipEventRecord(stop, s));
+        stats_waves = p->gPT * 8;
+    } else {
         ContractProb a = side_a(p, C, want_grad, out);
         stats_waves = p->qchunksA * cdiv(p->P, CONTRACT_OWN_PER_WG) * (a.bf16x6 ? 8 : 4);
         if (a.bf16x6 && !p->img_by_fwd)
@@ -898,14 +1021,15 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     }
     // gradient evaluations: the statistics run as a slice of the weight-gradient reduce (nothing reads lik or
     // gp slot 0 before the gather)
-    const StatsJob stats_job{p->stats, p->stats_cs, stats_waves, p->lik_buf, p->gp, p->dp,
-                             (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out};
+    const StatsJob stats_job{gram ? p->gstats : p->stats, gram ? p->gstats_cs : p->stats_cs, stats_waves, p->lik_buf,
+                             p->gp, p->dp, (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out};
     if (!want_grad)
         HIPCHK(launch_contract_stats(p->stats, p->stats_cs, stats_waves, C, p->lik_buf, p->gp, p->dp,
                                      (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out, s));
     if (want_grad) {
         Net& b = p->nets[0];
         Net& t = p->nets[1];
+        if (!gram) {
         ContractProb q{};
         q.Own = b.act + b.h_off.back();
         q.own_cs = b.act_cs;
@@ -945,6 +1069,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         if (stop) HIPCHK(hipEventRecord(stop, s));
         if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 2, std::max(p->lenA, p->lenB), C, s));
         else HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s));
+        }
 
         // backward through both MLPs, last layer first: one fused launch per layer (branch + trunk
         // grouped) computes delta_{l-1} and the dW / db partial slabs
@@ -1221,6 +1346,18 @@ int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float
     });
 }
 
+int vihmc_grad(vihmc_plan* p, const float* theta, int C, float* grad, void* stream) {
+    return guarded([&]() -> int {
+        if (!p || !theta || !grad) return fail("null argument");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        if (p->kind == 0) return deeponet_eval(p, theta, C, nullptr, grad, nullptr, s);
+        if (!p->lik_buf)                                  // BNN plans: the value lands in a plan-owned scratch
+            if (int rc = p->alloc(&p->lik_buf, p->maxC)) return rc;
+        if (int rc = mlp_eval(p, theta, C, p->lik_buf, grad, nullptr, s)) return rc;
+        return 0;
+    });
+}
+
 int vihmc_mlp_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, const float* p_in, float* p_out,
                          const float* g_in, float* g_out, float* logp_out, const float* eps, const float* inv_mass,
                          int L, int C, void* stream) {
@@ -1432,7 +1569,7 @@ int vihmc_plan_set_data(vihmc_plan* p, const float* x_branch, const float* y, vo
         HIPCHK(hipMemcpy2DAsync(b.input, (size_t)b.ld_in * sizeof(float), x_branch, in_b, in_b, (size_t)b.rows,
                                 hipMemcpyDeviceToDevice, s));
         HIPCHK(hipMemcpyAsync(p->y, y, (size_t)p->N * p->P * sizeof(float), hipMemcpyDeviceToDevice, s));
-        return 0;
+        return gram_images(p, s);
     });
 }
 
@@ -1445,7 +1582,7 @@ int vihmc_plan_set_trunk_rows(vihmc_plan* p, const float* trunk_all, const float
         Net& t = p->nets[1];
         HIPCHK(launch_gather_trunk(trunk_all, t.L[0].n_in, y_all, P_all, ind, p->P, p->N, t.input, t.ld_in, p->y,
                                    static_cast<hipStream_t>(stream)));
-        return 0;
+        return gram_images(p, static_cast<hipStream_t>(stream));
     });
 }
 
@@ -1499,7 +1636,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1513,6 +1650,8 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "img_scatter") p->img_by_scatter = value && p->smap_img;   // 0: split the images per evaluation
     else if (k == "mlp_fast") p->mlp_fast = value ? 1 : 0;
     else if (k == "bwd_chain") p->bwd_chain = value ? 1 : 0;
+    else if (k == "gram") p->gram = value ? 1 : 0;
+    else if (k == "gram_min_chains") p->gram_min_chains = std::max(1, value);
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     // captured graphs embed the kernel choice
     for (auto& g : p->graphs) (void)hipGraphExecDestroy(g.second);
@@ -1532,6 +1671,8 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "img_scatter") *value = p->img_by_scatter ? 1 : 0;
     else if (k == "mlp_fast") *value = p->mlp_fast && p->kind == 1 && mlp_bnn_fast_ok(p->mlp);
     else if (k == "bwd_chain") *value = p->bwd_chain | (p->last_bwd_chain ? 2 : 0);
+    else if (k == "gram") *value = (p->gram && p->gram_alloc ? 1 : 0) | (p->last_gram ? 2 : 0);
+    else if (k == "gram_min_chains") *value = p->gram_min_chains;
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
 }

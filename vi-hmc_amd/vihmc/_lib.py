@@ -52,6 +52,7 @@ SIGNATURES = {
     "vihmc_mlp_plan_create": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(MLPDesc), P_float, P_float, P_float,
                                       P_int64, P_float, P_float, c_int]),
     "vihmc_logp_grad": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+    "vihmc_grad": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "vihmc_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_mlp_trajectory": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_int, c_int, c_void_p]),

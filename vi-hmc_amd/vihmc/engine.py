@@ -99,6 +99,20 @@ class _Engine:
         _lib.check(rc, "vihmc_logp_grad")
         return logp, grad
 
+    def grad(self, theta: torch.Tensor, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """theta [C, K] -> grad [C, K] only (vihmc_grad: the leapfrog's inner evaluations; DeepONet plans run the
+        Gram-form contraction there)."""
+        th = self._theta(theta)
+        if self._sample_rng is not None:
+            self._redraw()
+        C = th.shape[0]
+        if grad is None:
+            grad = torch.empty(C, self.K, device=self.device, dtype=torch.float32)
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_grad(self._plan, th.data_ptr(), C, grad.data_ptr(), self._stream())
+        _lib.check(rc, "vihmc_grad")
+        return grad
+
     def logp(self, theta: torch.Tensor, logp: Optional[torch.Tensor] = None) -> torch.Tensor:
         th = self._theta(theta)
         if self._sample_rng is not None:
@@ -236,7 +250,7 @@ class _Engine:
 
     # ---- kernel timing hook (roofline) -----------------------------------------------------------
     # classes of include/vihmc.h VIHMC_T_*
-    T_CONTRACT_A, T_CONTRACT_B, T_BWD, T_FWD, T_EVAL, T_MLP = range(6)
+    T_CONTRACT_A, T_CONTRACT_B, T_BWD, T_FWD, T_EVAL, T_MLP, T_GRAM = range(7)
     T_ALL = -1
 
     def timing(self, which: int = 0, on: bool = True):

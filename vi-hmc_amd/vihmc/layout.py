@@ -114,6 +114,13 @@ class DeepONetSpec:
         d["contract_b"] = c
         return d
 
+    def flops_gram(self, n: int, p: int) -> float:
+        """Algorithmic FLOP per chain of the Gram-form gradient-only contraction (vihmc_gram.hip, the inner
+        leapfrog evaluations), which replaces side A + side B there: y Zt^ and y^T Zb^ (2 N P (W+1) each) and the
+        (N + P) (W+1)^2 Gram / correction products (Zt^T Zt^, Zb^T Zb^, Zt^ Gb, Zb^ Gt), augmented width W + 1."""
+        wa = self.out + 1
+        return 4.0 * n * p * wa + 4.0 * (n + p) * wa * wa
+
 
 @dataclass(frozen=True)
 class MLPSpec:

@@ -72,6 +72,13 @@ class EngineEvaluator:
         self.n_value += theta.shape[0]
         return self.engine.logp(theta)
 
+    def grad(self, theta):
+        """gradient only (the leapfrog's inner steps, whose log-prob hamiltorch discards): vihmc_grad"""
+        self.n_grad += theta.shape[0]
+        if hasattr(self.engine, "grad"):
+            return self.engine.grad(theta)
+        return self.engine.logp_grad(theta)[1]
+
     @property
     def fused_trajectory(self) -> bool:
         """Engines run a whole leapfrog trajectory per call (_Engine.trajectory / vihmc_trajectory: one launch for
@@ -103,6 +110,9 @@ class AutogradEvaluator:
             gs.append(g)
         self.n_grad += theta.shape[0]
         return torch.stack(lps).to(torch.float32), torch.stack(gs).to(torch.float32)
+
+    def grad(self, theta):
+        return self.logp_grad(theta)[1]
 
     def logp(self, theta):
         with torch.no_grad():
@@ -300,9 +310,12 @@ class HMCRunner:
             g_open = g if self.reuse else evs[0].logp_grad(th)[1]
             p = p + (0.5 * eps) * g_open
             lp_new = g_new = None
-            for _ in range(L):
+            for step in range(L):
                 th = th + eps * p if inv_mass is None else th + eps * inv_mass * p
-                lp_new, g_new = evs[0].logp_grad(th)
+                if step == L - 1:
+                    lp_new, g_new = evs[0].logp_grad(th)
+                else:
+                    g_new = evs[0].grad(th)
                 p = p + eps * g_new
             p = p - (0.5 * eps) * g_new
             return th, p, lp_new, g_new
@@ -312,18 +325,21 @@ class HMCRunner:
         # one fused kernel per update (torch.add with alpha; eps is a host float here) instead of a scale and
         # an add: config 4's per-step updates between the engine evaluations are launch-bound
         half = 0.5 * eps
-        for _ in range(L):
+        for step in range(L):
             for m in range(M):
                 if m == 0 and g0_cached is not None:
                     gm = g0_cached
                 else:
-                    _, gm = evs[m].logp_grad(th)
+                    gm = evs[m].grad(th)
                 p = torch.add(p, gm, alpha=half) if not torch.is_tensor(eps) else p + half * gm
                 if m < M - 1:
                     th = torch.add(th, p, alpha=sub) if not torch.is_tensor(eps) else th + sub * p
             for m in reversed(range(M)):
                 if not (m == M - 1 and self.reuse):      # same theta as the forward pass' last shard
-                    lp0_end, gm = evs[m].logp_grad(th)
+                    if step == L - 1 and m == 0:         # only the end point's log-prob is used
+                        lp0_end, gm = evs[m].logp_grad(th)
+                    else:
+                        gm = evs[m].grad(th)
                 p = torch.add(p, gm, alpha=half) if not torch.is_tensor(eps) else p + half * gm
                 if m > 0:
                     th = torch.add(th, p, alpha=sub) if not torch.is_tensor(eps) else th + sub * p
