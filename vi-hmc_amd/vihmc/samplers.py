@@ -222,6 +222,13 @@ class ChainResult:
         return self.samples[:, :n]
 
 
+def _grad(ev, theta):
+    """gradient-only evaluation of an inner leapfrog step (hamiltorch discards its log-prob); evaluators without
+    ``grad`` (any object with the logp_grad / logp contract) fall back to logp_grad"""
+    f = getattr(ev, "grad", None)
+    return f(theta) if f is not None else ev.logp_grad(theta)[1]
+
+
 def _kinetic(p, inv_mass):
     return 0.5 * (p * p).sum(1) if inv_mass is None else 0.5 * (p * (inv_mass * p)).sum(1)
 
@@ -315,7 +322,7 @@ class HMCRunner:
                 if step == L - 1:
                     lp_new, g_new = evs[0].logp_grad(th)
                 else:
-                    g_new = evs[0].grad(th)
+                    g_new = _grad(evs[0], th)
                 p = p + eps * g_new
             p = p - (0.5 * eps) * g_new
             return th, p, lp_new, g_new
@@ -330,7 +337,7 @@ class HMCRunner:
                 if m == 0 and g0_cached is not None:
                     gm = g0_cached
                 else:
-                    gm = evs[m].grad(th)
+                    gm = _grad(evs[m], th)
                 p = torch.add(p, gm, alpha=half) if not torch.is_tensor(eps) else p + half * gm
                 if m < M - 1:
                     th = torch.add(th, p, alpha=sub) if not torch.is_tensor(eps) else th + sub * p
@@ -339,7 +346,7 @@ class HMCRunner:
                     if step == L - 1 and m == 0:         # only the end point's log-prob is used
                         lp0_end, gm = evs[m].logp_grad(th)
                     else:
-                        gm = evs[m].grad(th)
+                        gm = _grad(evs[m], th)
                 p = torch.add(p, gm, alpha=half) if not torch.is_tensor(eps) else p + half * gm
                 if m > 0:
                     th = torch.add(th, p, alpha=sub) if not torch.is_tensor(eps) else th + sub * p
