@@ -188,7 +188,7 @@ enum {
     VIHMC_T_FWD = 3,          /* fused hidden-layer forward (k_fwd_fused_bf / k_fwd_fused) */
     VIHMC_T_EVAL = 4,         /* one whole DeepONet evaluation, first to last launch */
     VIHMC_T_MLP = 5,          /* BNN evaluation (k_mlp) */
-    VIHMC_T_GRAM = 6,         /* Gram-form gradient-only contraction (k_gram_aug, k_gram_a, k_gram_b, k_gram_c): one
+    VIHMC_T_GRAM = 6,         /* Gram-form gradient-only contraction (k_gram_aug, k_gram_a, k_gram_b): one
                                  event pair brackets the four launches */
     VIHMC_T_COUNT = 7
 };

@@ -624,9 +624,17 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
             *reinterpret_cast<__bf16*>(o) = y0;
             *reinterpret_cast<__bf16*>(o + QI_HALF) = y1;
             *reinterpret_cast<__bf16*>(o + 2 * QI_HALF) = y2;
-            if (lg < 3) {                                  // zero columns 100..111 of plane lg (8-B aligned)
+            if (lg < 3) {                                  // columns 100..111 of plane lg (8-B aligned): zero, but
                 uint64_t* z = reinterpret_cast<uint64_t*>(reg + lg * QI_HALF + lr * QI_PITCH + 200);
-                z[0] = 0;
+                uint64_t f100 = 0;                         // column 100 = plane lg of the augmentation value
+                if (N.aug) {
+                    const float av = N.aug == 1 ? 1.f : args.packed[c * args.dp];
+                    __bf16 a0, a1, a2;
+                    split3(av, a0, a1, a2);
+                    const __bf16 al = lg == 0 ? a0 : (lg == 1 ? a1 : a2);
+                    f100 = (uint64_t)__builtin_bit_cast(uint16_t, al);
+                }
+                z[0] = f100;
                 z[1] = 0;
                 z[2] = 0;
             }

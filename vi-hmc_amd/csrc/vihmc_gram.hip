@@ -21,7 +21,7 @@
 //                slab of a chain sums them in fixed order), Gb = Zb^T Zb^ (written negated, pre-split, as the
 //                B blocks of k_gram_b's extension)
 //   k_gram_b     dZt = -gscale (y^T Zb^ - Zt^ Gb) over the branch image + 4 extension blocks; d ll / d b0 slots
-//   k_gram_c     dZb = gscale (Zb^ Gt - sum_s T_b slab s)
+//   (k_gram_b)   dZb = gscale (Zb^ Gt - sum_s T_b slab s): epilogue units after the T_t units of k_gram_b
 // Images: the contraction's pre-split blocks (k_split_blocks' layout, written by the fused forward): block =
 // 3 planes [32 rows][112 features] bf16, 224-B rows. The B operand (rows = k) is read with ds_read_b64_tr_b16
 // (bf6::tr_frag), which delivers k rows 4lg..4lg+3 and 16+4lg..+3 of a 32-row block; the pre-split data images
@@ -43,6 +43,7 @@ constexpr int GR_PIECES = GR_BLK / 1024;                  // 21 one-KB DMA piece
 static_assert(GR_PIECES * 1024 == GR_BLK, "whole DMA pieces");
 constexpr int GR_NBUF = 3;
 constexpr int GR_LDS = GR_NBUF * GR_BLK;                  // 64.5 KB
+static_assert((101 * 112 + 101 * 32) * 4 <= GR_LDS, "dZb epilogue staging fits the ring");
 constexpr int GR_CW = 8;                                  // compute waves (32 rows each)
 constexpr int GR_THREADS = 64 * (GR_CW + 1);              // + one DMA wave
 
@@ -75,6 +76,20 @@ __device__ __forceinline__ void dma_role(unsigned char* lds, int lane, int nb, F
 __device__ __forceinline__ void load_b(const unsigned char* buf, int tro, int t, bf16x8 (&b)[3]) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) b[pl] = bf6::tr_frag(buf + pl * GR_PL, tro, 16 * t);
+}
+
+// one 32-long k block of a wave's 32 x 112 tile: B fragments of column tile t+1 read while tile t's 12 MFMAs run
+// (double-buffered fragments, so the wait before tile t's products leaves the next tile's reads in flight)
+__device__ __forceinline__ void mma_block(const unsigned char* buf, int tro, const bf16x8 (&a)[2][3],
+                                          f32x4 (&acc)[2][7]) {
+    bf16x8 b[2][3];
+    load_b(buf, tro, 0, b[0]);
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        if (t < 6) load_b(buf, tro, t + 1, b[(t + 1) & 1]);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b[t & 1], acc[rt][t]);
+    }
 }
 
 // unit of a workgroup with XCD-contiguous unit ranges (workgroup b runs on XCD b % 8): the first `upx` slots of
@@ -185,14 +200,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
             __syncthreads();
             load_a(an, i + 1);
             __builtin_amdgcn_sched_barrier(0);     // issue the next block's A loads here, a whole block ahead
-            const unsigned char* buf = lds + (i % GR_NBUF) * GR_BLK;
-#pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                bf16x8 b[3];
-                load_b(buf, tro, t, b);
-#pragma unroll
-                for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b, acc[rt][t]);
-            }
+            mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc);
         };
         load_a(a0, 0);
         int i = 0;
@@ -284,11 +292,17 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
 // (A = Zt^ rows from the trunk image, k = feature v; B = -Gb blocks). dZt = -gscale acc (p < P, w < 100);
 // column 100 summed into the d ll / d b0 slot (pt * 8 + w) of the chain.
 // ---------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char* lds);
+
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     int list, u;
-    unit_of(blockIdx.x, A.upx_b, A.PT * A.C, 0, list, u);
+    unit_of(blockIdx.x, A.upx_b, A.PT * A.C, A.C * ((A.N + 31) / 32), list, u);
     if (list < 0) return;
+    if (list == 1) {                   // the dZb epilogue units fill the tail of the T_t rounds (k_gram_a is done)
+        dzb_unit(A, u, lds);
+        return;
+    }
     const int pt = u / A.C, c = u - pt * A.C;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int nbm = A.nblkN, nb = nbm + 4;
@@ -322,14 +336,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
         __syncthreads();
         load_a(an, i + 1);
         __builtin_amdgcn_sched_barrier(0);
-        const unsigned char* buf = lds + (i % GR_NBUF) * GR_BLK;
-#pragma unroll
-        for (int t = 0; t < 7; ++t) {
-            bf16x8 b[3];
-            load_b(buf, tro, t, b);
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b, acc[rt][t]);
-        }
+        mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc);
     };
     load_a(a0, 0);
     int i = 0;
@@ -362,14 +369,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
                 if (!pval[rt]) lo = bf16x4{}, hi = bf16x4{};
                 a[rt][pl] = bf6::cat8(lo, hi);
             }
-        const unsigned char* buf = lds + ((nbm + e) % GR_NBUF) * GR_BLK;
-#pragma unroll
-        for (int t = 0; t < 7; ++t) {
-            bf16x8 b[3];
-            load_b(buf, tro, t, b);
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b, acc[rt][t]);
-        }
+        mma_block(lds + ((nbm + e) % GR_NBUF) * GR_BLK, tro, a, acc);
     }
     // dZt = -gscale acc
     const float sc = -A.gscale;
@@ -399,23 +399,23 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// k_gram_c: unit (c, 32-row group m): dZb[n][x] = gscale (sum_{v <= 100} Zb^[n][v] Gt[v][x] - sum_s T_b[s][n][x]).
-// 256 threads; wave wv handles the group's accumulator tiles (rt, t) = wv, wv + 4, ... of 14, lane layout of the
-// T_b slabs (rows 4lg + r, column lr). Gt (101 x 112) and Zb^T (101 x 32) staged in LDS.
+// dZb epilogue unit (c, 32-row group m) of k_gram_b: dZb[n][x] = gscale (sum_{v <= 100} Zb^[n][v] Gt[v][x] - sum_s T_b[s][n][x]).
+// Wave wv handles the group's accumulator tiles (rt, t) = wv, wv + 9, ... of 14, lane layout of the T_b slabs (rows
+// 4lg + r, column lr). Gt (101 x 112) and Zb^T (101 x 32) staged in the workgroup's LDS ring.
 // ---------------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gram_c(GramArgs A) {
-    __shared__ __attribute__((aligned(16))) float gts[101 * 112];
-    __shared__ __attribute__((aligned(16))) float zbt[101 * 32];
+__device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char* lds) {
+    float* gts = reinterpret_cast<float*>(lds);                  // Gt [101][112]
+    float* zbt = gts + 101 * 112;                                // Zb^T [101][32]
     const int ngroups = (A.N + 31) / 32;
-    const int c = blockIdx.x / ngroups, m = blockIdx.x - c * ngroups;
+    const int c = u / ngroups, m = u - c * ngroups;
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const float* gt = A.gt + c * A.gt_cs2;
-    for (int e = tid; e < 101 * 28; e += 256) {
+    for (int e = tid; e < 101 * 28; e += GR_THREADS) {
         const int v = e / 28, q = e - v * 28;
         *reinterpret_cast<f32x4*>(gts + v * 112 + 4 * q) = *reinterpret_cast<const f32x4*>(gt + v * 112 + 4 * q);
     }
     const float* zb = A.zb + c * A.zb_cs;
-    for (int e = tid; e < 32 * 101; e += 256) {
+    for (int e = tid; e < 32 * 101; e += GR_THREADS) {
         const int row = e / 101, v = e - row * 101, n = 32 * m + row;
         float z = 0.f;
         if (n < A.N) z = v < 100 ? zb[(int64_t)n * A.ldz + v] : 1.f;
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(256) void k_gram_c(GramArgs A) {
     const float* tb = A.tb_part + c * A.tb_cs + ((int64_t)(ng * GR_CW + w8) * 14) * 256 + 4 * lane;
     const int64_t sstride = (int64_t)A.NG * GR_CW * 14 * 256;
     float* out = A.dzb + c * A.dzb_cs;
-    for (int tile = wv; tile < 14; tile += 4) {
+    for (int tile = wv; tile < 14; tile += GR_THREADS / 64) {
         const int rt = tile / 7, t = tile - rt * 7;
         f32x4 ts = {0.f, 0.f, 0.f, 0.f};
         for (int ss = 0; ss < A.S; ++ss) {
@@ -493,10 +493,10 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     a.upx_a = (n1 + 7) / 8;
     const int gpx = (n2 + 7) / 8;
     a.upx_b = (a.PT * a.C + 7) / 8;
-    hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
+    const int cpx = (a.C * ((a.N + 31) / 32) + 7) / 8;
+    if (!a.aug_done) hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gram_a, dim3(8 * (a.upx_a + gpx)), dim3(GR_THREADS), GR_LDS, s, a);
-    hipLaunchKernelGGL(k_gram_b, dim3(8 * a.upx_b), dim3(GR_THREADS), GR_LDS, s, a);
-    hipLaunchKernelGGL(k_gram_c, dim3(a.C * ((a.N + 31) / 32)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gram_b, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GR_LDS, s, a);
     return hipGetLastError();
 }
 

@@ -155,6 +155,7 @@ struct GramArgs {
     const float* b0; int64_t b0_cs;
     int32_t N, P, ldz, NG, S, SL, PT, C;
     int32_t upx_a, upx_b;                                  // set by launch_gram
+    int32_t aug_done;                                      // feature 100 of both images already written
     float gscale;
 };
 hipError_t launch_gram(const GramArgs& a, hipStream_t s);
@@ -276,6 +277,9 @@ struct FusedNet {
     unsigned char* qimg; int64_t qimg_cs;           // or null: the last layer's output also written as the
                                                     // contraction's pre-split block image (k_split_blocks'
                                                     // layout; padding pre-zeroed by the plan)
+    int32_t aug;                                    // feature 100 of that image: 0 = zero, 1 = one (branch),
+                                                    // 2 = the chain's output bias b0 (trunk): the Gram form's
+                                                    // augmented outputs (vihmc_gram.hip; unused by the other paths)
 };
 struct FusedArgs {
     FusedNet net[2];

@@ -800,6 +800,10 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
             a.net[0].qimg_cs = p->qsplitA_cs;
             a.net[1].qimg = p->qsplitB;
             a.net[1].qimg_cs = p->qsplitB_cs;
+            if (p->gram_alloc) {                           // the Gram form's augmented outputs [Z_b | 1], [Z_t | b0]
+                a.net[0].aug = 1;
+                a.net[1].aug = 2;
+            }
             p->img_by_fwd = true;
         }
         if (p->fwd_wimg && p->wimg) {
@@ -1006,7 +1010,9 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         }
         hipEvent_t stop = nullptr;
         if (int rc = p->timing_begin(VIHMC_T_GRAM, s, &stop)) return rc;
-        HIPCHK(launch_gram(gram_args(p, C), s));
+        GramArgs ga = gram_args(p, C);
+        ga.aug_done = p->img_by_fwd ? 1 : 0;               // the fused forward wrote feature 100 of both images
+        HIPCHK(launch_gram(ga, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
         stats_waves = p->gPT * 8;
     } else {

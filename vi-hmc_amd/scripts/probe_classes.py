@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default="")
     ap.add_argument("--opt", action="append", default=[], help="plan option key=value (repeatable)")
+    ap.add_argument("--grad", action="store_true", help="gradient-only evaluations (vihmc_grad: the Gram form)")
     ap.add_argument("--config4", action="store_true",
                     help="config 4's evaluation: one data shard of N/2 functions, every parameter sampled")
     args = ap.parse_args()
@@ -45,20 +46,21 @@ def main():
         eng.option(k, int(v))
     th = torch.tensor(np.tile(prob.mu[prob.grad_ind], (C, 1)), device="cuda:0")
     th += 0.001 * torch.randn_like(th)
+    ev = (lambda t: eng.grad(t)) if args.grad else (lambda t: eng.logp_grad(t))
     for _ in range(5):
-        eng.logp_grad(th)
+        ev(th)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.iters):
-        eng.logp_grad(th)
+        ev(th)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / args.iters * 1e3
     eng.timing(-1, True)
     for _ in range(args.iters):
-        eng.logp_grad(th)
+        ev(th)
     torch.cuda.synchronize()
-    names = ["contract_a", "contract_b", "bwd", "fwd", "eval"]
-    out = {n: eng.timing_class(i)[0] / args.iters for i, n in enumerate(names)}
+    names = {0: "contract_a", 1: "contract_b", 2: "bwd", 3: "fwd", 4: "eval", 6: "gram"}
+    out = {n: eng.timing_class(i)[0] / args.iters for i, n in names.items()}
     eng.timing(-1, False)
     print(f"{args.tag:12s} C={C} wall {wall:.4f} ms/eval | " + " ".join(f"{n} {v:.4f}" for n, v in out.items()),
           flush=True)
