@@ -92,11 +92,15 @@ __device__ __forceinline__ void mma_block(const unsigned char* buf, int tro, con
     }
 }
 
-// unit of a workgroup with XCD-contiguous unit ranges (workgroup b runs on XCD b % 8): the first `upx` slots of
-// every XCD take units [x upx, (x + 1) upx) of the grouped list, the next `gpx` slots round-robin units of the
-// second list; -1 = idle slot
+// unit of a workgroup with XCD-contiguous unit ranges (workgroup b runs on XCD b % 8, checked by
+// scripts/diag/xcc_probe.hip): `upx` slots of every XCD take units [x upx, (x + 1) upx) of the grouped list, `gpx`
+// slots round-robin units of the second list; -1 = idle slot. The second list is dispatched first: k_gram_a's Gram units and k_gram_b's dZb epilogue units are shorter than
+// the GEMM units, which then fill the chip behind them (gradient-only evaluation at 16 chains: Gram form 0.542 ->
+// 0.525 ms, profiles/r03u_ab_gram.txt; raising the wave priority around the MFMAs measured neutral)
 __device__ __forceinline__ void unit_of(int b, int upx, int n1, int n2, int& list, int& u) {
-    const int x = b & 7, k = b >> 3;
+    const int x = b & 7, gpx = (n2 + 7) / 8;
+    int k = b >> 3;
+    k = k < gpx ? k + upx : k - gpx;
     if (k < upx) {
         list = 0;
         u = x * upx + k;
