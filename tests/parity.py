@@ -59,6 +59,15 @@ BOUNDS = {
     ("test_forward_without_weight_images_matches", "grad_relnorm"): 2e-06,   # max 2.77e-07 over 1
     ("test_forward_without_weight_images_matches", "logp_rel"): 2e-07,   # max 0.00e+00 over 1
     ("test_inv_mass_fused_trajectory_vs_scalar_reference", "pos_maxabs"): 1e-06,   # max 2.38e-07 over 4
+    # Gram-form gradient-only contraction (tests/test_gpu_gram.py), measured r03 (profiles/r03w_parity_errors.json)
+    ("test_gram_grad_burgers_matches_golden", "grad_elem"): 3e-06,   # max 5.19e-07 over 21
+    ("test_gram_grad_burgers_matches_golden", "grad_norm_rel"): 8e-07,   # max 1.82e-07 over 21
+    ("test_gram_grad_burgers_matches_golden", "grad_relnorm"): 2e-06,   # max 2.74e-07 over 21 (vs the residual form)
+    ("test_gram_grad_refshape_vs_fp64_oracle", "grad_relnorm"): 2e-07,   # max 3.77e-08 over 4
+    ("test_gram_grad_refshape_vs_fp64_oracle", "grad_elem"): 4e-07,   # max 9.25e-08 over 4
+    ("test_gram_after_set_data_and_trunk_rows", "grad_relnorm"): 4e-08,   # max 8.14e-09 over 2
+    ("test_full_shape_grad_vs_fp64_oracle", "grad_relnorm"): 1e-05,   # max 2.41e-06 (gram), 1.46e-06 (residual)
+    ("test_full_shape_grad_vs_fp64_oracle", "grad_elem"): 2e-05,   # max 3.25e-06 (gram), 1.52e-06 (residual)
     ("test_refshape_trajectories_accepts_and_predictive_mean", "mean_rel_l2"): 9e-07,   # max 2.07e-07 over 1
     ("test_refshape_trajectories_accepts_and_predictive_mean", "pos_maxabs"): 3e-07,   # max 5.96e-08 over 2
     ("test_split_burgers_shard_closures_match_reference", "grad_elem"): 3e-06,   # max 5.49e-07 over 8

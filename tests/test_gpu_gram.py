@@ -120,3 +120,26 @@ def test_gram_deterministic(cuda_device):
     a = eng.grad(th).clone()
     for _ in range(3):
         assert torch.equal(eng.grad(th), a)
+
+
+@pytest.mark.parametrize("form", ["gram", "residual"])
+def test_full_shape_grad_vs_fp64_oracle(form, cuda_device):
+    """Full Burgers shape, the golden theta and a perturbed copy: the gradient of each contraction form against the fp64 oracle (the
+    reference's own fp32 closure is within ~1e-7 of it: its goldens' grad subsample). Records how much precision the
+    Gram form's cancellation (Zb^ Gt vs y Zt^, sums over P = 10,201 points) costs next to the residual form."""
+    c = deeponet_case("deeponet_burgers")
+    p = c.prob
+    s = c.spec
+    eng = engine_for(c, 2, cuda_device)
+    th0 = np.asarray(c.thetas[0], np.float32)
+    thetas = [th0, (th0 + 0.01 * np.random.default_rng(11).standard_normal(th0.size)).astype(np.float32)]
+    th = torch.tensor(np.stack(thetas), device=cuda_device)
+    g = (eng.grad(th) if form == "gram" else eng.logp_grad(th)[1]).cpu().numpy()
+    assert bool(eng.get_option("gram") & 2) == (form == "gram")
+    lay = deeponet_layout(s.in_branch, s.width_branch, s.depth_branch, s.in_trunk, s.width_trunk, s.depth_trunk,
+                          s.out)
+    for i in range(2):
+        _, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, thetas[i], c.prior_mu,
+                                c.prior_sd, c.loss, c.tau_out)
+        parity.check("grad_relnorm", rel_norm(g[i], rg), f"{form} theta{i}")
+        parity.check("grad_elem", np.abs(g[i] - rg).max() / np.abs(rg).max(), f"{form} theta{i}")

@@ -220,9 +220,14 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
             for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(dst + (rt * 7 + t) * 256) = acc[rt][t];
     } else {
     // ---------------- Gram rows: wave w < 7 = row tile w ----------------
-    f32x4 acc[7];
+    // Every element of Gt / Gb enters all N (P) rows of the other side's correction product, so its rounding error
+    // adds up coherently in the last layer's bias gradient (a sum over rows): each block's six products are summed
+    // from zero in fp32 (one 32-long dot) and the blocks in fp64 -- not 240 fp32 roundings of one running sum.
+    double acc[7][4];
 #pragma unroll
-    for (int t = 0; t < 7; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 7; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][r] = 0.0;
     const int w = min(wave, 6);
     for (int i = 0; i < nb; ++i) {
         __syncthreads();
@@ -234,7 +239,9 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
             for (int t = 0; t < 7; ++t) {
                 bf16x8 b[3];
                 load_b(buf, tro, t, b);
-                acc[t] = six(a, b, acc[t]);
+                const f32x4 blk = six(a, b, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[t][r] += (double)blk[r];
             }
         }
     }
@@ -247,7 +254,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int v = 16 * w + 4 * lg + r, x = 16 * t + lr;
-                    const float val = -acc[t][r];
+                    const float val = (float)-acc[t][r];
                     const __bf16 p0 = (__bf16)val;
                     const float rr = val - (float)p0;
                     const __bf16 p1 = (__bf16)rr;
@@ -259,15 +266,16 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         }
     } else if (wave < 7) {
         // Gram-t slab s of chain c
-        float* part = A.gt_part + c * A.gt_cs;
+        double* part = A.gt_part + c * A.gt_cs;
 #pragma unroll
         for (int t = 0; t < 7; ++t)
-            *reinterpret_cast<f32x4*>(part + ((s * 7 + w) * 7 + t) * 256 + 4 * lane) = acc[t];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[((s * 7 + w) * 7 + t) * 256 + 4 * lane + r] = acc[t][r];
     }
     }
     if (kind != 1) return;
     // every wave (the DMA wave too) reaches the barriers below
-    const float* part = A.gt_part + c * A.gt_cs;
+    const double* part = A.gt_part + c * A.gt_cs;
     __shared__ int is_last;
     __syncthreads();
     if (tid == 0) {
@@ -281,11 +289,11 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     float* gt = A.gt + c * A.gt_cs2;
     for (int e = tid; e < 49 * 256; e += GR_CW * 64) {
         const int tile = e >> 8, within = e & 255, l = within >> 2, r = within & 3;
-        float sum = 0.f;
+        double sum = 0.0;
         for (int ss = 0; ss < A.S; ++ss)
             sum += __hip_atomic_load(part + ss * 49 * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int vt = tile / 7, t = tile - vt * 7;
-        gt[(16 * vt + 4 * (l >> 4) + r) * 112 + 16 * t + (l & 15)] = sum;
+        gt[(16 * vt + 4 * (l >> 4) + r) * 112 + 16 * t + (l & 15)] = (float)sum;
     }
     if (tid == 0) A.cnt[c] = 0u;
 }

@@ -144,7 +144,7 @@ struct GramArgs {
     const __bf16* ya; int64_t ya_plane; int32_t ya_ld;     // y [NG*256 rows n][32 nblkP], 3 planes, kpos order
     const __bf16* yb; int64_t yb_plane; int32_t yb_ld;     // y^T [PT*256 rows p][32 nblkN], 3 planes
     float* tb_part; int64_t tb_cs;                         // [C][S][NG][8 waves][14 tiles][256]
-    float* gt_part; int64_t gt_cs;                         // [C][S][49 tiles][256]
+    double* gt_part; int64_t gt_cs;                        // [C][S][49 tiles][256] (fp64 slab sums)
     float* gt; int64_t gt_cs2;                             // [C][112][112] Zt^T Zt^
     unsigned char* gbimg; int64_t gbimg_cs;                // [C][4 blocks] -Zb^T Zb^ pre-split
     uint32_t* cnt;                                         // [C] Gram-t slab counters (self-resetting)

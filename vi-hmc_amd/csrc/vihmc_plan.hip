@@ -160,7 +160,7 @@ struct vihmc_plan {
     int gya_ld = 0, gyb_ld = 0, gNG = 0, gS = 0, gSL = 0, gPT = 0;
     float* gtb_part = nullptr;
     int64_t gtb_cs = 0;
-    float* ggt_part = nullptr;
+    double* ggt_part = nullptr;
     int64_t ggt_part_cs = 0;
     float* ggt = nullptr;
     unsigned char* ggb = nullptr;
