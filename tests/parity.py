@@ -59,7 +59,7 @@ BOUNDS = {
     ("test_forward_without_weight_images_matches", "grad_relnorm"): 2e-06,   # max 2.77e-07 over 1
     ("test_forward_without_weight_images_matches", "logp_rel"): 2e-07,   # max 0.00e+00 over 1
     ("test_inv_mass_fused_trajectory_vs_scalar_reference", "pos_maxabs"): 1e-06,   # max 2.38e-07 over 4
-    # Gram-form gradient-only contraction (tests/test_gpu_gram.py), measured r03 (profiles/r03w_parity_errors.json)
+    # Gram-form gradient-only contraction (tests/test_gpu_gram.py), measured r03 (profiles/r03w_parity_errors_gram.json)
     ("test_gram_grad_burgers_matches_golden", "grad_elem"): 3e-06,   # max 5.19e-07 over 21
     ("test_gram_grad_burgers_matches_golden", "grad_norm_rel"): 8e-07,   # max 1.82e-07 over 21
     ("test_gram_grad_burgers_matches_golden", "grad_relnorm"): 2e-06,   # max 2.74e-07 over 21 (vs the residual form)
