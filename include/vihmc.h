@@ -210,8 +210,8 @@ int vihmc_graph_enable(vihmc_plan* p, int on);
  * G, dZ_trunk; width 100) and side B. "bwd_bf16x6" (default 1): the same for the layer backward (dX,
  * dW, db of layers with 100 outputs); its default (environment VIHMC_BWD_BF16) also sizes the backward
  * row chunks at plan creation. "graph" = vihmc_graph_enable. "gram" (default 1): gradient-only DeepONet
- * evaluations (vihmc_grad, the inner steps of vihmc_trajectory) in Gram form; "gram_min_chains" (default 2): the
- * smallest chain count that uses it. Changing an option drops captured graphs.
+ * evaluations (vihmc_grad, the inner steps of vihmc_trajectory) in Gram form; "gram_min_chains" (default 4): the
+ * smallest chain count that uses it (default 4: below it the residual form's split sweeps fill the chip better). Changing an option drops captured graphs.
  * Returns nonzero for an unknown key. */
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value);
 /* Current value of an option (contract_bf16x6 reads 1 only where the bf16x6 contraction applies,

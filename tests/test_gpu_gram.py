@@ -17,11 +17,13 @@ from oracle.deeponet_ref import deeponet_layout, np_logp_grad
 pytestmark = pytest.mark.gpu
 
 
-def engine_for(c, max_chains, device):
+def engine_for(c, max_chains, device, min_chains=2):
     from vihmc.engine import DeepONetEngine, trunk_features
     p = c.prob
-    return DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
-                          c.prior_sd, c.loss, c.tau_out, max_chains=max_chains, device=device)
+    eng = DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
+                         c.prior_sd, c.loss, c.tau_out, max_chains=max_chains, device=device)
+    eng.option("gram_min_chains", min_chains)       # the tests run the Gram form from 2 chains (default 4)
+    return eng
 
 
 def rel_norm(a, b):
@@ -76,17 +78,19 @@ def test_gram_grad_refshape_vs_fp64_oracle(cuda_device):
 
 
 def test_gram_option_off_is_the_residual_form(cuda_device):
-    """gram = 0 (or one chain below gram_min_chains): vihmc_grad is bitwise the gradient of vihmc_logp_grad."""
+    """gram = 0 (or fewer chains than gram_min_chains): vihmc_grad is bitwise the gradient of vihmc_logp_grad; the
+    default threshold is 4 chains."""
     c = deeponet_case("deeponet_refshape")
     eng = engine_for(c, 2, cuda_device)
     th = torch.tensor(np.stack(c.thetas[:2]), device=cuda_device)
     _, gr = eng.logp_grad(th)
+    assert eng.get_option("gram_min_chains") == 2
     eng.option("gram", 0)
     g = eng.grad(th)
     assert not eng.get_option("gram") & 2
     assert torch.equal(g, gr)
     eng.option("gram", 1)
-    g1 = eng.grad(th[:1])            # C = 1 < gram_min_chains (2)
+    g1 = eng.grad(th[:1])            # C = 1 < gram_min_chains (2 here)
     assert not eng.get_option("gram") & 2
     assert torch.equal(g1, gr[:1])
 

@@ -152,7 +152,9 @@ struct vihmc_plan {
     int bwd_chain = 1;            // plan option: whole-network backward in one launch when the chunks are 64 rows
     // Gram-form gradient-only contraction (vihmc_gram.hip) for the evaluations that return no log-prob (the
     // trajectory's inner leapfrog steps, vihmc_grad): plan options "gram" (on / off) and "gram_min_chains"
-    int gram = 1, gram_min_chains = 2;
+    // (gradient-only evaluation, Gram vs residual form, ms: C = 2 0.40 vs 0.34, C = 4 0.50 vs 0.53, C = 16 1.36 vs 1.48;
+    // profiles/r03x_gram_crossover.txt)
+    int gram = 1, gram_min_chains = 4;
     bool gram_alloc = false;      // W = 100 plan: images and work buffers allocated
     __bf16* gya = nullptr;        // y [NG*256][32 nblkP], 3 planes (kpos order inside each 32-long p block)
     __bf16* gyb = nullptr;        // y^T [PT*256][32 nblkN], 3 planes
