@@ -78,15 +78,20 @@ __device__ __forceinline__ void load_b(const unsigned char* buf, int tro, int t,
     for (int pl = 0; pl < 3; ++pl) b[pl] = bf6::tr_frag(buf + pl * GR_PL, tro, 16 * t);
 }
 
+#ifndef GR_ABL
+#define GR_ABL 0   // timing-only ablations (wrong results): 1 = no A loads in the main loops, 2 = one B fragment per
+                   // block (no per-tile LDS reads), 3 = both
+#endif
 // one 32-long k block of a wave's 32 x 112 tile: B fragments of column tile t+1 read while tile t's 12 MFMAs run
 // (double-buffered fragments, so the wait before tile t's products leaves the next tile's reads in flight)
 __device__ __forceinline__ void mma_block(const unsigned char* buf, int tro, const bf16x8 (&a)[2][3],
                                           f32x4 (&acc)[2][7]) {
     bf16x8 b[2][3];
     load_b(buf, tro, 0, b[0]);
+    if (GR_ABL & 2) load_b(buf, tro, 1, b[1]);
 #pragma unroll
     for (int t = 0; t < 7; ++t) {
-        if (t < 6) load_b(buf, tro, t + 1, b[(t + 1) & 1]);
+        if (t < 6 && !(GR_ABL & 2)) load_b(buf, tro, t + 1, b[(t + 1) & 1]);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b[t & 1], acc[rt][t]);
     }
@@ -188,7 +193,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         const int64_t rt16 = 16 * (int64_t)A.ya_ld;
         bf16x8 a0[2][3], a1[2][3];
         auto load_a = [&](bf16x8 (&a)[2][3], int i) __attribute__((always_inline)) {
-            const int ii = min(i, nb - 1);
+            const int ii = (GR_ABL & 1) ? 0 : min(i, nb - 1);
 #pragma unroll
             for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -332,7 +337,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     const int64_t rt16 = 16 * (int64_t)A.yb_ld;
     bf16x8 a0[2][3], a1[2][3];
     auto load_a = [&](bf16x8 (&a)[2][3], int i) __attribute__((always_inline)) {
-        const int ii = min(i, nbm - 1);
+        const int ii = (GR_ABL & 1) ? 0 : min(i, nbm - 1);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -495,6 +500,9 @@ hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya
 }
 
 int gram_lds_bytes() { return GR_LDS; }
+
+// timing-only switches this translation unit was built with (0 = product build)
+int diag_switches_gram() { return GR_ABL; }
 
 hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     GramArgs a = a0;

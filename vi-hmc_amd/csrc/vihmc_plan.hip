@@ -240,7 +240,7 @@ struct vihmc_plan {
 namespace vihmc {
 int diag_switches() {
     return diag_switches_fused() | diag_switches_contract_bf() | diag_switches_bwd_bf() | diag_switches_layers() |
-           diag_switches_bwd_chain();
+           diag_switches_bwd_chain() | diag_switches_gram();
 }
 }  // namespace vihmc
 
