@@ -146,9 +146,9 @@ __global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
 // list 1 = Gram units (C * S Gram-t slabs, then C Gram-b).
 //   T_b unit (ng, s, c): rows n0 = 256 ng + 32 w of wave w, trunk blocks [s SL, (s+1) SL): acc[2][7] tiles, stored
 //     tile-major to tb_part[c][s][ng][w][rt][t] (256 floats = 64 lanes x float4 each).
-//   Gram-t (c, s): wave w < 7 computes row tile w (features v = 16w..16w+15) of Zt^T Zt^ over the slab; its A
-//     operand is the B fragment of column tile w. Stored to gt_part[c][s][w][t]; the last slab of chain c to finish
-//     sums the S slabs in order s = 0.. into gt[c] ([112 v][112 w] fp32) and resets the counter.
+//   Gram-t (c, s): the 28 upper 16x16 tiles of Zt^T Zt^ over the slab (4 per wave, A = the B fragment of the tile's
+//     row); stored to gt_part[c][s][28][256] (fp64); the last slab of chain c to finish sums the S slabs in order
+//     s = 0.. into gt[c] ([112 v][112 w] fp32, both halves) and resets the counter.
 //   Gram-b (c): the same over all branch blocks; -Gb written pre-split as 4 blocks (rows v, k of the extension).
 // ---------------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
@@ -224,58 +224,70 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
 #pragma unroll
             for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(dst + (rt * 7 + t) * 256) = acc[rt][t];
     } else {
-    // ---------------- Gram rows: wave w < 7 = row tile w ----------------
+    // ---------------- Gram tiles: the 28 tiles (vt <= t) of the symmetric 112 x 112 matrix, 4 per wave ------------
     // Every element of Gt / Gb enters all N (P) rows of the other side's correction product, so its rounding error
     // adds up coherently in the last layer's bias gradient (a sum over rows): each block's six products are summed
     // from zero in fp32 (one 32-long dot) and the blocks in fp64 -- not 240 fp32 roundings of one running sum.
-    double acc[7][4];
+    // Wave w < 7 owns tiles j = w, w+7, w+14, w+21 of the row-major upper-triangle list (A = the B fragment of row
+    // tile vt); the mirror half is written from them.
+    double acc[4][4];
+    int tvt[4], tt[4];
 #pragma unroll
-    for (int t = 0; t < 7; ++t)
+    for (int q = 0; q < 4; ++q) {
+        int rem = min(wave, 6) + 7 * q, vt = 0;
+        while (rem >= 7 - vt) rem -= 7 - vt++;
+        tvt[q] = vt;
+        tt[q] = vt + rem;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[t][r] = 0.0;
-    const int w = min(wave, 6);
+        for (int r = 0; r < 4; ++r) acc[q][r] = 0.0;
+    }
     for (int i = 0; i < nb; ++i) {
         __syncthreads();
         if (wave < 7) {
             const unsigned char* buf = lds + (i % GR_NBUF) * GR_BLK;
-            bf16x8 a[3];
-            load_b(buf, tro, w, a);
 #pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                bf16x8 b[3];
-                load_b(buf, tro, t, b);
+            for (int q = 0; q < 4; ++q) {
+                bf16x8 a[3], b[3];
+                load_b(buf, tro, tvt[q], a);
+                load_b(buf, tro, tt[q], b);
                 const f32x4 blk = six(a, b, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[t][r] += (double)blk[r];
+                for (int r = 0; r < 4; ++r) acc[q][r] += (double)blk[r];
             }
         }
     }
     if (kind == 2) {
-        // -Gb pre-split into the extension blocks: element (v, x) -> block v / 32, row v % 32, feature x
+        // -Gb pre-split into the extension blocks: element (v, x) -> block v / 32, row v % 32, feature x; both halves
         if (wave < 7) {
             unsigned char* gb = A.gbimg + c * A.gbimg_cs;
+            auto put = [&](int v, int x, float val) __attribute__((always_inline)) {
+                const __bf16 p0 = (__bf16)val;
+                const float rr = val - (float)p0;
+                const __bf16 p1 = (__bf16)rr;
+                unsigned char* e = gb + (v / 32) * CONTRACT_SPLIT_BLOCK + (v % 32) * bf6::PITCH + 2 * x;
+                *reinterpret_cast<__bf16*>(e) = p0;
+                *reinterpret_cast<__bf16*>(e + GR_PL) = p1;
+                *reinterpret_cast<__bf16*>(e + 2 * GR_PL) = (__bf16)(rr - (float)p1);
+            };
 #pragma unroll
-            for (int t = 0; t < 7; ++t)
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int v = 16 * w + 4 * lg + r, x = 16 * t + lr;
-                    const float val = (float)-acc[t][r];
-                    const __bf16 p0 = (__bf16)val;
-                    const float rr = val - (float)p0;
-                    const __bf16 p1 = (__bf16)rr;
-                    unsigned char* e = gb + (v / 32) * CONTRACT_SPLIT_BLOCK + (v % 32) * bf6::PITCH + 2 * x;
-                    *reinterpret_cast<__bf16*>(e) = p0;
-                    *reinterpret_cast<__bf16*>(e + GR_PL) = p1;
-                    *reinterpret_cast<__bf16*>(e + 2 * GR_PL) = (__bf16)(rr - (float)p1);
+                    const int v = 16 * tvt[q] + 4 * lg + r, x = 16 * tt[q] + lr;
+                    const float val = (float)-acc[q][r];
+                    put(v, x, val);
+                    if (tvt[q] != tt[q]) put(x, v, val);
                 }
         }
-    } else if (wave < 7) {
-        // Gram-t slab s of chain c
+        return;
+    }
+    if (wave < 7) {
+        // Gram-t slab s of chain c: the 28 upper tiles
         double* part = A.gt_part + c * A.gt_cs;
 #pragma unroll
-        for (int t = 0; t < 7; ++t)
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) part[((s * 7 + w) * 7 + t) * 256 + 4 * lane + r] = acc[t][r];
+            for (int r = 0; r < 4; ++r) part[((s * 28) + wave + 7 * q) * 256 + 4 * lane + r] = acc[q][r];
     }
     }
     if (kind != 1) return;
@@ -292,13 +304,16 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     __threadfence();
     // fixed-order sum of the S slabs -> gt[c][v][x]
     float* gt = A.gt + c * A.gt_cs2;
-    for (int e = tid; e < 49 * 256; e += GR_CW * 64) {
+    for (int e = tid; e < 28 * 256; e += GR_CW * 64) {
         const int tile = e >> 8, within = e & 255, l = within >> 2, r = within & 3;
         double sum = 0.0;
         for (int ss = 0; ss < A.S; ++ss)
-            sum += __hip_atomic_load(part + ss * 49 * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int vt = tile / 7, t = tile - vt * 7;
-        gt[(16 * vt + 4 * (l >> 4) + r) * 112 + 16 * t + (l & 15)] = (float)sum;
+            sum += __hip_atomic_load(part + ss * 28 * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int rem = tile, vt = 0;
+        while (rem >= 7 - vt) rem -= 7 - vt++;
+        const int t = vt + rem, v = 16 * vt + 4 * (l >> 4) + r, x = 16 * t + (l & 15);
+        gt[v * 112 + x] = (float)sum;
+        gt[x * 112 + v] = (float)sum;        // the mirror (a diagonal tile writes its own elements twice)
     }
     if (tid == 0) A.cnt[c] = 0u;
 }

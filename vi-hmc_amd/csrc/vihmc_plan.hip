@@ -346,7 +346,7 @@ int gram_setup(vihmc_plan* p, int C) {
     if (int rc = p->alloc(&p->gyb, 3 * p->gyb_plane)) return rc;
     p->gtb_cs = (int64_t)p->gS * p->gNG * 8 * 14 * 256;
     if (int rc = p->alloc(&p->gtb_part, p->gtb_cs * C)) return rc;
-    p->ggt_part_cs = (int64_t)p->gS * 49 * 256;
+    p->ggt_part_cs = (int64_t)p->gS * 28 * 256;          // the 28 upper tiles per slab
     if (int rc = p->alloc(&p->ggt_part, p->ggt_part_cs * C)) return rc;
     if (int rc = p->alloc(&p->ggt, (int64_t)112 * 112 * C)) return rc;
     if (int rc = p->alloc(&p->ggb, (int64_t)4 * CONTRACT_SPLIT_BLOCK * C)) return rc;
