@@ -99,13 +99,13 @@ __device__ __forceinline__ void mma_block(const unsigned char* buf, int tro, con
 
 // unit of a workgroup with XCD-contiguous unit ranges (workgroup b runs on XCD b % 8, checked by
 // scripts/diag/xcc_probe.hip): `upx` slots of every XCD take units [x upx, (x + 1) upx) of the grouped list, `gpx`
-// slots round-robin units of the second list; -1 = idle slot. The second list is dispatched first: k_gram_a's Gram units and k_gram_b's dZb epilogue units are shorter than
+// slots round-robin units of the second list; -1 = idle slot. second_first: k_gram_a's Gram units are shorter than
 // the GEMM units, which then fill the chip behind them (gradient-only evaluation at 16 chains: Gram form 0.542 ->
 // 0.525 ms, profiles/r03u_ab_gram.txt; raising the wave priority around the MFMAs measured neutral)
-__device__ __forceinline__ void unit_of(int b, int upx, int n1, int n2, int& list, int& u) {
+__device__ __forceinline__ void unit_of(int b, int upx, int n1, int n2, int& list, int& u, bool second_first = true) {
     const int x = b & 7, gpx = (n2 + 7) / 8;
     int k = b >> 3;
-    k = k < gpx ? k + upx : k - gpx;
+    if (second_first) k = k < gpx ? k + upx : k - gpx;
     if (k < upx) {
         list = 0;
         u = x * upx + k;
@@ -329,7 +329,9 @@ __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     int list, u;
-    unit_of(blockIdx.x, A.upx_b, A.PT * A.C, A.C * ((A.N + 31) / 32), list, u);
+    // the dZb epilogue units go last: they fill the half round the 640 T_t units leave at 16 chains (0.531 -> 0.519 ms,
+    // profiles/r03z_ab_gram_epi_last.txt)
+    unit_of(blockIdx.x, A.upx_b, A.PT * A.C, A.C * ((A.N + 31) / 32), list, u, false);
     if (list < 0) return;
     if (list == 1) {                   // the dZb epilogue units fill the tail of the T_t rounds (k_gram_a is done)
         dzb_unit(A, u, lds);
