@@ -16,7 +16,8 @@
 // 32-long k-block, fp32 accumulation -- fp32-level accuracy, no splits inside the loops.
 //
 // Kernels (one evaluation, C chains):
-//   k_gram_aug   feature 100 of the pre-split output images: 1 (branch rows < N), b0 (trunk rows < P)
+//   k_gram_aug   feature 100 of the pre-split output images: 1 (branch rows < N), b0 (trunk rows < P) -- only when
+//                the fused forward did not write the images (it writes that column itself, FusedNet::aug)
 //   k_gram_a     T_b = y Zt^ over the trunk image (split-K partial slabs), Gt = Zt^T Zt^ (split-K, the last
 //                slab of a chain sums them in fixed order), Gb = Zb^T Zb^ (written negated, pre-split, as the
 //                B blocks of k_gram_b's extension)
@@ -516,7 +517,6 @@ hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya
     return hipGetLastError();
 }
 
-int gram_lds_bytes() { return GR_LDS; }
 
 // timing-only switches this translation unit was built with (0 = product build)
 int diag_switches_gram() { return GR_ABL; }

@@ -161,7 +161,6 @@ struct GramArgs {
 hipError_t launch_gram(const GramArgs& a, hipStream_t s);
 hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld, __bf16* yb,
                             int64_t yb_plane, int yb_ld, hipStream_t s);
-int gram_lds_bytes();
 
 // launchers (vihmc_kernels.hip)
 hipError_t launch_rowdot(const RowdotArgs& a, int nt, int ms, int mode, hipStream_t s);
