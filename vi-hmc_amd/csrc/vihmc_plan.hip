@@ -335,7 +335,7 @@ int gram_setup(vihmc_plan* p, int C) {
     const int nblkN = cdiv(p->N, CONTRACT_SPLIT_ROWS), nblkP = cdiv(p->P, CONTRACT_SPLIT_ROWS);
     p->gNG = cdiv(p->N, 256);
     p->gPT = cdiv(p->P, 256);
-    p->gS = 8;
+    p->gS = 8;          // slabs 4 / 8 / 12: 0.499 / 0.496 / 0.523 ms per Gram-form evaluation (profiles/r03z_ab_gram_slabs.txt)
     p->gSL = cdiv(nblkP, p->gS);
     p->gS = cdiv(nblkP, p->gSL);
     p->gya_ld = 32 * nblkP;
