@@ -66,6 +66,7 @@ BOUNDS = {
     ("test_gram_grad_refshape_vs_fp64_oracle", "grad_relnorm"): 2e-07,   # max 3.77e-08 over 4
     ("test_gram_grad_refshape_vs_fp64_oracle", "grad_elem"): 4e-07,   # max 9.25e-08 over 4
     ("test_gram_after_set_data_and_trunk_rows", "grad_relnorm"): 4e-08,   # max 8.14e-09 over 2
+    ("test_gram_loss_forms_vs_fp64_oracle", "grad_relnorm"): 2e-07,   # max 4.32e-08 over 8
     ("test_full_shape_grad_vs_fp64_oracle", "grad_relnorm"): 1e-05,   # max 2.41e-06 (gram), 1.46e-06 (residual)
     ("test_full_shape_grad_vs_fp64_oracle", "grad_elem"): 2e-05,   # max 3.25e-06 (gram), 1.52e-06 (residual)
     ("test_refshape_trajectories_accepts_and_predictive_mean", "mean_rel_l2"): 9e-07,   # max 2.07e-07 over 1

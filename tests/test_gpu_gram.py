@@ -147,3 +147,26 @@ def test_full_shape_grad_vs_fp64_oracle(form, cuda_device):
                                 c.prior_sd, c.loss, c.tau_out)
         parity.check("grad_relnorm", rel_norm(g[i], rg), f"{form} theta{i}")
         parity.check("grad_elem", np.abs(g[i] - rg).max() / np.abs(rg).max(), f"{form} theta{i}")
+
+
+@pytest.mark.parametrize("loss,tau", [("regression", 2.5), ("NLL", 0.3)])
+def test_gram_loss_forms_vs_fp64_oracle(loss, tau, cuda_device):
+    """Both Gaussian likelihood forms (gscale = -1/tau for 'NLL', -tau for 'regression') and a non-unit tau through
+    the Gram form, against the fp64 oracle at the reference shapes (4 chains)."""
+    from vihmc.engine import DeepONetEngine, trunk_features
+    c = deeponet_case("deeponet_refshape")
+    p, s = c.prob, c.spec
+    C = 4
+    rng = np.random.default_rng(9)
+    thetas = [np.asarray(c.thetas[i % len(c.thetas)], np.float32) +
+              (0.02 * rng.standard_normal(len(c.thetas[0]))).astype(np.float32) * (i > 1) for i in range(C)]
+    eng = DeepONetEngine(s, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu, c.prior_sd,
+                         loss, tau, max_chains=C, device=cuda_device)
+    g = eng.grad(torch.tensor(np.stack(thetas), device=cuda_device)).cpu().numpy()
+    assert eng.get_option("gram") & 2
+    lay = deeponet_layout(s.in_branch, s.width_branch, s.depth_branch, s.in_trunk, s.width_trunk, s.depth_trunk,
+                          s.out)
+    for i, th in enumerate(thetas):
+        _, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, c.prior_mu, c.prior_sd,
+                                loss, tau)
+        parity.check("grad_relnorm", rel_norm(g[i], rg), f"{loss} tau={tau} chain {i}")
