@@ -143,8 +143,9 @@ __global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// k_gram_a: list 0 = T_b units (g = ng * S + s major, chain minor: the 16 chains sharing one YA slab on one XCD),
-// list 1 = Gram units (C * S Gram-t slabs, then C Gram-b).
+// k_gram_a: list 0 = T_b units (g = s * NG + ng major, chain minor: with 8 slabs, XCD x runs slab x -- the chains
+// sharing one YA slab and the n groups sharing one chain's trunk slab are co-resident on one XCD, and its Gram-t units
+// (c * S + s, round robin) land there too), list 1 = Gram units (C * S Gram-t slabs, then C Gram-b).
 //   T_b unit (ng, s, c): rows n0 = 256 ng + 32 w of wave w, trunk blocks [s SL, (s+1) SL): acc[2][7] tiles, stored
 //     tile-major to tb_part[c][s][ng][w][rt][t] (256 floats = 64 lanes x float4 each).
 //   Gram-t (c, s): the 28 upper 16x16 tiles of Zt^T Zt^ over the slab (4 per wave, A = the B fragment of the tile's
@@ -163,8 +164,8 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     if (list == 0) {
         const int g = u / A.C;
         c = u - g * A.C;
-        ng = g / A.S;
-        s = g - ng * A.S;
+        s = g / A.NG;
+        ng = g - s * A.NG;
         kind = 0;
     } else if (u < A.C * A.S) {
         c = u / A.S;
