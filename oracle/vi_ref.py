@@ -5,6 +5,8 @@ bayesian_model.py:76-114 / layers/BBB/BBBLinear.py:54-78 / metrics.py:13-31,58-6
 autograd: for each weight draw j, W_j = mu + eps_j * softplus(rho), pred = DeepONet(W_j) (F.linear + act,
 einsum, + b), loss_j = gaussian_nll(mean) * train_size + beta * KL(prior || posterior); the step's loss is
 the mean over draws. Pinned by tests/golden/vi_deeponet_*.npz (the reference's own train_model).
+``log_var`` (learn_noise, noise_type 0: main_VI_deeponet.py:154-156, metrics.py:21-25): the NLL variance is
+exp(log_var), a trainable scalar; elbo_step then also returns d loss / d log_var.
 """
 from __future__ import annotations
 
@@ -25,15 +27,20 @@ def _mlp(W, layers, x, act):
     return h
 
 
+def _var(y, noise_var, lv):
+    return torch.full_like(y, noise_var) if lv is None else torch.exp(lv) * torch.ones_like(y)
+
+
 def elbo_step(layout, mu, rho, eps_list, branch_in, trunk_grid, y_grid, beta, train_size, noise_var=1.0,
-              prior_mu=0.0, prior_sigma=0.1, act="tanh"):
-    """(loss, d loss / d mu, d loss / d rho) in float64; y_grid [B, P] in trunk_grid order."""
+              prior_mu=0.0, prior_sigma=0.1, act="tanh", log_var=None):
+    """(loss, d loss / d mu, d loss / d rho[, d loss / d log_var]) in float64; y_grid [B, P] in trunk_grid order."""
     br, tr, D = layout
     mu_t = torch.tensor(np.asarray(mu, np.float64), requires_grad=True)
     rho_t = torch.tensor(np.asarray(rho, np.float64), requires_grad=True)
     xb = torch.tensor(np.asarray(branch_in, np.float64))
     ft = torch.tensor(trunk_feats_np(trunk_grid))
     y = torch.tensor(np.asarray(y_grid, np.float64))
+    lv = None if log_var is None else torch.tensor(float(log_var), dtype=torch.float64, requires_grad=True)
     sig = torch.log1p(torch.exp(rho_t))
     sp = torch.tensor(float(prior_sigma), dtype=torch.float64)
     kl = 0.5 * (2 * torch.log(sig / sp) - 1 + (sp / sig) ** 2 + ((mu_t - prior_mu) / sig) ** 2).sum()
@@ -41,15 +48,18 @@ def elbo_step(layout, mu, rho, eps_list, branch_in, trunk_grid, y_grid, beta, tr
     for eps in eps_list:
         W = mu_t + torch.tensor(np.asarray(eps, np.float64)) * sig
         pred = _mlp(W, br, xb, act) @ _mlp(W, tr, ft, act).T + W[0]
-        nll = F.gaussian_nll_loss(pred, y, torch.full_like(y, noise_var), reduction="mean")
+        nll = F.gaussian_nll_loss(pred, y, _var(y, noise_var, lv), reduction="mean")
         total = total + nll * train_size + beta * kl
     loss = total / len(eps_list)
-    gm, gr = torch.autograd.grad(loss, (mu_t, rho_t))
-    return float(loss.detach()), gm.numpy(), gr.numpy()
+    if lv is None:
+        gm, gr = torch.autograd.grad(loss, (mu_t, rho_t))
+        return float(loss.detach()), gm.numpy(), gr.numpy()
+    gm, gr, gl = torch.autograd.grad(loss, (mu_t, rho_t, lv))
+    return float(loss.detach()), gm.numpy(), gr.numpy(), float(gl)
 
 
 def eval_loss(layout, mu, rho, branch_in, trunk_grid, y_grid, beta, size, noise_var=1.0, prior_mu=0.0,
-              prior_sigma=0.1, act="tanh"):
+              prior_sigma=0.1, act="tanh", log_var=None):
     """validate_model's loss (eval mode: W = mu) and metrics.mse, float64."""
     br, tr, D = layout
     W = torch.tensor(np.asarray(mu, np.float64))
@@ -60,5 +70,6 @@ def eval_loss(layout, mu, rho, branch_in, trunk_grid, y_grid, beta, size, noise_
     ft = torch.tensor(trunk_feats_np(trunk_grid))
     y = torch.tensor(np.asarray(y_grid, np.float64))
     pred = _mlp(W, br, xb, act) @ _mlp(W, tr, ft, act).T + W[0]
-    nll = F.gaussian_nll_loss(pred, y, torch.full_like(y, noise_var), reduction="mean")
+    lv = None if log_var is None else torch.tensor(float(log_var), dtype=torch.float64)
+    nll = F.gaussian_nll_loss(pred, y, _var(y, noise_var, lv), reduction="mean")
     return float(nll * size + beta * kl), float(torch.mean((pred - y) ** 2))

@@ -493,11 +493,12 @@ def _flat(named, kind):
     return torch.cat(parts).numpy()
 
 
-def vi_cases(out):
+def vi_cases(out, only=None):
     """The reference's own train_model / validate_model / metrics.mse on a small Bayesian DeepONet: init
     (after torch.manual_seed), one training step's loss and mu / rho gradients with num_ens weight draws,
     the eval-mode validation loss and MSE. Batches: B functions, each with a permutation of the whole trunk
-    grid (BurgersDataSet with p = P, utils.py:39-41)."""
+    grid (BurgersDataSet with p = P, utils.py:39-41). learn_noise cases follow main_VI_deeponet.py:154-156: a
+    trainable log-variance drawn with torch.randn(1) after the model, ELBO(True, 0) (metrics.py:21-25)."""
     clash = ("util", "utils", "config", "config_sens", "model", "my_make_func", "sensitivity", "metrics",
              "bayesian_model", "main_VI_deeponet", "layers", "layers.BBB", "layers.BBB.BBBLinear", "layers.BBB.BBBConv",
              "layers.BBB_LRT", "layers.BBB_LRT.BBBLinear", "layers.BBB_LRT.BBBConv", "layers.misc")
@@ -509,14 +510,21 @@ def vi_cases(out):
                                  seed=51, rho0=(-5, 0.1)),
         "vi_deeponet_relu": dict(width=10, in_b=5, depth=4, act="relu", B=3, nt=4, nx=5, num_ens=3, beta="Standard",
                                  seed=52, rho0=(-3, 0.1)),
+        "vi_deeponet_noise": dict(width=12, in_b=7, depth=3, act="tanh", B=4, nt=5, nx=6, num_ens=2, beta=0.5,
+                                  seed=53, rho0=(-5, 0.1), learn_noise=True),
     }
     for name, c in cases.items():
+        if only is not None and name not in only:
+            continue
+        learn = c.get("learn_noise", False)
         priors = {"prior_mu": 0, "prior_sigma": 0.1, "posterior_mu_initial": (0, 0.1), "posterior_rho_initial": c["rho0"]}
         torch.manual_seed(c["seed"])
         model = BM.Bayesian_DeepONet(priors, c["width"], c["width"], c["in_b"], 5, c["depth"], c["depth"], c["width"],
                                      c["act"], 0, 0, impose_bc=True)
         named = {n: p.detach().clone() for n, p in model.named_parameters()}
         mu0, rho0 = _flat(named, "mu"), _flat(named, "rho")
+        noise = torch.nn.Parameter(torch.randn((1))) if learn else torch.tensor(1.0)
+        noise0 = noise.detach().clone()
         rng = np.random.default_rng(c["seed"])
         P = c["nt"] * c["nx"]
         t = np.linspace(0.0, 1.0, c["nt"], dtype=np.float32)
@@ -529,13 +537,14 @@ def vi_cases(out):
                  torch.from_numpy(np.stack([grid[perms[b]] for b in range(c["B"])])),
                  torch.from_numpy(np.stack([y_grid[b, perms[b]] for b in range(c["B"])])))
         train_size = c["B"] * P * 10
-        loss = MET.ELBO(False, 0)
+        loss = MET.ELBO(learn, 0)
         rec = _GradRecorder(model)
         torch.manual_seed(c["seed"] + 1000)
         l_train = M.train_model([batch], model, loss, rec, train_size, 1, c["num_ens"], c["beta"],
-                                noise_param=torch.tensor(1.0))
+                                noise_param=noise)
         g_mu, g_rho = _flat(rec.grads, "mu"), _flat(rec.grads, "rho")
-        l_val = M.validate_model([batch], model, loss, train_size, c["beta"], 1, noise_param=torch.tensor(1.0))
+        g_noise = noise.grad.detach().clone() if learn else torch.zeros(1)
+        l_val = M.validate_model([batch], model, loss, train_size, c["beta"], 1, noise_param=noise)
         m_val = MET.mse([batch], model, 0, "Burgers")
         with torch.no_grad():
             _, kl0 = model(batch[0], batch[1])      # eval mode after validate_model: W = mu
@@ -544,7 +553,9 @@ def vi_cases(out):
                  activation=c["act"], prior_rho0=np.array(c["rho0"], np.float64), seed=c["seed"], mu0=mu0, rho0=rho0,
                  branch_in=branch, trunk_grid=grid, perms=perms, y_grid=y_grid, train_size=train_size,
                  num_ens=c["num_ens"], beta=str(c["beta"]), loss_train=np.float64(l_train), grad_mu=g_mu,
-                 grad_rho=g_rho, loss_val=np.float64(l_val), mse_val=np.float64(m_val), kl0=np.float64(float(kl0)))
+                 grad_rho=g_rho, loss_val=np.float64(l_val), mse_val=np.float64(m_val), kl0=np.float64(float(kl0)),
+                 learn_noise=learn, noise0=noise0.numpy().reshape(-1).astype(np.float32),
+                 grad_noise=g_noise.numpy().reshape(-1).astype(np.float32))
         print(name, "D", mu0.size, "train loss", l_train, "val loss", l_val, "mse", m_val)
 
 
@@ -553,6 +564,9 @@ if __name__ == "__main__":
     torch.set_num_threads(8)
     if "--vi-only" in sys.argv:
         vi_cases(HERE)
+        sys.exit(0)
+    if "--vi-noise-only" in sys.argv:
+        vi_cases(HERE, only=("vi_deeponet_noise",))
         sys.exit(0)
     if "--sens-only" in sys.argv:
         sensitivity_cases(HERE)

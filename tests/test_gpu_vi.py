@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from oracle.vi_ref import elbo_step
-from vi_cases import VI_CASES, GradRecorder, make_model, rel_norm, vi_case
+from vi_cases import NOISE_CASE, VI_CASES, GradRecorder, make_model, rel_norm, vi_case
 
 pytestmark = pytest.mark.gpu
 
@@ -29,6 +29,37 @@ def test_train_validate_mse_match_reference(name, cuda_device):
         lv = validate_model([c.batch], m, ELBO(), c.train_size, c.beta, 1, engines=eng)
         assert lv == pytest.approx(float(c.g["loss_val"]), rel=2e-5)
         assert mse([c.batch], m, engines=eng) == pytest.approx(float(c.g["mse_val"]), rel=1e-4)
+    finally:
+        eng.close()
+
+
+def test_learn_noise_train_validate_match_reference(cuda_device):
+    """learn_noise (noise_type 0): the trainable log-variance through train_model / validate_model -- loss and the
+    mu / rho / log-variance gradients against the reference's own step (tests/golden/vi_deeponet_noise.npz)."""
+    from vihmc.vi import ELBO, BatchEngines, train_model, validate_model
+    c = vi_case(NOISE_CASE)
+    m = make_model(c)
+    noise = torch.nn.Parameter(torch.randn((1)).to(cuda_device))
+    assert np.array_equal(noise.detach().cpu().numpy(), c.g["noise0"])
+    m = m.to(cuda_device)
+    eng = BatchEngines(m.spec, c.g["trunk_grid"], 1.0, c.num_ens, cuda_device)
+    try:
+        rec = GradRecorder(m)
+        torch.manual_seed(c.seed + 1000)
+        loss = ELBO(True, 0)
+        lt = train_model([c.batch], m, loss, rec, c.train_size, 1, c.num_ens, c.beta, noise_param=noise, engines=eng)
+        assert lt == pytest.approx(float(c.g["loss_train"]), rel=2e-5)
+        assert rel_norm(rec.grads[0].cpu().numpy(), c.g["grad_mu"]) < 2e-4
+        assert rel_norm(rec.grads[1].cpu().numpy(), c.g["grad_rho"]) < 2e-4
+        assert float(noise.grad) == pytest.approx(float(c.g["grad_noise"][0]), rel=2e-3)
+        lv = validate_model([c.batch], m, loss, c.train_size, c.beta, 1, noise_param=noise, engines=eng)
+        assert lv == pytest.approx(float(c.g["loss_val"]), rel=2e-5)
+        with pytest.raises(ValueError):             # learn_noise needs variance-1 plans
+            bad = BatchEngines(m.spec, c.g["trunk_grid"], 2.0, c.num_ens, cuda_device)
+            try:
+                validate_model([c.batch], m, loss, c.train_size, c.beta, 1, noise_param=noise, engines=bad)
+            finally:
+                bad.close()
     finally:
         eng.close()
 
@@ -123,6 +154,13 @@ def test_run_end_to_end_writes_artefacts(tmp_path, cuda_device):
     torch.manual_seed(0)
     model, metrics = vi.run(cfg, tl, vl, 16 * P, 8 * P, grid, device=cuda_device, log=lambda s: None)
     assert len(metrics) == 2 and all(np.isfinite(m).all() for m in np.asarray(metrics))
+    cfg_n = configs.load("burgers_vi", epochs=2, N_train=16, N_valid=8, batch_size=8, num_ens=2, width_branch=20,
+                         width_trunk=20, output_neurons=20, branch_depth=3, trunk_depth=3, in_branch=11,
+                         learn_noise=True, save_loc=None)
+    cfg_n.p = P
+    _, mn = vi.run(cfg_n, tl, vl, 16 * P, 8 * P, grid, device=cuda_device, log=lambda s: None)
+    mn = np.asarray(mn)
+    assert mn.shape == (2, 5) and np.isfinite(mn).all() and (mn[:, 4] > 0).all()      # 5th entry: exp(noise_param)
     mu = torch.load(f"{tmp_path}/means_flattened_t", weights_only=True)
     sd = torch.load(f"{tmp_path}/stds_flattened_t", weights_only=True)
     assert mu.shape == (spec.n_params,) and sd.shape == mu.shape and bool((sd > 0).all())

@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from oracle.vi_ref import elbo_step, eval_loss
-from vi_cases import VI_CASES, make_model, rel_norm, vi_case
+from vi_cases import NOISE_CASE, VI_CASES, make_model, rel_norm, vi_case
 
 
 @pytest.mark.parametrize("name", VI_CASES)
@@ -70,3 +70,47 @@ def test_elbo_module_matches_formula():
     v = ELBO()(pred, y, kl, 0.5, 100, torch.tensor(2.0))
     ref = 100 * torch.mean(0.5 * (np.log(2.0) + (pred - y) ** 2 / 2.0)) + 0.5 * kl
     assert float(v) == pytest.approx(float(ref), rel=1e-6)
+
+
+def test_learn_noise_case_matches_reference():
+    """learn_noise, noise_type 0 (main_VI_deeponet.py:154-156, metrics.py:21-25): the log-variance draw after the
+    model, and the float64 oracle's loss and mu / rho / log-variance gradients with our weight-noise draws, against
+    the reference's own train_model / validate_model (tests/golden/vi_deeponet_noise.npz)."""
+    from vihmc.vi import get_beta
+    c = vi_case(NOISE_CASE)
+    assert bool(c.g["learn_noise"])
+    m = make_model(c)
+    noise0 = torch.randn((1))
+    assert np.array_equal(noise0.numpy(), c.g["noise0"])
+    torch.manual_seed(c.seed + 1000)
+    eps = [m.draw_eps().numpy() for _ in range(c.num_ens)]
+    beta = get_beta(0, 1, c.beta, None, None)
+    lv = float(c.g["noise0"][0])
+    loss, gm, gr, gl = elbo_step(c.layout, c.g["mu0"], c.g["rho0"], eps, c.g["branch_in"], c.g["trunk_grid"],
+                                 c.g["y_grid"], beta, c.train_size, act=c.act, log_var=lv)
+    assert loss == pytest.approx(float(c.g["loss_train"]), rel=2e-6)
+    assert rel_norm(gm, c.g["grad_mu"]) < 1e-5
+    assert rel_norm(gr, c.g["grad_rho"]) < 1e-5
+    assert gl == pytest.approx(float(c.g["grad_noise"][0]), rel=1e-4)
+    lval, _ = eval_loss(c.layout, c.g["mu0"], c.g["rho0"], c.g["branch_in"], c.g["trunk_grid"], c.g["y_grid"], beta,
+                        c.train_size, act=c.act, log_var=lv)
+    assert lval == pytest.approx(float(c.g["loss_val"]), rel=2e-6)
+
+
+def test_elbo_module_learn_noise_and_unsupported_head():
+    from vihmc.vi import ELBO, Bayesian_DeepONet, _check_loss, calculate_kl
+    torch.manual_seed(1)
+    pred, y = torch.randn(3, 7), torch.randn(3, 7)
+    kl = calculate_kl(0, 0.1, torch.randn(5), torch.rand(5) + 0.05)
+    lv = torch.tensor([0.3], requires_grad=True)
+    v = ELBO(True, 0)(pred, y, kl, 0.5, 100, lv)
+    ref = 100 * torch.mean(0.5 * (0.3 + (pred - y) ** 2 / np.exp(0.3))) + 0.5 * kl
+    assert float(v) == pytest.approx(float(ref), rel=1e-6)
+    v.backward()
+    dref = 100 * float(torch.mean(0.5 * (1 - (pred - y) ** 2 / np.exp(0.3))))
+    assert float(lv.grad) == pytest.approx(dref, rel=1e-5)
+    with pytest.raises(NotImplementedError):
+        _check_loss(ELBO(True, 1))
+    with pytest.raises(NotImplementedError):
+        Bayesian_DeepONet({"prior_mu": 0, "prior_sigma": 0.1, "posterior_mu_initial": (0, 0.1),
+                           "posterior_rho_initial": (-5, 0.1)}, 8, 8, 3, 5, 3, 3, 10, "tanh", 1, 2)

@@ -21,8 +21,13 @@ layer's W_eps then bias_eps, the trunk layers, then the output bias; layers/BBB/
 bayesian_model.py:100), so identical seeds give identical draws. Batches carry the whole trunk grid per
 function (config.py:30, p = 10201): the NLL is a sum over points, so each item's point permutation
 (utils.py:39-41) is undone by mapping its points onto the plan's grid order.
-Not supported: ``noise_type`` 1 (heteroscedastic head) and ``learn_noise`` (trainable noise variance),
-both off in the reference config (config.py:45-51); per-item trunk subsets (p < P) in training.
+``learn_noise`` with ``noise_type`` 0 (main_VI_deeponet.py:154-156, metrics.py:21-25; off in the reference
+config, config.py:45-51): the NLL variance is exp(noise_param), one trainable scalar. The plans are then built
+with variance 1, so one evaluation gives 0.5 sum r^2 per draw and its gradient; the log-variance enters in torch
+(``elbo_loss``). Not supported: ``noise_type`` 1 (heteroscedastic head, bayesian_model.py:90-92) -- its
+einsum("bi,bi->b") takes 2-D branch and trunk outputs, so the reference itself cannot run it on the Burgers
+batches (3-D trunk output [B, p, W]); the Cone dataset it serves is out of scope. Per-item trunk
+subsets (p < P) in training.
 """
 from __future__ import annotations
 
@@ -70,8 +75,9 @@ def get_beta(batch_idx, m, beta_type, epoch, num_epochs):
 
 
 class ELBO(nn.Module):
-    """metrics.py:13-31: gaussian_nll_loss(mean) * train_size + beta * kl on given predictions. The
-    training loop evaluates the same quantity through the engine (``elbo_loss``)."""
+    """metrics.py:13-31: gaussian_nll_loss(mean) * train_size + beta * kl on given predictions (learn_noise:
+    noise_param is the log-variance). The training loop evaluates the same quantity through the engine
+    (``elbo_loss``)."""
 
     def __init__(self, learn_noise=False, noise_type=0):
         super().__init__()
@@ -81,7 +87,9 @@ class ELBO(nn.Module):
     def forward(self, prediction, target, kl, beta, train_size, noise_param=None):
         assert not target.requires_grad
         if self.learn_noise:
-            raise NotImplementedError("learn_noise (trainable noise variance) is not supported")
+            assert noise_param is not None
+            var = torch.exp(noise_param) * torch.ones_like(target) if self.noise_type == 0 else torch.exp(noise_param)
+            return F.gaussian_nll_loss(prediction, target, var, reduction="mean") * train_size + beta * kl
         return F.gaussian_nll_loss(prediction.reshape(target.shape), target, noise_param * torch.ones_like(target),
                                    reduction="mean") * train_size + beta * kl
 
@@ -141,7 +149,8 @@ class Bayesian_DeepONet(nn.Module):
                  depth_trunk=4, output_neurons=20, activation="relu", noise_type=0, noise_neurons=0, impose_bc=True):
         super().__init__()
         if noise_type:
-            raise NotImplementedError("noise_type 1 (heteroscedastic head) is not supported")
+            raise NotImplementedError("noise_type 1 (heteroscedastic head, bayesian_model.py:90-92) is not supported: "
+                                      "the reference's einsum('bi,bi->b') cannot take the Burgers trunk output")
         if activation not in ("relu", "tanh"):
             raise ValueError("activation should be relu or tanh")
         self.neurons_branch, self.neurons_trunk = neurons_branch, neurons_trunk
@@ -313,10 +322,21 @@ class BatchEngines:
 # ------------------------------------------------------------------------------------------------
 # training / validation (main_VI_deeponet.py)
 # ------------------------------------------------------------------------------------------------
-def elbo_loss(model: Bayesian_DeepONet, engines: BatchEngines, batch, beta, train_size, num_ens=1, sample=True):
+def _nll_var(log_var):
+    """exp(log_var) with F.gaussian_nll_loss's variance clamp (eps 1e-6, applied to the value only)."""
+    v = torch.exp(log_var).clone()
+    with torch.no_grad():
+        v.clamp_(min=1e-6)
+    return v
+
+
+def elbo_loss(model: Bayesian_DeepONet, engines: BatchEngines, batch, beta, train_size, num_ens=1, sample=True,
+              log_var=None):
     """sum_j [NLL_mean(pred_j, y) * train_size + beta * kl] / num_ens for one batch (main_VI_deeponet.py:67-75),
     a torch scalar with gradients to the model's mu / rho; the network part is one engine evaluation of all
-    num_ens weight draws. ``sample=False`` is eval mode (W = mu, one evaluation)."""
+    num_ens weight draws. ``sample=False`` is eval mode (W = mu, one evaluation). ``log_var`` (learn_noise): the
+    trainable log-variance; the engines then run at variance 1 and NLL_mean = 0.5 log v + (0.5 sum r^2) / (v N P)
+    (metrics.py:23-25), differentiable in log_var as well."""
     eng = engines.load(batch)
     dev = eng.device
     mu = model.mu_flat()
@@ -326,26 +346,45 @@ def elbo_loss(model: Bayesian_DeepONet, engines: BatchEngines, batch, beta, trai
     else:
         num_ens = 1
         W = mu[None]
-    nll = _EngineNLL.apply(W, eng, float(train_size) / float(eng.N * eng.P))
+    if log_var is None:
+        nll = _EngineNLL.apply(W, eng, float(train_size) / float(eng.N * eng.P))
+    else:
+        if engines.tau_out != 1.0:
+            raise ValueError("learn_noise needs engines built with variance 1 (BatchEngines(..., 1.0, ...))")
+        half_sq = _EngineNLL.apply(W, eng, 1.0)              # 0.5 sum r^2 per draw
+        v = _nll_var(log_var.to(dev)).reshape(())
+        nll = float(train_size) * (0.5 * torch.log(v) + half_sq / (v * float(eng.N * eng.P)))
     return (nll + beta * model.kl()).sum() / num_ens
 
 
 def _check_loss(loss):
-    if getattr(loss, "learn_noise", False) or getattr(loss, "noise_type", 0):
-        raise NotImplementedError("learn_noise / noise_type 1 are not supported")
+    if getattr(loss, "noise_type", 0):
+        raise NotImplementedError("noise_type 1 (heteroscedastic head) is not supported")
+
+
+def _log_var(loss, noise_param):
+    """The trainable log-variance when the loss learns the noise (metrics.py:21-25), else None (fixed variance =
+    the engines' tau_out)."""
+    if not getattr(loss, "learn_noise", False):
+        return None
+    if noise_param is None:
+        raise ValueError("learn_noise needs noise_param (the log-variance parameter)")
+    return noise_param
 
 
 def train_model(train_loader, model, loss, optimizer, train_size, num_batches, num_ens=1, beta_type=0.1, epoch=None,
                 num_epochs=None, noise_param=None, engines: Optional[BatchEngines] = None):
     """main_VI_deeponet.py:23-81. ``engines`` holds the plans (``BatchEngines(model.spec, grid, noise_param,
-    num_ens, device)``); the NLL variance is the engines' tau_out (noise_param of the reference)."""
+    num_ens, device)``); the NLL variance is the engines' tau_out (noise_param of the reference), or, with
+    ``loss.learn_noise``, exp(noise_param) (engines at variance 1; noise_param is then a trainable tensor)."""
     _check_loss(loss)
+    lv = _log_var(loss, noise_param)
     l_total = 0
     for i, batch_data in enumerate(train_loader):
         model.train()
         optimizer.zero_grad()
         beta = get_beta(i, num_batches, beta_type, epoch, num_epochs)
-        l = elbo_loss(model, engines, batch_data, beta, train_size, num_ens, sample=True)
+        l = elbo_loss(model, engines, batch_data, beta, train_size, num_ens, sample=True, log_var=lv)
         l_total += l.item()
         l.backward()
         optimizer.step()
@@ -357,12 +396,13 @@ def validate_model(valid_loader, model, loss, valid_size, beta_type, num_batches
                    engines: Optional[BatchEngines] = None):
     """main_VI_deeponet.py:84-127 (eval mode: W = mu)."""
     _check_loss(loss)
+    lv = _log_var(loss, noise_param)
     l_total = 0
     for i, batch_data in enumerate(valid_loader):
         model.eval()
         beta = get_beta(i, num_batches, beta_type, None, None)
         with torch.no_grad():
-            l = elbo_loss(model, engines, batch_data, beta, valid_size, 1, sample=False)
+            l = elbo_loss(model, engines, batch_data, beta, valid_size, 1, sample=False, log_var=lv)
         l_total += l.item()
     l_total = l_total / (i + 1)
     return l_total
@@ -411,6 +451,8 @@ def export_posterior(model: Bayesian_DeepONet, save_loc: str, uid: str):
 def run(cfg, train_loader, valid_loader, tr_size, vld_size, trunk_grid, device=None, log=print):
     """main_VI_deeponet.py:130-203 without the checkpoint pickles: Adam + ReduceLROnPlateau over cfg.epochs;
     the posterior of the best validation epoch is exported (``export_posterior``) when cfg.save_loc is set.
+    learn_noise (noise_type 0): a trainable log-variance drawn after the model (torch.randn(1), lines 154-156),
+    optimised with it; each epoch's metrics then carry exp(noise_param) as a fifth entry (lines 173-175).
     Returns (model, train_metrics)."""
     dev = _op._device("cuda" if device is None else device)
     model = Bayesian_DeepONet(cfg.priors, cfg.width_branch, cfg.width_trunk, cfg.in_branch, cfg.in_trunk,
@@ -419,10 +461,16 @@ def run(cfg, train_loader, valid_loader, tr_size, vld_size, trunk_grid, device=N
                               impose_bc=cfg.dataset == "Burgers").to(dev)
     loss = ELBO(cfg.learn_noise, cfg.noise_type)
     _check_loss(loss)
-    optimizer = torch.optim.Adam(model.parameters(), lr=cfg.lr_start)
-    noise_param = float(cfg.noise_param)
+    learn = bool(cfg.learn_noise) and cfg.noise_type == 0
+    if learn:
+        noise_param = Parameter(torch.randn((1)).to(dev))
+        optimizer = torch.optim.Adam(list(model.parameters()) + [noise_param], lr=cfg.lr_start)
+        tau = 1.0
+    else:
+        optimizer = torch.optim.Adam(model.parameters(), lr=cfg.lr_start)
+        noise_param = tau = float(cfg.noise_param)
     lr_sched = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, patience=cfg.lr_patience, min_lr=1e-5)
-    engines = BatchEngines(model.spec, trunk_grid, noise_param, cfg.num_ens, dev)
+    engines = BatchEngines(model.spec, trunk_grid, tau, cfg.num_ens, dev)
     num_tr, num_val = len(train_loader), len(valid_loader)
     train_metrics = []
     best = float("inf")
@@ -435,9 +483,10 @@ def run(cfg, train_loader, valid_loader, tr_size, vld_size, trunk_grid, device=N
             lr_sched.step(vl)
             tm = mse(train_loader, model, engines=engines)
             vm = mse(valid_loader, model, engines=engines)
-            train_metrics.append([tl, vl, tm, vm])
+            alea_unc = float(torch.exp(noise_param.detach()).item()) if learn else 0
+            train_metrics.append([tl, vl, tm, vm, alea_unc] if learn else [tl, vl, tm, vm])
             log(f"Epoch: {epoch} \tTraining Loss: {tl:.6f} \tValidation Loss: {vl:.6f} \tTraining MSE: {tm:.6f} "
-                f"\tValidation MSE: {vm:.6f}")
+                f"\tValidation MSE: {vm:.6f} \tNoise: {alea_unc:.6f}")
             if vl <= best:
                 best = vl
                 if getattr(cfg, "save_loc", None):
