@@ -363,7 +363,7 @@ def main():
 
     from vihmc.data import deeponet_problem
     from vihmc.dist import gather_ragged_pool, max_over_ranks
-    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.engine import DeepONetEngine, ShaderClock, trunk_features
     from vihmc.layout import DeepONetSpec
     from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner
 
@@ -392,13 +392,17 @@ def main():
     eng.timing(-1, False)
     dom_cls = max(KCLASS, key=lambda k: cal.get(KCLASS[k][0], {}).get("share_of_eval", -1.0))
     ev.n_grad = 0
+    eng.option("gram_evals", 0)                     # reset the plan's evaluation counters (both forms)
+    clock = ShaderClock(dev)
     eng.timing(dom_cls, True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    clock.start()
     for _ in range(args.steps):
         runner.step()
+    clock.stop()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -406,6 +410,8 @@ def main():
     k_ms, k_n = eng.timing_class(dom_cls)
     eng.timing(-1, False)
     grad_evals = ev.n_grad
+    n_calls, n_gram = eng.get_option("grad_evals"), eng.get_option("gram_evals")
+    sclk = clock.mhz()
     T = max_over_ranks(t1 - t0, dev)
 
     extra = {}
@@ -442,6 +448,10 @@ def main():
     avg_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = flops_launch / avg_s / 1e12 if k_n else None
     evals_per_s = world * grad_evals / T
+    gram_frac = n_gram / max(n_calls, 1)
+    fl_res = spec.flops_per_grad_eval(prob.N, prob.P)
+    fl_gram = fl_res - fl["contract_a"] - fl["contract_b"] + fl["gram"]
+    flops_performed = (1.0 - gram_frac) * fl_res + gram_frac * fl_gram
     form_key = {"contract_a": "contract_bf16x6", "contract_b": "contract_bf16x6", "bwd": "bwd_bf16x6",
                 "fwd": "fwd_bf16x6", "gram": "contract_bf16x6"}[key]
     bf = eng.get_option(form_key)
@@ -469,6 +479,18 @@ def main():
         "eval_tflops_algorithmic": evals_per_s * spec.flops_per_grad_eval(prob.N, prob.P) / 1e12,
         "eval_flops_basis": "the reference's residual-form FLOPs per gradient evaluation (the inner leapfrog steps run the "
                             "Gram form, which does fewer: layout.flops_gram)",
+        "eval_tflops_performed": evals_per_s * flops_performed / 1e12,
+        "eval_flops_performed_basis": "FLOPs of the forms that ran: residual-form evaluations at "
+                                      "flops_per_grad_eval, Gram-form evaluations with the contraction at flops_gram",
+        "gram_eval_fraction": gram_frac,
+        "gram_eval_fraction_basis": f"{n_gram} of {n_calls} gradient-evaluation calls in the timed region ran the "
+                                    "Gram form (plan counters grad_evals / gram_evals)",
+        "sclk_mhz": float(np.mean(list(sclk.values()))) if sclk else None,
+        "sclk_mhz_by_xcd": {str(k): round(v, 1) for k, v in sclk.items()},
+        "sclk_basis": "average shader clock over the timed region: d s_memtime / d s_memrealtime x 100 MHz per XCD "
+                      "(vihmc_clock_stamp before and after the region, MI355X_MICROARCH.md DVFS item 6); nominal 2400",
+        "roofline_frac_at_sclk": ((achieved / (peak * float(np.mean(list(sclk.values()))) / 2400.0))
+                                  if (achieved and sclk) else None),
         "accept_rate": acc_rate,
         "roofline": {"kernel": f"{kname}: {what}", "selected_as": "largest share of the evaluation's GPU time "
                      f"({cal[key]['share_of_eval']:.3f}, HIP-event calibration before the timed region)",

@@ -115,7 +115,7 @@ int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float
 
 /* d log p / d theta_c only (no log-prob): the leapfrog's inner gradient evaluations (hamiltorch's params_grad
  * between the position updates, SURVEY.md App. A.2, whose log-prob value is discarded). DeepONet plans with
- * width 100 and C >= the plan option "gram_min_chains" use the Gram-form contraction (vihmc_gram.hip: no N x P
+ * width 100 and max_chains >= the plan option "gram_min_chains" use the Gram-form contraction (vihmc_gram.hip: no N x P
  * residual, plan option "gram"); vihmc_trajectory uses the same path for its inner steps. */
 int vihmc_grad(vihmc_plan* p, const float* theta, int C, float* grad, void* stream);
 
@@ -211,12 +211,21 @@ int vihmc_graph_enable(vihmc_plan* p, int on);
  * dW, db of layers with 100 outputs); its default (environment VIHMC_BWD_BF16) also sizes the backward
  * row chunks at plan creation. "graph" = vihmc_graph_enable. "gram" (default 1): gradient-only DeepONet
  * evaluations (vihmc_grad, the inner steps of vihmc_trajectory) in Gram form; "gram_min_chains" (default 4): the
- * smallest chain count that uses it (default 4: below it the residual form's split sweeps fill the chip better). Changing an option drops captured graphs.
+ * smallest plan max_chains that uses it (default 4: below it the residual form's split sweeps fill the chip better;
+ * decided per plan, so a chain's trajectory does not depend on the call's chain count). "grad_evals" / "gram_evals"
+ * (read: gradient-evaluation calls since creation / of which in Gram form; set: any value resets both; direct
+ * launches only). Changing an option drops captured graphs.
  * Returns nonzero for an unknown key. */
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value);
 /* Current value of an option (contract_bf16x6 reads 1 only where the bf16x6 contraction applies,
  * i.e. width 100; graph reads -1 while it follows VIHMC_GRAPH). */
 int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value);
+
+/* Measurement (new; no reference counterpart): enqueue on `stream` one stamp of the shader clock. out is DEVICE
+ * memory [64][3] uint64: per one-wave workgroup (8 per XCD) its XCD id, s_memtime (shader-clock ticks) and
+ * s_memrealtime (100 MHz ticks). Two stamps around a timed region give each XCD's average shader clock over it:
+ * (d memtime / d memrealtime) x 100 MHz (bench.py: "sclk_mhz"). */
+int vihmc_clock_stamp(uint64_t* out, void* stream);
 
 void        vihmc_plan_destroy(vihmc_plan* p);
 const char* vihmc_last_error(void);

@@ -4,5 +4,5 @@
 set -e
 for cfg in "$@"; do
   echo "== $cfg"
-  env $cfg timeout -k 10 120 python vi-hmc_amd/scripts/probe_eval.py --chains 16 --iters 30 2>&1 | grep "C="
+  env $cfg timeout -k 10 120 python profiles/scripts/probes/probe_eval.py --chains 16 --iters 30 2>&1 | grep "C="
 done

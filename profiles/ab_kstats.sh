@@ -12,7 +12,7 @@ export VIHMC_ALLOW_DIAG=1   # timing-only ablation variants are timed here, neve
 for f in "$@"; do
   if [ "$f" = base ]; then unset VIHMC_LIB; else export VIHMC_LIB=$ROOT/_var/$f; fi
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$f -o s -- \
-      python3 $ROOT/vi-hmc_amd/scripts/probe_eval.py --chains 16 --iters 20 > $O/$f.log 2>&1
+      python3 $ROOT/profiles/scripts/probes/probe_eval.py --chains 16 --iters 20 > $O/$f.log 2>&1
   echo "== $f: $(grep 'C= 16' $O/$f.log)" >> $O/summary.txt
   python3 $ROOT/profiles/kstats.py $(ls $O/$f/*kernel_stats.csv | head -1) 8 >> $O/summary.txt
 done

@@ -4,5 +4,5 @@
 set -e
 for f in "$@"; do
   echo "== $f"
-  VIHMC_LIB=$GRAFT_REPO_ROOT/_var/$f timeout -k 10 120 python vi-hmc_amd/scripts/probe_eval.py --chains 16 --iters 30 2>&1 | grep "C="
+  VIHMC_LIB=$GRAFT_REPO_ROOT/_var/$f timeout -k 10 120 python profiles/scripts/probes/probe_eval.py --chains 16 --iters 30 2>&1 | grep "C="
 done

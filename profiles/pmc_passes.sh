@@ -6,7 +6,7 @@ set -e
 NAME=${1:-pmc}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
-P="python3 $ROOT/vi-hmc_amd/scripts/probe_eval.py --chains 16 --iters 3"
+P="python3 $ROOT/profiles/scripts/probes/probe_eval.py --chains 16 --iters 3"
 run() {
     local tag=$1; shift
     timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv --pmc "$@" -d "$ROOT/gpurun_out/${NAME}_$tag" -o p -- $P \

@@ -8,6 +8,6 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_sampler.py tests/test_gpu_s
     --timeout 300 --timeout-method thread > gpurun_out/${TAG}_bnn_tests.txt 2>&1 || exit 1
 for rep in 1 2; do
   for kv in "$@"; do
-    env $kv timeout -k 10 120 python vi-hmc_amd/scripts/probe_bnn.py --tag "$kv" >> gpurun_out/${TAG}_bnn_ab.txt 2>/dev/null || exit 1
+    env $kv timeout -k 10 120 python profiles/scripts/probes/probe_bnn.py --tag "$kv" >> gpurun_out/${TAG}_bnn_ab.txt 2>/dev/null || exit 1
   done
 done

@@ -4,7 +4,7 @@ TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/${TAG}_ab.txt
 : > $O
-P=$ROOT/vi-hmc_amd/scripts/probe_classes.py
+P=$ROOT/profiles/scripts/probes/probe_classes.py
 for rep in 1 2; do
   for v in new "$@"; do
     L=""; [ "$v" != new ] && L=$ROOT/_ab/$v.so

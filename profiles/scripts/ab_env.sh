@@ -5,7 +5,7 @@ TAG=$1; shift
 mkdir -p gpurun_out
 for rep in 1 2; do
   for kv in "$@"; do
-    env $kv timeout -k 10 120 python vi-hmc_amd/scripts/probe_classes.py --chains 16 --iters 30 --tag "$kv" \
+    env $kv timeout -k 10 120 python profiles/scripts/probes/probe_classes.py --chains 16 --iters 30 --tag "$kv" \
         >> gpurun_out/${TAG}_ab.txt 2>/dev/null || exit 1
   done
 done

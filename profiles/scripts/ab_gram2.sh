@@ -5,8 +5,8 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/${TAG}_ab.txt
 : > $O
 for rep in 1 2 3; do
-  timeout -k 10 120 python3 $ROOT/vi-hmc_amd/scripts/probe_classes.py --chains 16 --iters 20 --grad --tag new >> $O 2>&1 || exit 1
+  timeout -k 10 120 python3 $ROOT/profiles/scripts/probes/probe_classes.py --chains 16 --iters 20 --grad --tag new >> $O 2>&1 || exit 1
   for v in "$@"; do
-    VIHMC_LIB=$ROOT/_ab/$v.so timeout -k 10 120 python3 $ROOT/vi-hmc_amd/scripts/probe_classes.py --chains 16 --iters 20 --grad --tag $v >> $O 2>&1 || exit 1
+    VIHMC_LIB=$ROOT/_ab/$v.so timeout -k 10 120 python3 $ROOT/profiles/scripts/probes/probe_classes.py --chains 16 --iters 20 --grad --tag $v >> $O 2>&1 || exit 1
   done
 done

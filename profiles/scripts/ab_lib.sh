@@ -11,5 +11,5 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sc
     --timeout-method thread > gpurun_out/${TAG}_parity.txt 2>&1 && \
 bash profiles/scripts/ab_env.sh $TAG "${ARGS[@]}" && \
 bash profiles/scripts/ktrace.sh $TAG && \
-VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/bbstamp.so timeout -k 10 120 python vi-hmc_amd/scripts/diag/stamps_bwd.py \
+VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/bbstamp.so timeout -k 10 120 python profiles/scripts/diag/stamps_bwd.py \
     > gpurun_out/${TAG}_stamps.log 2>&1

@@ -7,7 +7,7 @@ for rep in 1 2 3; do
   for set in "$@"; do
     args=""
     for kv in $set; do args="$args --opt $kv"; done
-    timeout -k 10 120 python vi-hmc_amd/scripts/probe_classes.py --chains $C --iters 30 --tag "${set:-default}" $args \
+    timeout -k 10 120 python profiles/scripts/probes/probe_classes.py --chains $C --iters 30 --tag "${set:-default}" $args \
         >> gpurun_out/${TAG}_ab.txt 2>/dev/null || exit 1
   done
 done

@@ -3,5 +3,5 @@
 set -o pipefail
 TAG=$1
 bash profiles/scripts/ab_side_a.sh "$@" && \
-VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/cbstamp.so timeout -k 10 120 python vi-hmc_amd/scripts/diag/stamps_side_a.py \
+VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/cbstamp.so timeout -k 10 120 python profiles/scripts/diag/stamps_side_a.py \
     > gpurun_out/${TAG}_stamps_a.log 2>&1

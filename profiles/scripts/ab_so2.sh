@@ -4,8 +4,8 @@
 TAG=$1; C=$2; V=$3
 mkdir -p gpurun_out
 for rep in 1 2 3; do
-  timeout -k 10 120 python vi-hmc_amd/scripts/probe_classes.py --chains $C --iters 30 --tag new \
+  timeout -k 10 120 python profiles/scripts/probes/probe_classes.py --chains $C --iters 30 --tag new \
       >> gpurun_out/${TAG}_ab.txt 2>/dev/null || exit 1
-  VIHMC_LIB=$PWD/$V timeout -k 10 120 python vi-hmc_amd/scripts/probe_classes.py --chains $C --iters 30 --tag old \
+  VIHMC_LIB=$PWD/$V timeout -k 10 120 python profiles/scripts/probes/probe_classes.py --chains $C --iters 30 --tag old \
       >> gpurun_out/${TAG}_ab.txt 2>/dev/null || exit 1
 done

@@ -1,9 +1,9 @@
 """Per-layer difference between the whole-network backward (bwd_chain = 1) and the per-layer launches (0) of one
-single-chain full-parameter evaluation: python vi-hmc_amd/scripts/diag/chain_diff.py [--small]"""
+single-chain full-parameter evaluation: python profiles/scripts/diag/chain_diff.py [--small]"""
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "vi-hmc_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

@@ -1,9 +1,9 @@
 """Dump log p and its gradient of full-parameter Burgers evaluations (1 and 16 chains, seeded perturbations) from
 the library VIHMC_LIB points at, for a bitwise comparison between two builds:
 
-    VIHMC_LIB=a.so python vi-hmc_amd/scripts/diag/dump_eval.py out_a.npz
-    VIHMC_LIB=b.so python vi-hmc_amd/scripts/diag/dump_eval.py out_b.npz
-    python vi-hmc_amd/scripts/diag/dump_eval.py --compare out_a.npz out_b.npz
+    VIHMC_LIB=a.so python profiles/scripts/diag/dump_eval.py out_a.npz
+    VIHMC_LIB=b.so python profiles/scripts/diag/dump_eval.py out_b.npz
+    python profiles/scripts/diag/dump_eval.py --compare out_a.npz out_b.npz
 """
 import os
 import sys
@@ -21,7 +21,7 @@ if sys.argv[1] == "--compare":
     print("BITWISE EQUAL" if bad == 0 else "DIFFERENT")
     sys.exit(0 if bad == 0 else 1)
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "vi-hmc_amd"))
 import torch  # noqa: E402
 
 from vihmc.data import deeponet_problem  # noqa: E402

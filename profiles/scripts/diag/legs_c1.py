@@ -1,5 +1,5 @@
 """bench.py's one-chain side legs alone (config 4's split HMC and the one-chain VI-HMC DeepONet), repeated:
-python vi-hmc_amd/scripts/diag/legs_c1.py [reps]"""
+python profiles/scripts/diag/legs_c1.py [reps]"""
 import json
 import os
 import sys

@@ -1,7 +1,7 @@
 """Phase stamps of the bf16x6 layer backward (k_bwd_bf) from a -DBB_STAMP=1 variant build.
 
     make -C vi-hmc_amd OUT=$PWD/_var/bbstamp.so BUILD=$PWD/build/bbstamp EXTRA=-DBB_STAMP=1
-    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/bbstamp.so python vi-hmc_amd/scripts/diag/stamps_bwd.py
+    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/bbstamp.so python profiles/scripts/diag/stamps_bwd.py
 
 Every 16th trunk workgroup of the last launch with a dX part (layer 1) records per wave and 32-row sub-tile:
 s_memtime at the barrier exit, after staging the next sub-tile (split + LDS stores + the loads two ahead), and
@@ -13,7 +13,7 @@ import sys
 
 os.environ.setdefault("VIHMC_ALLOW_DIAG", "1")   # a stamp build is a diagnostic build
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "vi-hmc_amd"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

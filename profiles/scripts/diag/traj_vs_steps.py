@@ -2,7 +2,7 @@
 import os
 import sys
 
-sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."),
+sys.path[:0] = [os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "vi-hmc_amd"),
                 os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "tests")]
 import torch  # noqa: E402
 

@@ -8,4 +8,4 @@ for kv in "$@"; do
   export $kv
 done
 timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $ROOT/gpurun_out/${TAG}_kt -o t -- \
-    python3 $ROOT/vi-hmc_amd/scripts/probe_classes.py --chains 16 --iters 5 > $ROOT/gpurun_out/${TAG}_kt.log 2>&1
+    python3 $ROOT/profiles/scripts/probes/probe_classes.py --chains 16 --iters 5 > $ROOT/gpurun_out/${TAG}_kt.log 2>&1

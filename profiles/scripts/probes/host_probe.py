@@ -1,6 +1,6 @@
 """Host enqueue time vs GPU wall time per DeepONet evaluation (is a small-C evaluation launch-bound?)."""
 import os, sys, time
-sys.path.insert(0, os.path.join(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."), "vi-hmc_amd"))
+sys.path.insert(0, os.path.join(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", ".."), "vi-hmc_amd"))
 import numpy as np, torch
 from vihmc.data import deeponet_problem
 from vihmc.engine import DeepONetEngine, trunk_features

@@ -1,13 +1,13 @@
 """Single-chain evaluation latency with and without HIP-event timing / hipGraph replay (the round-1 note:
 C = 1 ran 2x faster under rocprofv3 than plain).
 
-    python vi-hmc_amd/scripts/probe_c1.py
+    python profiles/scripts/probes/probe_c1.py
 """
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "vi-hmc_amd"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -1,6 +1,6 @@
 """Per-kernel-class HIP-event times of the batched DeepONet evaluation (Burgers shapes), for A/B runs:
 
-    python vi-hmc_amd/scripts/probe_classes.py --chains 16 --iters 20 [--tag NAME]
+    python profiles/scripts/probes/probe_classes.py --chains 16 --iters 20 [--tag NAME]
 
 Prints one line: eval ms and per-class ms per evaluation (include/vihmc.h VIHMC_T_*), measured with every class
 timed (events add ~4 % to the evaluation), then the untimed wall per evaluation.
@@ -10,7 +10,7 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "vi-hmc_amd"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

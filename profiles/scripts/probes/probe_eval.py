@@ -1,13 +1,13 @@
 """Time one batched DeepONet log-prob+grad evaluation (Burgers shapes) on the GPU.
 
-    python vi-hmc_amd/scripts/probe_eval.py --chains 16 --iters 10
+    python profiles/scripts/probes/probe_eval.py --chains 16 --iters 10
 """
 import argparse
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "vi-hmc_amd"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

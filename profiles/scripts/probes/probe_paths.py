@@ -1,6 +1,6 @@
 """Time the paths next to the gradient evaluation (SURVEY §8 "next" rows) at Burgers shapes on the GPU.
 
-    python vi-hmc_amd/scripts/probe_paths.py [--chains 16] [--iters 10]
+    python profiles/scripts/probes/probe_paths.py [--chains 16] [--iters 10]
 
 * value-only log-prob (hamiltorch's Hamiltonian evaluations at the accept step) -- engine.logp
 * posterior-predictive forward (predict_model: out [C, N, P]) -- engine.forward
@@ -12,7 +12,7 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "vi-hmc_amd"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

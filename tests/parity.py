@@ -8,6 +8,7 @@ Quantities (all dimensionless):
   grad_norm_rel | ||g|| - ||ref|| | / ||ref||           (full-shape goldens keep the norm of the full gradient)
   pred_elem     max |out - ref| / max |ref|
   pos_maxabs    max |theta_gpu - theta_ref| over a sampler trajectory (absolute; the positions are O(0.1))
+  mom_maxabs    max |p_gpu - p_ref| (absolute; momenta are O(1))
   mean_rel_l2   relative L2 of the posterior-predictive mean (north-star criterion, < 1e-4 regardless)
 
 BOUNDS holds the tolerance of each (test, quantity): about 4x the largest error measured over the test's cases on
@@ -21,7 +22,7 @@ import os
 RECORDS = []
 
 LOOSE = {"logp_rel": 1e-3, "grad_relnorm": 2e-4, "grad_elem": 2e-3, "grad_norm_rel": 2e-4, "pred_elem": 1e-3,
-         "pos_maxabs": 1e-4, "mean_rel_l2": 1e-4}
+         "pos_maxabs": 1e-4, "mom_maxabs": 1e-4, "mean_rel_l2": 1e-4}
 
 # (test function, quantity) -> bound; measured r03 (see the module docstring)
 BOUNDS = {

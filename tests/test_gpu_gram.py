@@ -6,6 +6,9 @@ outputs Zb^ = [Z_b | 1], Zt^ = [Z_t | b0]) instead of forming G = gscale (S + b0
 autograd backward of my_make_func.py:79-82 + the Gaussian NLL (main_VI_HMC_burgers.py:157-163); its rounding
 differs from the residual form by the cancellation between Zb^ Gt and y Zt^, so it has its own recorded bounds.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -78,8 +81,9 @@ def test_gram_grad_refshape_vs_fp64_oracle(cuda_device):
 
 
 def test_gram_option_off_is_the_residual_form(cuda_device):
-    """gram = 0 (or fewer chains than gram_min_chains): vihmc_grad is bitwise the gradient of vihmc_logp_grad; the
-    default threshold is 4 chains."""
+    """gram = 0 (or a plan max_chains below gram_min_chains): vihmc_grad is bitwise the gradient of vihmc_logp_grad.
+    The form is decided per plan, not per call: a one-chain call on a 2-chain plan runs the Gram form too. The
+    evaluation counters count both forms."""
     c = deeponet_case("deeponet_refshape")
     eng = engine_for(c, 2, cuda_device)
     th = torch.tensor(np.stack(c.thetas[:2]), device=cuda_device)
@@ -90,9 +94,16 @@ def test_gram_option_off_is_the_residual_form(cuda_device):
     assert not eng.get_option("gram") & 2
     assert torch.equal(g, gr)
     eng.option("gram", 1)
-    g1 = eng.grad(th[:1])            # C = 1 < gram_min_chains (2 here)
+    eng.option("gram_evals", 0)
+    g1 = eng.grad(th[:1])            # C = 1 on a max_chains = 2 plan: still the Gram form
+    assert eng.get_option("gram") & 2
+    assert (eng.get_option("grad_evals"), eng.get_option("gram_evals")) == (1, 1)
+    parity.check("grad_relnorm", rel_norm(g1[0].cpu().numpy(), gr[0].cpu().numpy()), "C = 1 call, Gram form")
+    eng.option("gram_min_chains", 3)  # max_chains = 2 < 3: the residual form at every chain count
+    g1 = eng.grad(th[:1])
     assert not eng.get_option("gram") & 2
     assert torch.equal(g1, gr[:1])
+    assert (eng.get_option("grad_evals"), eng.get_option("gram_evals")) == (2, 1)
 
 
 def test_gram_after_set_data_and_trunk_rows(cuda_device):
@@ -170,3 +181,46 @@ def test_gram_loss_forms_vs_fp64_oracle(loss, tau, cuda_device):
         _, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, c.prior_mu, c.prior_sd,
                                 loss, tau)
         parity.check("grad_relnorm", rel_norm(g[i], rg), f"{loss} tau={tau} chain {i}")
+
+
+FIT_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gpurun_out", "gram_fit_table.json")
+
+
+@pytest.mark.parametrize("noise", [1e-2, 1e-3, 1e-4])
+def test_gram_precision_vs_fit(noise, cuda_device):
+    """The Gram form's cancellation (Zb^ Gt vs y Zt^) grows with |y| / |S - y|: full Burgers shape, theta AT the
+    teacher with the frozen weights at the teacher too (mu_noise = 0), so the residual is the data noise alone
+    (Sigma r^2 / Sigma y^2 ~ noise^2 / E y^2). Both forms against the fp64 oracle; the table of error vs fit goes to
+    gpurun_out/gram_fit_table.json (profiles/r04_gram_fit_table.json)."""
+    from vihmc.data import deeponet_problem
+    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.layout import DeepONetSpec
+    spec = DeepONetSpec()
+    p = deeponet_problem(seed=3, noise=noise, mu_noise=0.0)
+    th = p.teacher[p.grad_ind].astype(np.float32)
+    eng = DeepONetEngine(spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, 0.1, "NLL", 1.0,
+                         max_chains=2, device=cuda_device)
+    eng.option("gram_min_chains", 2)
+    tt = torch.tensor(np.stack([th, th]), device=cuda_device)
+    gg = eng.grad(tt)[0].cpu().numpy()
+    assert eng.get_option("gram") & 2
+    lp, gres = eng.logp_grad(tt)
+    gres = gres[0].cpu().numpy()
+    lay = deeponet_layout(spec.in_branch, spec.width_branch, spec.depth_branch, spec.in_trunk, spec.width_trunk,
+                          spec.depth_trunk, spec.out)
+    rl, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, 0.0, 0.1, "NLL", 1.0)
+    # fit ratio from the log-likelihood: ll = -0.5 sum r^2 (v = 1: the log v term is 0); prior part removed
+    prior = float(np.sum(-0.5 * (th.astype(np.float64) / 0.1) ** 2 - np.log(0.1) - 0.5 * np.log(2 * np.pi)))
+    ssr = -2.0 * (rl - prior)
+    fit = ssr / float(np.sum(p.y.astype(np.float64) ** 2))
+    e_gram, e_res = rel_norm(gg, rg), rel_norm(gres, rg)
+    row = {"noise": noise, "fit_ratio": fit, "gram_relnorm": e_gram, "residual_relnorm": e_res,
+           "gram_elem": float(np.abs(gg - rg).max() / np.abs(rg).max()),
+           "residual_elem": float(np.abs(gres - rg).max() / np.abs(rg).max())}
+    print(json.dumps(row))
+    os.makedirs(os.path.dirname(FIT_TABLE), exist_ok=True)
+    rows = json.load(open(FIT_TABLE)) if os.path.exists(FIT_TABLE) else []
+    rows = [r for r in rows if r["noise"] != noise] + [row]
+    json.dump(sorted(rows, key=lambda r: -r["noise"]), open(FIT_TABLE, "w"), indent=1)
+    parity.check("grad_relnorm", e_gram, f"gram, noise {noise:g}, fit {fit:.1e}")
+    parity.check("grad_relnorm", e_res, f"residual, noise {noise:g}, fit {fit:.1e}")

@@ -121,21 +121,23 @@ def test_sharding_independence(cuda_device):
     assert torch.equal(full.stacked()[2:], part.stacked())
 
 
-@pytest.mark.parametrize("variant,case,fuse_scatter", [("hmc", "deeponet_small", 1),
-                                                       ("inv_mass", "deeponet_small", 1),
-                                                       ("nuts", "deeponet_small", 1),
-                                                       ("inv_mass", "deeponet_refshape", 1),
-                                                       ("hmc", "deeponet_refshape", 0)])
-def test_deeponet_fused_trajectory_bitwise_equals_stepwise(variant, case, fuse_scatter, cuda_device):
+@pytest.mark.parametrize("variant,case,fuse_scatter,C", [("hmc", "deeponet_small", 1, 3),
+                                                         ("inv_mass", "deeponet_small", 1, 3),
+                                                         ("nuts", "deeponet_small", 1, 3),
+                                                         ("inv_mass", "deeponet_refshape", 1, 2),
+                                                         ("hmc", "deeponet_refshape", 0, 2),
+                                                         ("hmc", "deeponet_refshape", 1, 4),
+                                                         ("nuts", "deeponet_refshape", 1, 4)])
+def test_deeponet_fused_trajectory_bitwise_equals_stepwise(variant, case, fuse_scatter, C, cuda_device):
     """vihmc_trajectory on a DeepONet plan (leapfrog updates fused into the gradient gather) == L separate
     evaluations driven by the torch elementwise updates, bit for bit: positions, accepts, log-probs, step sizes.
     deeponet_refshape is width 100: the bf16x6 fused forward, the weight images kept current by the scatter and by
-    the leapfrog's own scatter in k_leap_open / k_gather_prior<LEAP> (fuse_scatter = 1) or by k_scatter (0)."""
+    the leapfrog's own scatter in k_leap_open / k_gather_prior<LEAP> (fuse_scatter = 1) or by k_scatter (0). At
+    C = 4 (max_chains 4 >= gram_min_chains) both paths run the interior steps in Gram form (counters checked)."""
     from vihmc.engine import DeepONetEngine, trunk_features
     from vihmc.samplers import ChainRNG, EngineEvaluator, Sampler, run_chains
     c = deeponet_case(case)
     p = c.prob
-    C = 3 if case == "deeponet_small" else 2
     th0 = torch.tensor(c.thetas[0])
     kw = dict(burn=2)
     if variant == "inv_mass":
@@ -149,8 +151,11 @@ def test_deeponet_fused_trajectory_bitwise_equals_stepwise(variant, case, fuse_s
         eng.fused_trajectory = fused
         eng.option("fuse_scatter", fuse_scatter)
         S, L, eps = (8, 7, 2e-3) if case == "deeponet_small" else (5, 3, 5e-3)
+        eng.option("gram_evals", 0)
         out.append(run_chains(EngineEvaluator(eng), th0[None].repeat(C, 1), S, L, eps,
                               rng=ChainRNG(C, th0.numel(), cuda_device, seeds=[20 + i for i in range(C)]), **kw))
+        n_gram = eng.get_option("gram_evals")
+        assert (n_gram == S * (L - 1)) if (C >= 4 and case == "deeponet_refshape") else n_gram == 0, n_gram
     a, b = out
     assert torch.equal(a.accepted, b.accepted)
     assert torch.equal(a.counts, b.counts)

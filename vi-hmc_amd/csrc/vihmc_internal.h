@@ -219,6 +219,8 @@ struct StatsJob {
 };
 hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s,
                          const StatsJob* stats = nullptr);
+constexpr int CLOCK_STAMP_WG = 64;     // k_clock_stamp workgroups; 3 uint64 each
+hipError_t launch_clock_stamp(unsigned long long* out, hipStream_t s);
 hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_waves, int C, float* lik,
                                  float* gp, int64_t gp_cs, double count, int loss, float tau_out, hipStream_t s);
 // Leapfrog update fused into the gradient gather (vihmc_trajectory on DeepONet plans), hamiltorch's order with

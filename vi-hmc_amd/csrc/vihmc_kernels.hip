@@ -825,4 +825,19 @@ hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int ma
     VIHMC_LAUNCH(k_mlp_traj<0>, dim3(C), dim3(64), shm, s, a, maxw, tt);
 }
 
+// Shader-clock stamp (measurement, vihmc_clock_stamp): 64 one-wave workgroups (8 per XCD under the b % 8 dispatch)
+// record their XCD id, s_memtime (shader-clock ticks) and s_memrealtime (100 MHz); two stamps around a timed region
+// give each XCD's average shader clock over it (MI355X_MICROARCH.md "DVFS give-back" item 6). Vector stores only.
+__global__ __launch_bounds__(64) void k_clock_stamp(unsigned long long* out) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x < 3) out[blockIdx.x * 3 + threadIdx.x] = threadIdx.x == 0 ? (unsigned long long)x : threadIdx.x == 1 ? t : r;
+}
+
+hipError_t launch_clock_stamp(unsigned long long* out, hipStream_t s) {
+    VIHMC_LAUNCH(k_clock_stamp, dim3(CLOCK_STAMP_WG), dim3(64), 0, s, out);
+}
+
 }  // namespace vihmc

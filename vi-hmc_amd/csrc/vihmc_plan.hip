@@ -170,6 +170,8 @@ struct vihmc_plan {
     double* gstats = nullptr;
     int64_t gstats_cs = 0;
     bool last_gram = false;       // the last gradient evaluation ran the Gram form (get_option gram: bit 1)
+    int64_t n_grad_calls = 0;     // DeepONet gradient evaluations (calls) since creation / reset (get_option grad_evals)
+    int64_t n_gram_calls = 0;     // ... of which ran the Gram form (get_option gram_evals)
     bool timg_live = false;       // the W^T images hold this evaluation's theta (scatter-kept or split this evaluation)
     bool last_bwd_chain = false;  // the last gradient evaluation ran k_bwd_chain (get_option bwd_chain: bit 1)
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
@@ -363,8 +365,10 @@ int gram_images(vihmc_plan* p, hipStream_t s) {
     return 0;
 }
 
-bool gram_on(const vihmc_plan* p, int C) {
-    return p->gram && p->gram_alloc && p->W == 100 && p->contract_bf16x6 && C >= p->gram_min_chains;
+// The form is a property of the plan (its max_chains), not of the call's chain count: a chain's trajectory does not
+// depend on how many chains share its launch (a ragged last rank, a partial batch) -- ADVICE r3.
+bool gram_on(const vihmc_plan* p) {
+    return p->gram && p->gram_alloc && p->W == 100 && p->contract_bf16x6 && p->maxC >= p->gram_min_chains;
 }
 
 GramArgs gram_args(vihmc_plan* p, int C) {
@@ -1000,8 +1004,12 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     p->timg_live = p->img_by_scatter && p->wtimg;      // the scatter above kept the W^T images current
     if (int rc = deeponet_forward_layers(p, C, s, want_grad && p->contract_bf16x6 && p->W == 100)) return rc;
     // gradient-only evaluations (no log-prob returned): the Gram-form contraction, which forms no residual
-    const bool gram = want_grad && logp == nullptr && gram_on(p, C);
+    const bool gram = want_grad && logp == nullptr && gram_on(p);
     p->last_gram = gram;
+    if (want_grad) {
+        ++p->n_grad_calls;
+        if (gram) ++p->n_gram_calls;
+    }
     int stats_waves = 0;
     if (gram) {
         Net& b = p->nets[0];
@@ -1644,7 +1652,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, grad_evals, gram_evals"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1660,6 +1668,10 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "bwd_chain") p->bwd_chain = value ? 1 : 0;
     else if (k == "gram") p->gram = value ? 1 : 0;
     else if (k == "gram_min_chains") p->gram_min_chains = std::max(1, value);
+    else if (k == "grad_evals" || k == "gram_evals") {          // counters: any value resets both
+        p->n_grad_calls = p->n_gram_calls = 0;
+        return 0;
+    }
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     // captured graphs embed the kernel choice
     for (auto& g : p->graphs) (void)hipGraphExecDestroy(g.second);
@@ -1681,8 +1693,18 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "bwd_chain") *value = p->bwd_chain | (p->last_bwd_chain ? 2 : 0);
     else if (k == "gram") *value = (p->gram && p->gram_alloc ? 1 : 0) | (p->last_gram ? 2 : 0);
     else if (k == "gram_min_chains") *value = p->gram_min_chains;
+    else if (k == "grad_evals") *value = (int)std::min<int64_t>(p->n_grad_calls, INT32_MAX);
+    else if (k == "gram_evals") *value = (int)std::min<int64_t>(p->n_gram_calls, INT32_MAX);
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
+}
+
+int vihmc_clock_stamp(uint64_t* out, void* stream) {
+    return guarded([&]() -> int {
+        if (!out) return fail("null argument");
+        HIPCHK(launch_clock_stamp(reinterpret_cast<unsigned long long*>(out), static_cast<hipStream_t>(stream)));
+        return 0;
+    });
 }
 
 int vihmc_graph_enable(vihmc_plan* p, int on) {

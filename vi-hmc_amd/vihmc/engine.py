@@ -292,6 +292,40 @@ class _Engine:
         return ms.value, n.value
 
 
+class ShaderClock:
+    """Average shader clock of each XCD over a region of a stream: vihmc_clock_stamp before and after it (64 one-wave
+    workgroups, 8 per XCD: XCD id, s_memtime, s_memrealtime); clock = d memtime / d memrealtime x 100 MHz."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf = torch.zeros(2, 64, 3, dtype=torch.int64, device=self.device)
+        self.L = _lib.lib()
+
+    def _stamp(self, i):
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_clock_stamp(self.buf[i].data_ptr(),
+                                          ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        _lib.check(rc, "vihmc_clock_stamp")
+
+    def start(self):
+        self._stamp(0)
+
+    def stop(self):
+        self._stamp(1)
+
+    def mhz(self) -> dict:
+        """{xcd: MHz} from the two stamps (syncs); medians over each XCD's workgroups."""
+        b = self.buf.cpu().numpy().view(np.uint64).astype(np.float64)
+        out = {}
+        for x in sorted(set(int(v) for v in b[0, :, 0]) & set(int(v) for v in b[1, :, 0])):
+            a0, a1 = b[0][b[0, :, 0] == x], b[1][b[1, :, 0] == x]
+            dt = np.median(a1[:, 1]) - np.median(a0[:, 1])
+            dr = np.median(a1[:, 2]) - np.median(a0[:, 2])
+            if dr > 0:
+                out[x] = 100.0 * dt / dr
+        return out
+
+
 def expand_prior(K: int, mu, sd) -> (np.ndarray, np.ndarray):
     mu = np.broadcast_to(np.asarray(mu, np.float32), (K,)).copy()
     sd = np.broadcast_to(np.asarray(sd, np.float32), (K,)).copy()

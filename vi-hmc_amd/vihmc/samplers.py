@@ -336,6 +336,10 @@ class HMCRunner:
             for m in range(M):
                 if m == 0 and g0_cached is not None:
                     gm = g0_cached
+                elif step == 0 and m == 0:
+                    # the trajectory's start point: the residual form, as at its end point (time-symmetric form
+                    # assignment), also without the reuse
+                    gm = evs[m].logp_grad(th)[1]
                 else:
                     gm = _grad(evs[m], th)
                 p = torch.add(p, gm, alpha=half) if not torch.is_tensor(eps) else p + half * gm
