@@ -201,6 +201,7 @@ def test_gram_precision_vs_fit(noise, cuda_device):
     eng = DeepONetEngine(spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, 0.1, "NLL", 1.0,
                          max_chains=2, device=cuda_device)
     eng.option("gram_min_chains", 2)
+    eng.option("gram_guard", 0)                      # measure the Gram form itself at every fit
     tt = torch.tensor(np.stack([th, th]), device=cuda_device)
     gg = eng.grad(tt)[0].cpu().numpy()
     assert eng.get_option("gram") & 2
@@ -224,3 +225,91 @@ def test_gram_precision_vs_fit(noise, cuda_device):
     json.dump(sorted(rows, key=lambda r: -r["noise"]), open(FIT_TABLE, "w"), indent=1)
     parity.check("grad_relnorm", e_gram, f"gram, noise {noise:g}, fit {fit:.1e}")
     parity.check("grad_relnorm", e_res, f"residual, noise {noise:g}, fit {fit:.1e}")
+
+
+def _teacher_problem():
+    """W = 100 DeepONet, 64 functions x 21 x 21 points, frozen weights at the teacher and tiny data noise: at the
+    teacher the fit ratio sum r^2 / sum y^2 is ~1e-11, far below the guard threshold."""
+    from vihmc.data import deeponet_problem
+    return deeponet_problem(seed=5, n=64, nt=21, nx=21, noise=1e-6, mu_noise=0.0)
+
+
+def _guard_engine(p, C, dev):
+    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.layout import DeepONetSpec
+    return DeepONetEngine(DeepONetSpec(), p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, 0.1,
+                          "NLL", 1.0, max_chains=C, device=dev)
+
+
+def test_gram_guard_switch_per_chain(cuda_device):
+    """Fit guard (plan option gram_guard = k: residual form below sum r^2 / sum y^2 = 10^-k, decided from each
+    chain's previous-but-one likelihood evaluation): 2 chains at the teacher (fit ~1e-11) and 2 perturbed (fit
+    ~1e-2) in one gradient-only call run both forms -- the guarded chains bitwise the residual-form gradient, the
+    others bitwise the all-Gram call; both sides of the threshold; the two-evaluation lag."""
+    p = _teacher_problem()
+    C = 4
+    eng = _guard_engine(p, C, cuda_device)
+    assert eng.get_option("gram_guard") > 0 and eng.get_option("gram_min_chains") == 4
+    t = p.teacher[p.grad_ind].astype(np.float32)
+    rng = np.random.default_rng(4)
+    pert = [(t + 0.05 * rng.standard_normal(t.size)).astype(np.float32) for _ in range(2)]
+    th = torch.tensor(np.stack([t, t] + pert), device=cuda_device)
+    _, g_res = eng.logp_grad(th)                       # snapshot 1 (all-residual evaluation)
+    g = eng.grad(th)                                   # one snapshot only: no decision yet, all Gram
+    assert eng.get_option("gram_chains") == 4
+    g_all_gram = g.clone()
+    eng.logp_grad(th)                                  # snapshot 2
+    g = eng.grad(th)
+    assert eng.get_option("gram_chains") == 2, eng.get_option("gram_chains")
+    assert torch.equal(g[:2], g_res[:2]), "guarded chains: the residual-form gradient"
+    assert torch.equal(g[2:], g_all_gram[2:]), "the other chains: the Gram form, independent of the guarded ones"
+    for i in (2, 3):
+        parity.check("grad_relnorm", rel_norm(g[i].cpu().numpy(), g_res[i].cpu().numpy()), f"Gram chain {i}")
+    # the other side of the threshold: 10^-14 is below every chain's fit -> all Gram; guard off -> all Gram
+    eng.option("gram_guard", 14)
+    eng.logp_grad(th)
+    eng.logp_grad(th)
+    eng.grad(th)
+    assert eng.get_option("gram_chains") == 4
+    eng.option("gram_guard", 0)
+    eng.logp_grad(th)
+    eng.logp_grad(th)
+    assert torch.equal(eng.grad(th), g_all_gram)
+    # lag: chain 0 moves away from the teacher; the decision follows its previous-but-one snapshot
+    eng.option("gram_guard", 6)
+    eng.logp_grad(th)
+    eng.logp_grad(th)                                  # snapshots: (teacher, teacher) for chain 0
+    th2 = th.clone()
+    th2[0] = th[2]
+    eng.logp_grad(th2)                                 # latest snapshot: chain 0 well off the teacher
+    eng.grad(th2)
+    assert eng.get_option("gram_chains") == 2          # still guarded by the previous-but-one snapshot
+    eng.logp_grad(th2)
+    eng.grad(th2)
+    assert eng.get_option("gram_chains") == 3
+
+
+def test_gram_guard_fused_trajectory_bitwise_equals_stepwise(cuda_device):
+    """The guard inside vihmc_trajectory: chains at the teacher fall back to the residual form from their third
+    trajectory on; fused and step-by-step paths take the same decisions (same snapshots) and agree bit for bit."""
+    from vihmc.samplers import ChainRNG, EngineEvaluator, run_chains
+    p = _teacher_problem()
+    C = 4
+    t = p.teacher[p.grad_ind].astype(np.float32)
+    rng = np.random.default_rng(6)
+    th0 = torch.tensor(np.stack([t, t] + [(t + 0.05 * rng.standard_normal(t.size)).astype(np.float32)
+                                          for _ in range(2)]))
+    out, counts = [], []
+    for fused in (True, False):
+        eng = _guard_engine(p, C, cuda_device)
+        eng.fused_trajectory = fused
+        eng.option("gram_evals", 0)
+        res = run_chains(EngineEvaluator(eng), th0, 5, 4, 1e-6, rng=ChainRNG(C, t.size, cuda_device, seeds=[7, 8, 9, 10]))
+        out.append(res)
+        counts.append((eng.get_option("grad_evals"), eng.get_option("gram_evals"), eng.get_option("gram_chains")))
+    a, b = out
+    assert counts[0] == counts[1], counts
+    assert counts[0][2] == 2, counts                   # the last inner evaluation ran Gram for 2 of the 4 chains
+    assert torch.equal(a.accepted, b.accepted)
+    assert torch.equal(a.samples[:, :int(a.counts.max())], b.samples[:, :int(b.counts.max())])
+    assert torch.equal(a.logp_trace, b.logp_trace)

@@ -93,6 +93,7 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
 #endif
     const int per_chain = P.o_tiles * P.q_chunks;
     const int c = b / per_chain;
+    if (P.sel && !chain_bit(P.bits, c)) return;          // fit guard: a chain that runs the Gram form
     b -= c * per_chain;
     const int qc = b / P.o_tiles;
     const int og = b - qc * P.o_tiles;
@@ -391,6 +392,7 @@ __global__ __launch_bounds__(CBB_THREADS, 1) void k_contract_bf_b(ContractProb P
     }
     const int per_chain = P.o_tiles * P.q_chunks;
     const int c = b / per_chain;
+    if (P.sel && !chain_bit(P.bits, c)) return;          // fit guard: a chain that runs the Gram form
     b -= c * per_chain;
     const int qc = b / P.o_tiles;
     const int og = b - qc * P.o_tiles;

@@ -122,6 +122,7 @@ __device__ __forceinline__ void unit_of(int b, int upx, int n1, int n2, int& lis
 // ---------------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
     const int c = blockIdx.y;
+    if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
     const int r = blockIdx.x * 256 + threadIdx.x;
     const int f = 2 * 100;                                    // byte offset of feature 100 in a plane row
     if (r < A.N) {
@@ -175,6 +176,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         c = u - A.C * A.S;
         kind = 2;
     }
+    if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain (unit-uniform)
     const unsigned char* src0;
     int nb, kb0 = 0;
     if (kind == 2) {
@@ -340,6 +342,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
         return;
     }
     const int pt = u / A.C, c = u - pt * A.C;
+    if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int nbm = A.nblkN, nb = nbm + 4;
     if (wave == GR_CW) {
@@ -444,6 +447,7 @@ __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char
     float* zbt = gts + 101 * 112;                                // Zb^T [101][32]
     const int ngroups = (A.N + 31) / 32;
     const int c = u / ngroups, m = u - c * ngroups;
+    if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const float* gt = A.gt + c * A.gt_cs2;
     for (int e = tid; e < 101 * 28; e += GR_THREADS) {

@@ -113,6 +113,17 @@ int bwd_chain_rows();
 //         recompute; y^T with load_g = 0) -> dZ_branch partial per chunk
 // Forward-only (predict) writes out[q][o] = S into `out` (side A, o = p contiguous).
 // ---------------------------------------------------------------------------------------------
+// Gram-form fit guard (vihmc_plan.hip, plan option gram_guard): per-chain selection of the contraction form in a
+// gradient-only evaluation. Bit c set: chain c runs the residual form (k_contract_bf + k_contract_bf_b + reduce);
+// clear: the Gram form. The selection is a launch argument, so every kernel sees it without a memory read.
+constexpr int GUARD_MAXC = 256;
+struct ChainBits {
+    uint32_t w[GUARD_MAXC / 32];
+};
+__host__ __device__ inline bool chain_bit(const ChainBits& b, int c) {
+    return c < GUARD_MAXC && ((b.w[c >> 5] >> (c & 31)) & 1u) != 0u;
+}
+
 struct ContractProb {
     const float* Own; int64_t own_cs; int32_t ldown;
     const float* Q;   int64_t q_cs;   int32_t ldq;
@@ -132,6 +143,7 @@ struct ContractProb {
                                           //    operands, six products (k_contract_bf)
     const unsigned char* qimg; int64_t qimg_cs;   // bf16x6: Q pre-split into blocks (launch_split_blocks)
     float gscale;
+    int32_t sel; ChainBits bits;          // sel = 1: only the chains whose bit is set (the others' workgroups exit)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -157,6 +169,7 @@ struct GramArgs {
     int32_t upx_a, upx_b;                                  // set by launch_gram
     int32_t aug_done;                                      // feature 100 of both images already written
     float gscale;
+    int32_t sel; ChainBits bits;                           // sel = 1: chains whose bit is set exit (residual form)
 };
 hipError_t launch_gram(const GramArgs& a, hipStream_t s);
 hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld, __bf16* yb,
@@ -213,16 +226,23 @@ __host__ __device__ inline int bwd_tile_off(int tn, int t, int ntj, int lane) {
 }
 // Likelihood statistics of the contraction (k_contract_stats): ll from the per-wave (sum r^2, sum G) pairs and
 // d ll / d b0 into packed slot 0 of gp. Optionally run as one extra grid slice of the weight-gradient reduce.
+// Mixed Gram / residual evaluation (fit guard): chains whose bit is set read (stats2, n_waves2). fit != null: the
+// fit ratio sum r^2 / sum y^2 (*ysq) of every chain is written to fit[c] (all-residual evaluations only).
 struct StatsJob {
     const double* stats; int64_t stats_cs; int32_t n_waves;
     float* lik; float* gp; int64_t gp_cs; double count; int32_t loss; float tau_out;
+    const double* stats2; int64_t stats2_cs; int32_t n_waves2;
+    int32_t sel; ChainBits bits;
+    float* fit; const double* ysq;
 };
 hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s,
-                         const StatsJob* stats = nullptr);
+                         const StatsJob* stats = nullptr, const ChainBits* only = nullptr);
 constexpr int CLOCK_STAMP_WG = 64;     // k_clock_stamp workgroups; 3 uint64 each
 hipError_t launch_clock_stamp(unsigned long long* out, hipStream_t s);
-hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_waves, int C, float* lik,
-                                 float* gp, int64_t gp_cs, double count, int loss, float tau_out, hipStream_t s);
+hipError_t launch_contract_stats(const StatsJob& J, int C, hipStream_t s);
+// sum of y^2 over n elements (fixed order, fp64): `parts` partial sums into part[], then *out (the fit guard's scale)
+constexpr int YSQ_PARTS = 1024;
+hipError_t launch_ysq(const float* y, int64_t n, double* part, double* out, hipStream_t s);
 // Leapfrog update fused into the gradient gather (vihmc_trajectory on DeepONet plans), hamiltorch's order with
 // every product and sum rounded separately: p += eps g; then on the last step p -= (eps / 2) g, otherwise
 // theta += eps p (eps inv_mass p with a diagonal mass). p and theta are updated in place (theta is the

@@ -125,9 +125,11 @@ __device__ double block_sum(double v, double* sh) {
 
 __device__ void contract_stats_body(const StatsJob& J, int c) {
     __shared__ double sh[8];
-    const double* st = J.stats + c * J.stats_cs;
+    const bool alt = J.sel && chain_bit(J.bits, c);     // fit guard: this chain ran the other contraction form
+    const double* st = alt ? J.stats2 + c * J.stats2_cs : J.stats + c * J.stats_cs;
+    const int nw = alt ? J.n_waves2 : J.n_waves;
     double ssq = 0.0, gs = 0.0;
-    for (int i = threadIdx.x; i < J.n_waves; i += blockDim.x) {
+    for (int i = threadIdx.x; i < nw; i += blockDim.x) {
         ssq += st[2 * i];
         gs += st[2 * i + 1];
     }
@@ -143,6 +145,7 @@ __device__ void contract_stats_body(const StatsJob& J, int c) {
         }
         J.lik[c] = (float)ll;
         J.gp[c * J.gp_cs] = (float)gs;   // d ll / d b0 (packed slot 0)
+        if (J.fit) J.fit[c] = (float)(ssq / fmax(*J.ysq, 1e-300));
     }
 }
 
@@ -155,13 +158,14 @@ __global__ __launch_bounds__(256) void k_contract_stats(StatsJob J) { contract_s
 // Fixed-order sum of partial slabs (p = 0, 1, ... sequentially -- bitwise reproducible); grid slice y = n_jobs
 // (when present) runs the likelihood statistics instead (saves their launch after side A); 4 consecutive
 // elements per thread as float4 when the job's strides allow, 8 slab loads in flight ahead of the adds.
-__global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_jobs, StatsJob sj) {
+__global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_jobs, StatsJob sj, int sel, ChainBits only) {
     if ((int)blockIdx.y == n_jobs) {                   // the optional likelihood-statistics slice
         if (blockIdx.x == 0) contract_stats_body(sj, blockIdx.z);
         return;
     }
     const ReduceJob J = jobs[blockIdx.y];
     const int c = blockIdx.z;
+    if (sel && !chain_bit(only, c)) return;            // fit guard: a chain that ran the Gram form
     if (J.tiled) {
         // float4 quads of the tiled slabs (one accumulator quad of a dW tile each), summed over the slabs in the
         // row-major paths' fixed orders -- so both layouts give bitwise equal gradients -- then scattered to the
@@ -752,16 +756,38 @@ hipError_t launch_scatter(float* packed, int64_t dp, int C, const float* theta, 
 }
 
 hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s,
-                         const StatsJob* stats) {
+                         const StatsJob* stats, const ChainBits* only) {
     // grid sized for the scalar path; vectorised jobs leave 3/4 of the x-blocks idle (cheap exits)
     dim3 g((max_len + 255) / 256, n_jobs + (stats ? 1 : 0), C), blk(256);
-    VIHMC_LAUNCH(k_reduce, g, blk, 0, s, jobs_dev, n_jobs, stats ? *stats : StatsJob{});
+    VIHMC_LAUNCH(k_reduce, g, blk, 0, s, jobs_dev, n_jobs, stats ? *stats : StatsJob{}, only ? 1 : 0,
+                 only ? *only : ChainBits{});
 }
 
-hipError_t launch_contract_stats(const double* stats, int64_t stats_cs, int n_waves, int C, float* lik,
-                                 float* gp, int64_t gp_cs, double count, int loss, float tau_out, hipStream_t s) {
-    const StatsJob J{stats, stats_cs, n_waves, lik, gp, gp_cs, count, loss, tau_out};
+hipError_t launch_contract_stats(const StatsJob& J, int C, hipStream_t s) {
     VIHMC_LAUNCH(k_contract_stats, dim3(C), dim3(256), 0, s, J);
+}
+
+// sum of y^2 in fixed order: YSQ_PARTS contiguous chunks (thread-strided fp64 sums + block tree), then one block
+// over the partials
+__global__ __launch_bounds__(256) void k_ysq_part(const float* y, int64_t n, double* part) {
+    __shared__ double sh[8];
+    const int64_t chunk = (n + YSQ_PARTS - 1) / YSQ_PARTS;
+    const int64_t e0 = (int64_t)blockIdx.x * chunk, e1 = e0 + chunk < n ? e0 + chunk : n;
+    double v = 0.0;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) v += (double)y[e] * (double)y[e];
+    v = block_sum(v, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = v;
+}
+__global__ __launch_bounds__(256) void k_ysq_final(const double* part, double* out) {
+    __shared__ double sh[8];
+    double v = 0.0;
+    for (int i = threadIdx.x; i < YSQ_PARTS; i += 256) v += part[i];
+    v = block_sum(v, sh);
+    if (threadIdx.x == 0) *out = v;
+}
+hipError_t launch_ysq(const float* y, int64_t n, double* part, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_ysq_part, dim3(YSQ_PARTS), dim3(256), 0, s, y, n, part);
+    VIHMC_LAUNCH(k_ysq_final, dim3(1), dim3(256), 0, s, part, out);
 }
 
 hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* smap, const float* theta, int K,

@@ -170,8 +170,24 @@ struct vihmc_plan {
     double* gstats = nullptr;
     int64_t gstats_cs = 0;
     bool last_gram = false;       // the last gradient evaluation ran the Gram form (get_option gram: bit 1)
+    int last_gram_chains = 0;     // ... for this many of its chains (get_option gram_chains)
     int64_t n_grad_calls = 0;     // DeepONet gradient evaluations (calls) since creation / reset (get_option grad_evals)
-    int64_t n_gram_calls = 0;     // ... of which ran the Gram form (get_option gram_evals)
+    int64_t n_gram_calls = 0;     // ... of which ran the Gram form for some chain (get_option gram_evals)
+    // Fit guard (plan option gram_guard = k: threshold 10^-k on sum r^2 / sum y^2; 0 = off). The Gram form's two
+    // O(|y|) terms cancel to O(|S - y|), so its rounding grows like |y| / |S - y| (profiles/r04_gram_fit_table.json).
+    // Every all-residual evaluation (end points, log-prob / value / forward calls) writes each chain's fit ratio and
+    // copies it to a pinned 2-slot ring (event per slot); a gradient-only evaluation sends chain c to the residual
+    // form when the ratio of its PREVIOUS-BUT-ONE snapshot is below the threshold -- a deterministic function of the
+    // chain's own history (two evaluations of lag keep the host one trajectory ahead of the GPU without a stall).
+    int gram_guard = 6;
+    float* fit_dev = nullptr;     // [maxC] fit ratios of the last all-residual evaluation
+    double* ysq_dev = nullptr;    // sum y^2 (k_ysq, whenever the data images are rebuilt)
+    double* ysq_part = nullptr;
+    float* fit_host = nullptr;    // pinned [2][maxC]
+    hipEvent_t fit_ev[2] = {nullptr, nullptr};
+    int snap_C[2] = {0, 0};
+    int64_t n_snap = 0;
+    bool capturing = false;       // inside a hipGraph capture: no snapshot (the ring is host state)
     bool timg_live = false;       // the W^T images hold this evaluation's theta (scatter-kept or split this evaluation)
     bool last_bwd_chain = false;  // the last gradient evaluation ran k_bwd_chain (get_option bwd_chain: bit 1)
     float *g_theta = nullptr, *g_logp = nullptr, *g_grad = nullptr;
@@ -214,6 +230,9 @@ struct vihmc_plan {
         return 0;
     }
     ~vihmc_plan() {
+        for (hipEvent_t e : fit_ev)
+            if (e) (void)hipEventDestroy(e);
+        if (fit_host) (void)hipHostFree(fit_host);
         for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
         if (cap_stream) (void)hipStreamDestroy(cap_stream);
         for (void* p : allocs) (void)hipFree(p);
@@ -355,13 +374,54 @@ int gram_setup(vihmc_plan* p, int C) {
     if (int rc = p->alloc(&p->gcnt, C)) return rc;
     p->gstats_cs = 2 * (int64_t)p->gPT * 8;
     if (int rc = p->alloc(&p->gstats, p->gstats_cs * C)) return rc;
+    if (int rc = p->alloc(&p->fit_dev, C)) return rc;
+    if (int rc = p->alloc(&p->ysq_dev, 1)) return rc;
+    if (int rc = p->alloc(&p->ysq_part, YSQ_PARTS)) return rc;
+    HIPCHK(hipHostMalloc((void**)&p->fit_host, sizeof(float) * 2 * (size_t)C));
+    for (auto& e : p->fit_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     p->gram_alloc = true;
     return 0;
 }
 
+// data images + the fit guard's sum y^2, whenever the plan's data change (the guard's history starts over)
 int gram_images(vihmc_plan* p, hipStream_t s) {
     if (!p->gram_alloc) return 0;
     HIPCHK(launch_gram_yimg(p->y, p->N, p->P, p->gya, p->gya_plane, p->gya_ld, p->gyb, p->gyb_plane, p->gyb_ld, s));
+    HIPCHK(launch_ysq(p->y, (int64_t)p->N * p->P, p->ysq_part, p->ysq_dev, s));
+    p->n_snap = 0;
+    return 0;
+}
+
+bool guard_live(const vihmc_plan* p) {
+    return p->gram_alloc && p->gram_guard > 0 && p->maxC <= GUARD_MAXC && !p->capturing;
+}
+
+// chains of this gradient-only evaluation that run the residual form: previous-but-one snapshot below the threshold
+int guard_select(vihmc_plan* p, int C, ChainBits& bits, int& n) {
+    n = 0;
+    bits = ChainBits{};
+    if (!guard_live(p) || p->n_snap < 2) return 0;
+    const int k = (int)((p->n_snap - 2) & 1);
+    if (p->snap_C[k] != C) return 0;                     // a snapshot of another chain count says nothing here
+    HIPCHK(hipEventSynchronize(p->fit_ev[k]));           // normally complete already (one trajectory back)
+    const float thr = std::pow(10.f, -(float)p->gram_guard);
+    const float* f = p->fit_host + (size_t)k * p->maxC;
+    for (int c = 0; c < C; ++c)
+        if (f[c] < thr) {
+            bits.w[c >> 5] |= 1u << (c & 31);
+            ++n;
+        }
+    return 0;
+}
+
+// after an all-residual evaluation wrote fit_dev: copy it into the next ring slot
+int guard_snapshot(vihmc_plan* p, int C, hipStream_t s) {
+    const int k = (int)(p->n_snap & 1);
+    HIPCHK(hipMemcpyAsync(p->fit_host + (size_t)k * p->maxC, p->fit_dev, sizeof(float) * (size_t)C,
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(p->fit_ev[k], s));
+    p->snap_C[k] = C;
+    ++p->n_snap;
     return 0;
 }
 
@@ -1003,14 +1063,24 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     p->img_by_fwd = false;
     p->timg_live = p->img_by_scatter && p->wtimg;      // the scatter above kept the W^T images current
     if (int rc = deeponet_forward_layers(p, C, s, want_grad && p->contract_bf16x6 && p->W == 100)) return rc;
-    // gradient-only evaluations (no log-prob returned): the Gram-form contraction, which forms no residual
-    const bool gram = want_grad && logp == nullptr && gram_on(p);
+    // gradient-only evaluations (no log-prob returned): the Gram-form contraction, which forms no residual; the fit
+    // guard sends the chains whose fit is too good for its cancellation to the residual form (both forms in one
+    // evaluation, each launch skipping the other form's chains)
+    const bool gram_elig = want_grad && logp == nullptr && gram_on(p);
+    ChainBits resid{};
+    int n_resid = 0;
+    if (gram_elig)
+        if (int rc = guard_select(p, C, resid, n_resid)) return rc;
+    const bool gram = gram_elig && n_resid < C;          // some chain runs the Gram form
+    const bool resid_any = !gram;                        // ... or every chain the residual form
+    const bool mixed = gram && n_resid > 0;
     p->last_gram = gram;
+    p->last_gram_chains = gram ? C - n_resid : 0;
     if (want_grad) {
         ++p->n_grad_calls;
         if (gram) ++p->n_gram_calls;
     }
-    int stats_waves = 0;
+    int stats_waves = 0, stats_waves_res = 0;
     if (gram) {
         Net& b = p->nets[0];
         Net& t = p->nets[1];
@@ -1022,13 +1092,18 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         if (int rc = p->timing_begin(VIHMC_T_GRAM, s, &stop)) return rc;
         GramArgs ga = gram_args(p, C);
         ga.aug_done = p->img_by_fwd ? 1 : 0;               // the fused forward wrote feature 100 of both images
+        ga.sel = mixed ? 1 : 0;
+        ga.bits = resid;
         HIPCHK(launch_gram(ga, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
         stats_waves = p->gPT * 8;
-    } else {
+    }
+    if (resid_any || mixed) {
         ContractProb a = side_a(p, C, want_grad, out);
-        stats_waves = p->qchunksA * cdiv(p->P, CONTRACT_OWN_PER_WG) * (a.bf16x6 ? 8 : 4);
-        if (a.bf16x6 && !p->img_by_fwd)
+        a.sel = mixed ? 1 : 0;
+        a.bits = resid;
+        stats_waves_res = p->qchunksA * cdiv(p->P, CONTRACT_OWN_PER_WG) * (a.bf16x6 ? 8 : 4);
+        if (a.bf16x6 && !p->img_by_fwd && !gram)
             HIPCHK(launch_split_blocks(a.Q, a.q_cs, a.ldq, p->N, p->qsplitA, p->qsplitA_cs, C, s));
         hipEvent_t stop = nullptr;
         if (int rc = p->timing_begin(VIHMC_T_CONTRACT_A, s, &stop)) return rc;
@@ -1037,15 +1112,25 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     }
     // gradient evaluations: the statistics run as a slice of the weight-gradient reduce (nothing reads lik or
     // gp slot 0 before the gather)
-    const StatsJob stats_job{gram ? p->gstats : p->stats, gram ? p->gstats_cs : p->stats_cs, stats_waves, p->lik_buf,
-                             p->gp, p->dp, (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out};
-    if (!want_grad)
-        HIPCHK(launch_contract_stats(p->stats, p->stats_cs, stats_waves, C, p->lik_buf, p->gp, p->dp,
-                                     (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out, s));
+    StatsJob stats_job{gram ? p->gstats : p->stats, gram ? p->gstats_cs : p->stats_cs, gram ? stats_waves : stats_waves_res,
+                       p->lik_buf, p->gp, p->dp, (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out};
+    if (mixed) {
+        stats_job.stats2 = p->stats;
+        stats_job.stats2_cs = p->stats_cs;
+        stats_job.n_waves2 = stats_waves_res;
+        stats_job.sel = 1;
+        stats_job.bits = resid;
+    }
+    const bool snap = !gram && guard_live(p);          // every chain computed its likelihood: a fit snapshot
+    if (snap) {
+        stats_job.fit = p->fit_dev;
+        stats_job.ysq = p->ysq_dev;
+    }
+    if (!want_grad) HIPCHK(launch_contract_stats(stats_job, C, s));
     if (want_grad) {
         Net& b = p->nets[0];
         Net& t = p->nets[1];
-        if (!gram) {
+        if (resid_any || mixed) {
         ContractProb q{};
         q.Own = b.act + b.h_off.back();
         q.own_cs = b.act_cs;
@@ -1063,6 +1148,8 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         q.xcd_group = ((int64_t)C * p->qchunksB) % 8 == 0 ? 1 : 0;
         q.b0 = p->packed;
         q.b0_cs = p->dp;
+        q.sel = mixed ? 1 : 0;
+        q.bits = resid;
         q.out = p->partB;
         q.out_cs = p->partB_cs;
         q.ldout = p->ldz;
@@ -1083,8 +1170,9 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         if (int rc = p->timing_begin(VIHMC_T_CONTRACT_B, s, &stop)) return rc;
         HIPCHK(launch_contract(q, C, true, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
-        if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 2, std::max(p->lenA, p->lenB), C, s));
-        else HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s));
+        const ChainBits* only = mixed ? &resid : nullptr;
+        if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 2, std::max(p->lenA, p->lenB), C, s, nullptr, only));
+        else HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s, nullptr, only));
         }
 
         // backward through both MLPs, last layer first: one fused launch per layer (branch + trunk
@@ -1146,6 +1234,8 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
                                p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, p->fin_cnt, s,
                                want_grad ? leap : nullptr));
+    if (snap)
+        if (int rc = guard_snapshot(p, C, s)) return rc;
     return 0;
 }
 
@@ -1174,8 +1264,10 @@ int eval_graph(vihmc_plan* p, const float* theta, int C, float* logp, float* gra
     if (!exec) {
         if (!p->cap_stream) HIPCHK(hipStreamCreateWithFlags(&p->cap_stream, hipStreamNonBlocking));
         HIPCHK(hipStreamBeginCapture(p->cap_stream, hipStreamCaptureModeThreadLocal));
+        p->capturing = true;
         const int rc = p->kind == 0 ? deeponet_eval(p, p->g_theta, C, p->g_logp, p->g_grad, nullptr, p->cap_stream)
                                     : mlp_eval(p, p->g_theta, C, p->g_logp, p->g_grad, nullptr, p->cap_stream);
+        p->capturing = false;
         hipGraph_t graph = nullptr;
         const hipError_t ec = hipStreamEndCapture(p->cap_stream, &graph);
         if (rc) {
@@ -1652,7 +1744,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, grad_evals, gram_evals"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1668,6 +1760,10 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "bwd_chain") p->bwd_chain = value ? 1 : 0;
     else if (k == "gram") p->gram = value ? 1 : 0;
     else if (k == "gram_min_chains") p->gram_min_chains = std::max(1, value);
+    else if (k == "gram_guard") {                               // threshold 10^-value (0: off); history restarts
+        p->gram_guard = std::max(0, value);
+        p->n_snap = 0;
+    }
     else if (k == "grad_evals" || k == "gram_evals") {          // counters: any value resets both
         p->n_grad_calls = p->n_gram_calls = 0;
         return 0;
@@ -1695,6 +1791,8 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "gram_min_chains") *value = p->gram_min_chains;
     else if (k == "grad_evals") *value = (int)std::min<int64_t>(p->n_grad_calls, INT32_MAX);
     else if (k == "gram_evals") *value = (int)std::min<int64_t>(p->n_gram_calls, INT32_MAX);
+    else if (k == "gram_chains") *value = p->last_gram_chains;
+    else if (k == "gram_guard") *value = p->gram_guard;
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
 }
