@@ -221,6 +221,12 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value);
  * i.e. width 100; graph reads -1 while it follows VIHMC_GRAPH). */
 int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value);
 
+/* Bounds audit (new; no reference counterpart): a plan created with the environment variable VIHMC_CANARY=1 gives
+ * every device buffer it owns a 4-KB tail of 0xA5 bytes that no kernel may write. This synchronises the device and
+ * returns in *corrupted the number of tail bytes that changed (0 = no out-of-bounds write into a plan buffer); it
+ * fails for plans created without the variable. */
+int vihmc_plan_check_canaries(vihmc_plan* p, int64_t* corrupted);
+
 /* Measurement (new; no reference counterpart): enqueue on `stream` one stamp of the shader clock. out is DEVICE
  * memory [64][3] uint64: per one-wave workgroup (8 per XCD) its XCD id, s_memtime (shader-clock ticks) and
  * s_memrealtime (100 MHz ticks). Two stamps around a timed region give each XCD's average shader clock over it:

@@ -165,3 +165,45 @@ def test_odd_width_plan_after_gram_plan_matches_fresh_process(cuda_device, tmp_p
     assert np.array_equal(lpf.cpu().numpy(), ref["lpf"]) and np.array_equal(out.cpu().numpy(), ref["out"])
     big.close()
     eng.close()
+
+
+@pytest.mark.parametrize("case,C", [("deeponet_small", 2), ("deeponet_odd_full", 2), ("deeponet_refshape", 4),
+                                    ("deeponet_burgers", 4), ("deeponet_burgers", 1)])
+def test_no_out_of_bounds_writes_into_plan_buffers(case, C, cuda_device, monkeypatch):
+    """Bounds audit (VIHMC_CANARY=1: a 4-KB 0xA5 tail behind every plan buffer): value, gradient, Gram-form gradient,
+    forward and one fused trajectory on every golden geometry (odd widths 37 / 21, N = 45, P = 63 included) leave
+    every tail intact."""
+    from vihmc.engine import DeepONetEngine, trunk_features
+    monkeypatch.setenv("VIHMC_CANARY", "1")
+    c = deeponet_case(case)
+    p = c.prob
+    eng = DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
+                         c.prior_sd, c.loss, c.tau_out, max_chains=C, device=cuda_device)
+    monkeypatch.delenv("VIHMC_CANARY")
+    eng.option("gram_min_chains", 1)
+    n = len(c.thetas)
+    th = torch.tensor(np.stack([c.thetas[i % n] for i in range(C)]), device=cuda_device)
+    lp, g = eng.logp_grad(th)
+    eng.logp(th)
+    eng.grad(th)
+    eng.forward(th)
+    pm = torch.randn(th.shape, generator=torch.Generator().manual_seed(1)).to(cuda_device)
+    eng.trajectory(th, pm, g, 1e-5, 3)
+    assert eng.check_canaries() == 0
+    eng.close()
+
+
+def test_no_out_of_bounds_writes_bnn(cuda_device, monkeypatch):
+    from goldens import bnn_case
+    from vihmc.engine import MLPEngine
+    monkeypatch.setenv("VIHMC_CANARY", "1")
+    c = bnn_case("bnn_vi_hmc")
+    g = c.g
+    eng = MLPEngine(c.spec, c.data["x_train"], c.data["y_train"], g["mu"], c.idx, c.prior_mu, c.prior_sd, c.loss,
+                    c.tau_out, max_chains=3, device=cuda_device)
+    monkeypatch.delenv("VIHMC_CANARY")
+    th = torch.tensor(np.stack([c.thetas[0]] * 3), device=cuda_device)
+    lp, gr = eng.logp_grad(th)
+    eng.forward(th)
+    eng.trajectory(th, torch.ones_like(th), gr, 1e-4, 5)
+    assert eng.check_canaries() == 0

@@ -25,6 +25,7 @@ using namespace vihmc;
 namespace {
 
 thread_local std::string g_err;
+constexpr size_t CANARY_BYTES = 4096;
 
 int fail(const std::string& msg, int code = 1) {
     g_err = msg;
@@ -73,6 +74,13 @@ struct vihmc_plan {
     vihmc_lik_desc lik{};
     std::vector<void*> allocs;
     int64_t bytes = 0;
+    // bounds audit (environment VIHMC_CANARY=1 at plan creation): every plan buffer gets a CANARY_BYTES tail of
+    // 0xA5 that no kernel may write; vihmc_plan_check_canaries counts the tail bytes that changed
+    bool canary = [] {
+        const char* e = std::getenv("VIHMC_CANARY");
+        return e && std::atoi(e) != 0;
+    }();
+    std::vector<unsigned char*> canaries;
 
     int32_t* smap_w = nullptr;
     int32_t* smap_wt = nullptr;
@@ -214,10 +222,15 @@ struct vihmc_plan {
     int alloc(T** p, int64_t n) {
         void* v = nullptr;
         const size_t sz = std::max<int64_t>(n, 1) * sizeof(T);
-        hipError_t e = hipMalloc(&v, sz);
+        hipError_t e = hipMalloc(&v, sz + (canary ? CANARY_BYTES : 0));
         if (e != hipSuccess) return fail(std::string("hipMalloc(") + std::to_string(sz) + "): " + hipGetErrorString(e), (int)e);
         e = hipMemset(v, 0, sz);
         if (e != hipSuccess) return fail(std::string("hipMemset: ") + hipGetErrorString(e), (int)e);
+        if (canary) {
+            e = hipMemset(static_cast<unsigned char*>(v) + sz, 0xA5, CANARY_BYTES);
+            if (e != hipSuccess) return fail(std::string("hipMemset: ") + hipGetErrorString(e), (int)e);
+            canaries.push_back(static_cast<unsigned char*>(v) + sz);
+        }
         allocs.push_back(v);
         bytes += sz;
         *p = static_cast<T*>(v);
@@ -1795,6 +1808,22 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "gram_guard") *value = p->gram_guard;
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
+}
+
+int vihmc_plan_check_canaries(vihmc_plan* p, int64_t* corrupted) {
+    return guarded([&]() -> int {
+        if (!p || !corrupted) return fail("null argument");
+        if (!p->canary) return fail("vihmc_plan_check_canaries: plan created without VIHMC_CANARY=1");
+        HIPCHK(hipDeviceSynchronize());
+        std::vector<unsigned char> h(CANARY_BYTES);
+        int64_t bad = 0;
+        for (unsigned char* c : p->canaries) {
+            HIPCHK(hipMemcpy(h.data(), c, CANARY_BYTES, hipMemcpyDeviceToHost));
+            for (unsigned char v : h) bad += v != 0xA5;
+        }
+        *corrupted = bad;
+        return 0;
+    });
 }
 
 int vihmc_clock_stamp(uint64_t* out, void* stream) {

@@ -74,6 +74,7 @@ SIGNATURES = {
     "vihmc_timing_read_class": (c_int, [c_void_p, c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_int64)]),
     "vihmc_timing_reset": (c_int, [c_void_p]),
     "vihmc_clock_stamp": (c_int, [c_void_p, c_void_p]),
+    "vihmc_plan_check_canaries": (c_int, [c_void_p, ctypes.POINTER(c_int64)]),
     "vihmc_plan_destroy": (None, [c_void_p]),
     "vihmc_last_error": (c_char_p, []),
     "vihmc_version": (c_char_p, []),

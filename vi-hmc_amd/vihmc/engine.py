@@ -285,6 +285,13 @@ class _Engine:
                    f"vihmc_plan_get_option({key})")
         return v.value
 
+    def check_canaries(self) -> int:
+        """vihmc_plan_check_canaries: bytes written past the end of the plan's buffers (plan created with the
+        environment VIHMC_CANARY=1); syncs the device."""
+        n = ctypes.c_int64()
+        _lib.check(self.L.vihmc_plan_check_canaries(self._plan, ctypes.byref(n)), "vihmc_plan_check_canaries")
+        return n.value
+
     def timing_read(self):
         """(total ms, launches) over every recorded class; discards the events."""
         ms, n = ctypes.c_double(), ctypes.c_int64()
