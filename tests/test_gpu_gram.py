@@ -20,12 +20,12 @@ from oracle.deeponet_ref import deeponet_layout, np_logp_grad
 pytestmark = pytest.mark.gpu
 
 
-def engine_for(c, max_chains, device, min_chains=2):
+def engine_for(c, max_chains, device, min_chains=1):
     from vihmc.engine import DeepONetEngine, trunk_features
     p = c.prob
     eng = DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
                          c.prior_sd, c.loss, c.tau_out, max_chains=max_chains, device=device)
-    eng.option("gram_min_chains", min_chains)       # the tests run the Gram form from 2 chains (default 4)
+    eng.option("gram_min_chains", min_chains)       # the tests run the Gram form from 1 chain (default 4)
     return eng
 
 
@@ -35,10 +35,12 @@ def rel_norm(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
-@pytest.mark.parametrize("C", [2, 3, 16])
+@pytest.mark.parametrize("C", [1, 2, 3, 16])
 def test_gram_grad_burgers_matches_golden(C, cuda_device):
     """Full Burgers shape (N = 1000, P = 10,201, W = 100): every chain's Gram-form gradient against the reference
-    closure's golden (4,096-entry subsample + the norm of the whole gradient) and against the residual form."""
+    closure's golden (4,096-entry subsample + the norm of the whole gradient) and against the residual form. The
+    split-K sizes follow the plan's chain count: C = 1 (46 T_b slabs, 16 Gram-t slabs, 5 T_t splits), C = 2 (25, 16,
+    2), C = 3 (16, 16, 1), C = 16 (8, 8, 1)."""
     c = deeponet_case("deeponet_burgers")
     eng = engine_for(c, C, cuda_device)
     n = len(c.thetas)
@@ -85,7 +87,7 @@ def test_gram_option_off_is_the_residual_form(cuda_device):
     The form is decided per plan, not per call: a one-chain call on a 2-chain plan runs the Gram form too. The
     evaluation counters count both forms."""
     c = deeponet_case("deeponet_refshape")
-    eng = engine_for(c, 2, cuda_device)
+    eng = engine_for(c, 2, cuda_device, min_chains=2)
     th = torch.tensor(np.stack(c.thetas[:2]), device=cuda_device)
     _, gr = eng.logp_grad(th)
     assert eng.get_option("gram_min_chains") == 2

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     int list, u;
-    unit_of(blockIdx.x, A.upx_a, A.NG * A.S * A.C, A.C * A.S + A.C, list, u);
+    unit_of(blockIdx.x, A.upx_a, A.NG * A.S * A.C, A.C * A.St + A.C, list, u);
     if (list < 0) return;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     // decode the unit
@@ -168,12 +168,12 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         s = g / A.NG;
         ng = g - s * A.NG;
         kind = 0;
-    } else if (u < A.C * A.S) {
-        c = u / A.S;
-        s = u - c * A.S;
+    } else if (u < A.C * A.St) {
+        c = u / A.St;
+        s = u - c * A.St;
         kind = 1;
     } else {
-        c = u - A.C * A.S;
+        c = u - A.C * A.St;
         kind = 2;
     }
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain (unit-uniform)
@@ -182,6 +182,10 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     if (kind == 2) {
         src0 = A.bimg + c * A.bimg_cs;
         nb = A.nblkN;
+    } else if (kind == 1) {
+        kb0 = s * A.SLt;                  // Gram-t slab s: its own split (St, SLt) of the trunk blocks
+        nb = min(A.SLt, A.nblkP - kb0);
+        src0 = A.timg + c * A.timg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
     } else {
         kb0 = s * A.SL;
         nb = min(A.SL, A.nblkP - kb0);
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     __syncthreads();
     if (tid == 0) {
         __threadfence();
-        is_last = atomicAdd(A.cnt + c, 1u) == (unsigned)(A.S - 1);
+        is_last = atomicAdd(A.cnt + c, 1u) == (unsigned)(A.St - 1);
     }
     __syncthreads();
     if (!is_last) return;
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     for (int e = tid; e < 28 * 256; e += GR_CW * 64) {
         const int tile = e >> 8, within = e & 255, l = within >> 2, r = within & 3;
         double sum = 0.0;
-        for (int ss = 0; ss < A.S; ++ss)
+        for (int ss = 0; ss < A.St; ++ss)
             sum += __hip_atomic_load(part + ss * 28 * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int rem = tile, vt = 0;
         while (rem >= 7 - vt) rem -= 7 - vt++;
@@ -323,10 +327,12 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// k_gram_b: unit (pt, c), pt-major (the chains sharing one YB slab on one XCD). Waves own 32 trunk rows
-// p0 = 256 pt + 32 w; k runs over the branch blocks (A = YB rows, 16-B loads) and then 4 extension blocks
-// (A = Zt^ rows from the trunk image, k = feature v; B = -Gb blocks). dZt = -gscale acc (p < P, w < 100);
-// column 100 summed into the d ll / d b0 slot (pt * 8 + w) of the chain.
+// k_gram_b: unit (pt, sb, c), chains minor (the chains sharing one YB slab on one XCD). Waves own 32 trunk rows
+// p0 = 256 pt + 32 w; k runs over the split's branch blocks [sb SLB, (sb+1) SLB) (A = YB rows, 16-B loads) and, in
+// the last split, 4 extension blocks (A = Zt^ rows from the trunk image, k = feature v; B = -Gb blocks). With SB = 1
+// (enough chains to fill the chip) dZt = -gscale acc is written directly; with SB > 1 (few chains: 5 splits at one
+// chain) each split stores its partial tiles and the last one to finish sums them. Column 100 goes to the
+// d ll / d b0 slot (pt * 8 + w) of the chain.
 // ---------------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char* lds);
 
@@ -335,80 +341,123 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     int list, u;
     // the dZb epilogue units go last: they fill the half round the 640 T_t units leave at 16 chains (0.531 -> 0.519 ms,
     // profiles/r03z_ab_gram_epi_last.txt)
-    unit_of(blockIdx.x, A.upx_b, A.PT * A.C, A.C * ((A.N + 31) / 32), list, u, false);
+    unit_of(blockIdx.x, A.upx_b, A.PT * A.SB * A.C, A.C * ((A.N + 31) / 32), list, u, false);
     if (list < 0) return;
     if (list == 1) {                   // the dZb epilogue units fill the tail of the T_t rounds (k_gram_a is done)
         dzb_unit(A, u, lds);
         return;
     }
-    const int pt = u / A.C, c = u - pt * A.C;
+    // T_t unit (pt, sb, c): chains minor, so the chains sharing one YB slab (rows, k range) run on one XCD
+    const int g = u / A.C, c = u - g * A.C;
+    const int pt = g / A.SB, sb = g - pt * A.SB;
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-    const int nbm = A.nblkN, nb = nbm + 4;
+    const int kb0 = sb * A.SLB;
+    const int nbm = min(A.SLB, A.nblkN - kb0);            // this split's branch blocks (>= 1: SB = cdiv(nblkN, SLB))
+    const bool ext = sb == A.SB - 1;                      // the last split also runs the 4 extension blocks
+    const int nb = nbm + (ext ? 4 : 0);
+    const int p0 = 256 * pt + 32 * wave;
+    f32x4 acc[2][7];
     if (wave == GR_CW) {
-        const unsigned char* bsrc = A.bimg + c * A.bimg_cs;
+        const unsigned char* bsrc = A.bimg + c * A.bimg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
         const unsigned char* gsrc = A.gbimg + c * A.gbimg_cs;
         dma_role(lds, lane, nb, [&](int i) {
             return i < nbm ? bsrc + (int64_t)i * CONTRACT_SPLIT_BLOCK : gsrc + (int64_t)(i - nbm) * CONTRACT_SPLIT_BLOCK;
         });
-        return;
-    }
-    const int tro = bf6::tr_lane_off(lr, lg);
-    const int p0 = 256 * pt + 32 * wave;
-    const __bf16* yb = A.yb + (int64_t)(p0 + lr) * A.yb_ld + 8 * lg;
-    const int64_t rt16 = 16 * (int64_t)A.yb_ld;
-    bf16x8 a0[2][3], a1[2][3];
-    auto load_a = [&](bf16x8 (&a)[2][3], int i) __attribute__((always_inline)) {
-        const int ii = (GR_ABL & 1) ? 0 : min(i, nbm - 1);
+    } else {
+        const int tro = bf6::tr_lane_off(lr, lg);
+        const __bf16* yb = A.yb + (int64_t)(p0 + lr) * A.yb_ld + (int64_t)kb0 * 32 + 8 * lg;
+        const int64_t rt16 = 16 * (int64_t)A.yb_ld;
+        bf16x8 a0[2][3], a1[2][3];
+        auto load_a = [&](bf16x8 (&a)[2][3], int i) __attribute__((always_inline)) {
+            const int ii = (GR_ABL & 1) ? 0 : min(i, nbm - 1);
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl)
+                    a[rt][pl] = *reinterpret_cast<const bf16x8*>(yb + pl * A.yb_plane + rt * rt16 + 32 * ii);
+        };
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-                a[rt][pl] = *reinterpret_cast<const bf16x8*>(yb + pl * A.yb_plane + rt * rt16 + 32 * ii);
-    };
-    f32x4 acc[2][7];
+            for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
+            __syncthreads();
+            load_a(an, i + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc);
+        };
+        load_a(a0, 0);
+        int i = 0;
+        for (; i + 1 < nbm; i += 2) {
+            step(i, a0, a1);
+            step(i + 1, a1, a0);
+        }
+        if (i < nbm) step(i, a0, a1);
+        if (ext) {
+            // extension: acc -= Zt^ Gb (B blocks hold -Gb); A lane (lr, lg) = Zt^[p][32e + 4lg + j] (j < 4) and
+            // [32e + 16 + 4lg + j - 4] (j >= 4), two 8-B loads per plane from the trunk image row; rows past P read 0
+            const unsigned char* trow[2];
+            bool pval[2];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
-        __syncthreads();
-        load_a(an, i + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc);
-    };
-    load_a(a0, 0);
-    int i = 0;
-    for (; i + 1 < nbm; i += 2) {
-        step(i, a0, a1);
-        step(i + 1, a1, a0);
-    }
-    if (i < nbm) step(i, a0, a1);
-    // extension: acc -= Zt^ Gb (B blocks hold -Gb); A lane (lr, lg) = Zt^[p][32e + 4lg + j] (j < 4) and
-    // [32e + 16 + 4lg + j - 4] (j >= 4), two 8-B loads per plane from the trunk image row; rows past P read 0
-    const unsigned char* trow[2];
-    bool pval[2];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-        const int p = p0 + 16 * rt + lr;
-        pval[rt] = p < A.P;
-        const int pc = min(p, A.P - 1);
-        trow[rt] = A.timg + c * A.timg_cs + (int64_t)(pc / 32) * CONTRACT_SPLIT_BLOCK + (pc % 32) * bf6::PITCH;
-    }
-    for (int e = 0; e < 4; ++e) {
-        __syncthreads();
-        bf16x8 a[2][3];
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl) {
-                const unsigned char* q = trow[rt] + pl * GR_PL + 2 * (32 * e + 4 * lg);
-                bf16x4 lo = *reinterpret_cast<const bf16x4*>(q);
-                bf16x4 hi = e < 3 ? *reinterpret_cast<const bf16x4*>(q + 32) : bf16x4{};
-                if (!pval[rt]) lo = bf16x4{}, hi = bf16x4{};
-                a[rt][pl] = bf6::cat8(lo, hi);
+            for (int rt = 0; rt < 2; ++rt) {
+                const int p = p0 + 16 * rt + lr;
+                pval[rt] = p < A.P;
+                const int pc = min(p, A.P - 1);
+                trow[rt] = A.timg + c * A.timg_cs + (int64_t)(pc / 32) * CONTRACT_SPLIT_BLOCK + (pc % 32) * bf6::PITCH;
             }
-        mma_block(lds + ((nbm + e) % GR_NBUF) * GR_BLK, tro, a, acc);
+            for (int e = 0; e < 4; ++e) {
+                __syncthreads();
+                bf16x8 a[2][3];
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) {
+                        const unsigned char* q = trow[rt] + pl * GR_PL + 2 * (32 * e + 4 * lg);
+                        bf16x4 lo = *reinterpret_cast<const bf16x4*>(q);
+                        bf16x4 hi = e < 3 ? *reinterpret_cast<const bf16x4*>(q + 32) : bf16x4{};
+                        if (!pval[rt]) lo = bf16x4{}, hi = bf16x4{};
+                        a[rt][pl] = bf6::cat8(lo, hi);
+                    }
+                mma_block(lds + ((nbm + e) % GR_NBUF) * GR_BLK, tro, a, acc);
+            }
+        }
+    }
+    if (A.SB > 1) {
+        // split-K: this split's tiles as they stand; the last split of (pt, c) to finish sums the SB slabs in the
+        // order s = 0, 1, .. (from zero: the same sum whichever split arrives last) and runs the epilogue
+        const int64_t sstride = (int64_t)GR_CW * 14 * 256;
+        float* tp = A.tt_part + c * A.tt_cs + (int64_t)pt * A.SB * sstride + (int64_t)wave * 14 * 256 + 4 * lane;
+        if (wave < GR_CW) {
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+                for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(tp + sb * sstride + (rt * 7 + t) * 256) = acc[rt][t];
+        }
+        __shared__ int is_last;
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence();
+            is_last = atomicAdd(A.tcnt + c * A.PT + pt, 1u) == (unsigned)(A.SB - 1);
+        }
+        __syncthreads();
+        if (!is_last || wave == GR_CW) return;
+        __threadfence();
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                for (int ss = 0; ss < A.SB; ++ss) {
+                    const float* q = tp + ss * sstride + (rt * 7 + t) * 256;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] += __hip_atomic_load(q + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                acc[rt][t] = v;
+            }
+        if (tid == 0) A.tcnt[c * A.PT + pt] = 0u;
+    } else if (wave == GR_CW) {
+        return;
     }
     // dZt = -gscale acc
     const float sc = -A.gscale;
@@ -531,10 +580,13 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     if (a.ya_ld % 8 || a.yb_ld % 8 || a.NG * 256 < a.N || a.PT * 256 < a.P || a.nblkN * 32 < a.N ||
         a.nblkP * 32 < a.P || a.S * a.SL < a.nblkP || a.C < 1)
         return hipErrorInvalidValue;
-    const int n1 = a.NG * a.S * a.C, n2 = a.C * a.S + a.C;
+    if (a.SB < 1 || a.SLB < 1 || a.SB * a.SLB < a.nblkN || (a.SB - 1) * a.SLB >= a.nblkN || (a.SB > 1 && !a.tt_part))
+        return hipErrorInvalidValue;
+    if (a.St < 1 || a.SLt < 1 || a.St * a.SLt < a.nblkP || (a.St - 1) * a.SLt >= a.nblkP) return hipErrorInvalidValue;
+    const int n1 = a.NG * a.S * a.C, n2 = a.C * a.St + a.C;
     a.upx_a = (n1 + 7) / 8;
     const int gpx = (n2 + 7) / 8;
-    a.upx_b = (a.PT * a.C + 7) / 8;
+    a.upx_b = (a.PT * a.SB * a.C + 7) / 8;
     const int cpx = (a.C * ((a.N + 31) / 32) + 7) / 8;
     if (!a.aug_done) hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gram_a, dim3(8 * (a.upx_a + gpx)), dim3(GR_THREADS), GR_LDS, s, a);

@@ -156,7 +156,7 @@ struct GramArgs {
     const __bf16* ya; int64_t ya_plane; int32_t ya_ld;     // y [NG*256 rows n][32 nblkP], 3 planes, kpos order
     const __bf16* yb; int64_t yb_plane; int32_t yb_ld;     // y^T [PT*256 rows p][32 nblkN], 3 planes
     float* tb_part; int64_t tb_cs;                         // [C][S][NG][8 waves][14 tiles][256]
-    double* gt_part; int64_t gt_cs;                        // [C][S][49 tiles][256] (fp64 slab sums)
+    double* gt_part; int64_t gt_cs;                        // [C][St][28 tiles][256] (fp64 slab sums)
     float* gt; int64_t gt_cs2;                             // [C][112][112] Zt^T Zt^
     unsigned char* gbimg; int64_t gbimg_cs;                // [C][4 blocks] -Zb^T Zb^ pre-split
     uint32_t* cnt;                                         // [C] Gram-t slab counters (self-resetting)
@@ -166,6 +166,13 @@ struct GramArgs {
     double* stats; int64_t stats_cs;                       // (0, sum G) pairs, PT * 8 per chain
     const float* b0; int64_t b0_cs;
     int32_t N, P, ldz, NG, S, SL, PT, C;
+    int32_t St, SLt;                                       // Gram-t split of the trunk blocks (gt_part: St slabs)
+    // split-K of T_t = y^T Zb^ over the branch blocks (SB splits of SLB blocks; the last also runs the 4 extension
+    // blocks): SB > 1 writes partial slabs tt_part [C][PT][SB][8 waves][14 tiles][256] and the last split of (pt, c)
+    // to finish (counter tcnt[c * PT + pt], self-resetting) sums them in order s = 0.. and writes dZt
+    int32_t SB, SLB;
+    float* tt_part; int64_t tt_cs;
+    uint32_t* tcnt;
     int32_t upx_a, upx_b;                                  // set by launch_gram
     int32_t aug_done;                                      // feature 100 of both images already written
     float gscale;

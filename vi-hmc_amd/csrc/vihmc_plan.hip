@@ -167,7 +167,10 @@ struct vihmc_plan {
     __bf16* gya = nullptr;        // y [NG*256][32 nblkP], 3 planes (kpos order inside each 32-long p block)
     __bf16* gyb = nullptr;        // y^T [PT*256][32 nblkN], 3 planes
     int64_t gya_plane = 0, gyb_plane = 0;
-    int gya_ld = 0, gyb_ld = 0, gNG = 0, gS = 0, gSL = 0, gPT = 0;
+    int gya_ld = 0, gyb_ld = 0, gNG = 0, gS = 0, gSL = 0, gPT = 0, gSB = 1, gSLB = 1, gSt = 1, gSLt = 1;
+    float* gtt_part = nullptr;    // T_t split-K slabs (gSB > 1)
+    int64_t gtt_cs = 0;
+    uint32_t* gtcnt = nullptr;    // [C][PT] T_t split counters (self-resetting)
     float* gtb_part = nullptr;
     int64_t gtb_cs = 0;
     double* ggt_part = nullptr;
@@ -369,9 +372,22 @@ int gram_setup(vihmc_plan* p, int C) {
     const int nblkN = cdiv(p->N, CONTRACT_SPLIT_ROWS), nblkP = cdiv(p->P, CONTRACT_SPLIT_ROWS);
     p->gNG = cdiv(p->N, 256);
     p->gPT = cdiv(p->P, 256);
-    p->gS = 8;          // slabs 4 / 8 / 12: 0.499 / 0.496 / 0.523 ms per Gram-form evaluation (profiles/r03z_ab_gram_slabs.txt)
+    // split-K of the two data products sized for the plan's chain count, so one launch of each kernel fills the 256
+    // CUs: k_gram_a's NG S C T_b + S C Gram-t + C Gram-b units, k_gram_b's PT SB C T_t + C ceil(N/32) dZb units
+    // within one round where the chain count allows. At 16 chains: S = 8 (slabs 4 / 8 / 12: 0.499 / 0.496 / 0.523 ms
+    // per Gram-form evaluation, profiles/r03z_ab_gram_slabs.txt), SB = 1; at one chain S = 46, SB = 5.
+    p->gS = std::max(8, (256 - C) / ((p->gNG + 1) * C));
+    p->gS = std::min(p->gS, nblkP);
     p->gSL = cdiv(nblkP, p->gS);
     p->gS = cdiv(nblkP, p->gSL);
+    // Gram-t slabs: their own split (<= 16 slabs, so the last slab's fixed-order sum stays short)
+    p->gSt = std::min(p->gS, 16);
+    p->gSLt = cdiv(nblkP, p->gSt);
+    p->gSt = cdiv(nblkP, p->gSLt);
+    const int ngrp = cdiv(p->N, 32);
+    p->gSB = std::max(1, std::min(nblkN, (256 - std::min(ngrp * C, 128)) / (p->gPT * C)));
+    p->gSLB = cdiv(nblkN, p->gSB);
+    p->gSB = cdiv(nblkN, p->gSLB);
     p->gya_ld = 32 * nblkP;
     p->gyb_ld = 32 * nblkN;
     p->gya_plane = (int64_t)p->gNG * 256 * p->gya_ld;
@@ -380,13 +396,18 @@ int gram_setup(vihmc_plan* p, int C) {
     if (int rc = p->alloc(&p->gyb, 3 * p->gyb_plane)) return rc;
     p->gtb_cs = (int64_t)p->gS * p->gNG * 8 * 14 * 256;
     if (int rc = p->alloc(&p->gtb_part, p->gtb_cs * C)) return rc;
-    p->ggt_part_cs = (int64_t)p->gS * 28 * 256;          // the 28 upper tiles per slab
+    p->ggt_part_cs = (int64_t)p->gSt * 28 * 256;         // the 28 upper tiles per slab
     if (int rc = p->alloc(&p->ggt_part, p->ggt_part_cs * C)) return rc;
     if (int rc = p->alloc(&p->ggt, (int64_t)112 * 112 * C)) return rc;
     if (int rc = p->alloc(&p->ggb, (int64_t)4 * CONTRACT_SPLIT_BLOCK * C)) return rc;
     if (int rc = p->alloc(&p->gcnt, C)) return rc;
     p->gstats_cs = 2 * (int64_t)p->gPT * 8;
     if (int rc = p->alloc(&p->gstats, p->gstats_cs * C)) return rc;
+    if (p->gSB > 1) {
+        p->gtt_cs = (int64_t)p->gPT * p->gSB * 8 * 14 * 256;
+        if (int rc = p->alloc(&p->gtt_part, p->gtt_cs * C)) return rc;
+    }
+    if (int rc = p->alloc(&p->gtcnt, (int64_t)C * p->gPT)) return rc;
     if (int rc = p->alloc(&p->fit_dev, C)) return rc;
     if (int rc = p->alloc(&p->ysq_dev, 1)) return rc;
     if (int rc = p->alloc(&p->ysq_part, YSQ_PARTS)) return rc;
@@ -486,6 +507,13 @@ GramArgs gram_args(vihmc_plan* p, int C) {
     a.S = p->gS;
     a.SL = p->gSL;
     a.PT = p->gPT;
+    a.St = p->gSt;
+    a.SLt = p->gSLt;
+    a.SB = p->gSB;
+    a.SLB = p->gSLB;
+    a.tt_part = p->gtt_part;
+    a.tt_cs = p->gtt_cs;
+    a.tcnt = p->gtcnt;
     a.C = C;
     const float v = std::max(p->lik.tau_out, 1e-6f);
     a.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
