@@ -129,12 +129,15 @@ def test_gram_after_set_data_and_trunk_rows(cuda_device):
     parity.check("grad_relnorm", max(rel_norm(g[i], gr[i].cpu().numpy()) for i in range(2)), "set_trunk_rows")
 
 
-def test_gram_deterministic(cuda_device):
-    """Fixed-order reductions only (split-K slabs, Gram slabs, d ll / d b0 slots): repeated calls are bitwise equal."""
+@pytest.mark.parametrize("C", [1, 2, 4])
+def test_gram_deterministic(C, cuda_device):
+    """Fixed-order reductions only (split-K slabs, Gram slabs, T_t split-K with its arrival counter at C = 1 / 2, d ll /
+    d b0 slots): repeated calls are bitwise equal."""
     c = deeponet_case("deeponet_burgers")
-    eng = engine_for(c, 4, cuda_device)
-    th = torch.tensor(np.stack([c.thetas[i % len(c.thetas)] for i in range(4)]), device=cuda_device)
+    eng = engine_for(c, C, cuda_device)
+    th = torch.tensor(np.stack([c.thetas[i % len(c.thetas)] for i in range(C)]), device=cuda_device)
     a = eng.grad(th).clone()
+    assert eng.get_option("gram") & 2
     for _ in range(3):
         assert torch.equal(eng.grad(th), a)
 
@@ -260,6 +263,7 @@ def test_gram_guard_switch_per_chain(cuda_device):
     g = eng.grad(th)                                   # one snapshot only: no decision yet, all Gram
     assert eng.get_option("gram_chains") == 4
     g_all_gram = g.clone()
+    assert torch.equal(eng.grad(th), g_all_gram), "Gram form (split-K T_t at this shape) not deterministic"
     eng.logp_grad(th)                                  # snapshot 2
     g = eng.grad(th)
     assert eng.get_option("gram_chains") == 2, eng.get_option("gram_chains")
@@ -302,16 +306,18 @@ def test_gram_guard_fused_trajectory_bitwise_equals_stepwise(cuda_device):
     th0 = torch.tensor(np.stack([t, t] + [(t + 0.05 * rng.standard_normal(t.size)).astype(np.float32)
                                           for _ in range(2)]))
     out, counts = [], []
+    S, L = 5, 4
     for fused in (True, False):
         eng = _guard_engine(p, C, cuda_device)
         eng.fused_trajectory = fused
         eng.option("gram_evals", 0)
-        res = run_chains(EngineEvaluator(eng), th0, 5, 4, 1e-6, rng=ChainRNG(C, t.size, cuda_device, seeds=[7, 8, 9, 10]))
+        res = run_chains(EngineEvaluator(eng), th0, S, L, 1e-6, rng=ChainRNG(C, t.size, cuda_device, seeds=[7, 8, 9, 10]))
         out.append(res)
-        counts.append((eng.get_option("grad_evals"), eng.get_option("gram_evals"), eng.get_option("gram_chains")))
+        counts.append((eng.get_option("grad_evals"), eng.get_option("gram_evals"), eng.get_option("gram_chain_evals")))
     a, b = out
     assert counts[0] == counts[1], counts
-    assert counts[0][2] == 2, counts                   # the last inner evaluation ran Gram for 2 of the 4 chains
+    # trajectories 1-2: no decision yet (all 4 chains in Gram form); 3-5: the 2 teacher chains guarded
+    assert counts[0] == (1 + S * L, S * (L - 1), 2 * (L - 1) * 4 + 3 * (L - 1) * 2), counts
     assert torch.equal(a.accepted, b.accepted)
     assert torch.equal(a.samples[:, :int(a.counts.max())], b.samples[:, :int(b.counts.max())])
     assert torch.equal(a.logp_trace, b.logp_trace)

@@ -470,10 +470,15 @@ __global__ __launch_bounds__(BWD_THREADS, 4) void k_bwd_ws(BwdArgs args) {
     const float4* Hv = reinterpret_cast<const float4*>(H);
     float4* dt4 = reinterpret_cast<float4*>(dt);
     float4* ht4 = reinterpret_cast<float4*>(ht);
+// An idle slot (st = -1) loads row SUB, column 0 -- an address inside the tile -- and never stores it. (It used to
+// take the column from st & 255 = 255: a read 4 KB past the row, beyond the end of the delta / h buffer for narrow
+// layers. Harmless while the next allocation was mapped there; the illegal-address faults of round 3
+// (deeponet_odd_full) and round 4 (deeponet_small) were this read, found with VIHMC_GUARD=1: DESIGN §7.)
 #define VIHMC_BWD_LOAD(SUB)                                                                         \
     _Pragma("unroll") for (int v = 0; v < BWD_SLOTS; ++v) {                                         \
-        const int row = min((SUB) + (max(st[v], 0) >> 8), P.M - 1);                                 \
-        const int c4 = st[v] & 255;                                                                 \
+        const int sv = max(st[v], 0);                                                               \
+        const int row = min((SUB) + (sv >> 8), P.M - 1);                                            \
+        const int c4 = sv & 255;                                                                    \
         pf[v] = ((st_d >> v) & 1) ? Dv[(int64_t)row * (P.ldd >> 2) + c4]                            \
                                   : Hv[(int64_t)row * (P.ldh >> 2) + c4];                           \
     }

@@ -81,6 +81,43 @@ struct vihmc_plan {
         return e && std::atoi(e) != 0;
     }();
     std::vector<unsigned char*> canaries;
+    // bounds audit of reads too (environment VIHMC_GUARD=1 at plan creation): every buffer is placed at the end of its
+    // own HIP virtual-memory mapping, followed by an unmapped granule, so an access more than 255 B past its end
+    // faults at once instead of landing in a neighbouring allocation (debug runs only: each buffer takes whole granules)
+    bool guard_pages = [] {
+        const char* e = std::getenv("VIHMC_GUARD");
+        return e && std::atoi(e) != 0;
+    }();
+    struct VmmBuf {
+        void* base;
+        size_t total, mapped;
+        hipMemGenericAllocationHandle_t h;
+    };
+    std::vector<VmmBuf> vmm;
+    hipError_t vmm_alloc(void** out, size_t sz) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        hipMemAllocationProp prop{};
+        prop.type = hipMemAllocationTypePinned;
+        prop.location.type = hipMemLocationTypeDevice;
+        prop.location.id = dev;
+        size_t g = 0;
+        e = hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityMinimum);
+        if (e != hipSuccess) return e;
+        const size_t m = (sz + g - 1) / g * g, total = m + g;
+        VmmBuf b{nullptr, total, m, {}};
+        if ((e = hipMemAddressReserve(&b.base, total, 0, nullptr, 0)) != hipSuccess) return e;
+        if ((e = hipMemCreate(&b.h, m, &prop, 0)) != hipSuccess) return e;
+        if ((e = hipMemMap(b.base, m, 0, b.h, 0)) != hipSuccess) return e;
+        hipMemAccessDesc ad{};
+        ad.location = prop.location;
+        ad.flags = hipMemAccessFlagsProtReadWrite;
+        if ((e = hipMemSetAccess(b.base, m, &ad, 1)) != hipSuccess) return e;
+        vmm.push_back(b);
+        *out = static_cast<unsigned char*>(b.base) + (m - (sz + 255) / 256 * 256);
+        return hipSuccess;
+    }
 
     int32_t* smap_w = nullptr;
     int32_t* smap_wt = nullptr;
@@ -184,6 +221,7 @@ struct vihmc_plan {
     int last_gram_chains = 0;     // ... for this many of its chains (get_option gram_chains)
     int64_t n_grad_calls = 0;     // DeepONet gradient evaluations (calls) since creation / reset (get_option grad_evals)
     int64_t n_gram_calls = 0;     // ... of which ran the Gram form for some chain (get_option gram_evals)
+    int64_t n_gram_chain_evals = 0;   // chain-evaluations in Gram form (get_option gram_chain_evals)
     // Fit guard (plan option gram_guard = k: threshold 10^-k on sum r^2 / sum y^2; 0 = off). The Gram form's two
     // O(|y|) terms cancel to O(|S - y|), so its rounding grows like |y| / |S - y| (profiles/r04_gram_fit_table.json).
     // Every all-residual evaluation (end points, log-prob / value / forward calls) writes each chain's fit ratio and
@@ -225,7 +263,8 @@ struct vihmc_plan {
     int alloc(T** p, int64_t n) {
         void* v = nullptr;
         const size_t sz = std::max<int64_t>(n, 1) * sizeof(T);
-        hipError_t e = hipMalloc(&v, sz + (canary ? CANARY_BYTES : 0));
+        hipError_t e = guard_pages ? vmm_alloc(&v, sz + (canary ? CANARY_BYTES : 0))
+                                   : hipMalloc(&v, sz + (canary ? CANARY_BYTES : 0));
         if (e != hipSuccess) return fail(std::string("hipMalloc(") + std::to_string(sz) + "): " + hipGetErrorString(e), (int)e);
         e = hipMemset(v, 0, sz);
         if (e != hipSuccess) return fail(std::string("hipMemset: ") + hipGetErrorString(e), (int)e);
@@ -234,7 +273,7 @@ struct vihmc_plan {
             if (e != hipSuccess) return fail(std::string("hipMemset: ") + hipGetErrorString(e), (int)e);
             canaries.push_back(static_cast<unsigned char*>(v) + sz);
         }
-        allocs.push_back(v);
+        if (!guard_pages) allocs.push_back(v);
         bytes += sz;
         *p = static_cast<T*>(v);
         return 0;
@@ -252,6 +291,12 @@ struct vihmc_plan {
         for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
         if (cap_stream) (void)hipStreamDestroy(cap_stream);
         for (void* p : allocs) (void)hipFree(p);
+        if (!vmm.empty()) (void)hipDeviceSynchronize();
+        for (auto& b : vmm) {
+            (void)hipMemUnmap(b.base, b.mapped);
+            (void)hipMemRelease(b.h);
+            (void)hipMemAddressFree(b.base, b.total);
+        }
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     }
 
@@ -1120,6 +1165,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     if (want_grad) {
         ++p->n_grad_calls;
         if (gram) ++p->n_gram_calls;
+        if (gram) p->n_gram_chain_evals += C - n_resid;
     }
     int stats_waves = 0, stats_waves_res = 0;
     if (gram) {
@@ -1785,7 +1831,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1806,7 +1852,7 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
         p->n_snap = 0;
     }
     else if (k == "grad_evals" || k == "gram_evals") {          // counters: any value resets both
-        p->n_grad_calls = p->n_gram_calls = 0;
+        p->n_grad_calls = p->n_gram_calls = p->n_gram_chain_evals = 0;
         return 0;
     }
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
@@ -1833,6 +1879,7 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "grad_evals") *value = (int)std::min<int64_t>(p->n_grad_calls, INT32_MAX);
     else if (k == "gram_evals") *value = (int)std::min<int64_t>(p->n_gram_calls, INT32_MAX);
     else if (k == "gram_chains") *value = p->last_gram_chains;
+    else if (k == "gram_chain_evals") *value = (int)std::min<int64_t>(p->n_gram_chain_evals, INT32_MAX);
     else if (k == "gram_guard") *value = p->gram_guard;
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
