@@ -302,11 +302,10 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     // every wave (the DMA wave too) reaches the barriers below
     const double* part = A.gt_part + c * A.gt_cs;
     __shared__ int is_last;
+    // every wave's slab stores complete (agent scope) before the arrival is counted (see k_gram_b's split-K tail)
+    __threadfence();
     __syncthreads();
-    if (tid == 0) {
-        __threadfence();
-        is_last = atomicAdd(A.cnt + c, 1u) == (unsigned)(A.St - 1);
-    }
+    if (tid == 0) is_last = atomicAdd(A.cnt + c, 1u) == (unsigned)(A.St - 1);
     __syncthreads();
     if (!is_last) return;
     __threadfence();
@@ -435,11 +434,11 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
                 for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(tp + sb * sstride + (rt * 7 + t) * 256) = acc[rt][t];
         }
         __shared__ int is_last;
+        // every wave's slab stores complete (agent scope) before the arrival is counted: the barrier alone does not
+        // wait for other waves' outstanding stores, and a split that arrives last would read stale slabs
+        __threadfence();
         __syncthreads();
-        if (tid == 0) {
-            __threadfence();
-            is_last = atomicAdd(A.tcnt + c * A.PT + pt, 1u) == (unsigned)(A.SB - 1);
-        }
+        if (tid == 0) is_last = atomicAdd(A.tcnt + c * A.PT + pt, 1u) == (unsigned)(A.SB - 1);
         __syncthreads();
         if (!is_last || wave == GR_CW) return;
         __threadfence();
