@@ -191,21 +191,24 @@ def test_gram_loss_forms_vs_fp64_oracle(loss, tau, cuda_device):
 FIT_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gpurun_out", "gram_fit_table.json")
 
 
-@pytest.mark.parametrize("noise", [1e-2, 1e-3, 1e-4])
+@pytest.mark.parametrize("noise", [1e-2, 1e-3, 1e-4, 1e-5, 1e-6])
 def test_gram_precision_vs_fit(noise, cuda_device):
     """The Gram form's cancellation (Zb^ Gt vs y Zt^) grows with |y| / |S - y|: full Burgers shape, theta AT the
     teacher with the frozen weights at the teacher too (mu_noise = 0), so the residual is the data noise alone
-    (Sigma r^2 / Sigma y^2 ~ noise^2 / E y^2). Both forms against the fp64 oracle; the table of error vs fit goes to
+    (sum r^2 / sum y^2 ~ noise^2 / E y^2). A flat prior (sd 1e3) leaves the likelihood gradient, whose error the
+    cancellation affects. Both forms against the fp64 oracle; the table of error vs fit goes to
     gpurun_out/gram_fit_table.json (profiles/r04_gram_fit_table.json)."""
     from vihmc.data import deeponet_problem
     from vihmc.engine import DeepONetEngine, trunk_features
     from vihmc.layout import DeepONetSpec
     spec = DeepONetSpec()
+    sd = 1e3
     p = deeponet_problem(seed=3, noise=noise, mu_noise=0.0)
     th = p.teacher[p.grad_ind].astype(np.float32)
-    eng = DeepONetEngine(spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, 0.1, "NLL", 1.0,
+    eng = DeepONetEngine(spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, sd, "NLL", 1.0,
                          max_chains=2, device=cuda_device)
     eng.option("gram_min_chains", 2)
+    k_default = eng.get_option("gram_guard")
     eng.option("gram_guard", 0)                      # measure the Gram form itself at every fit
     tt = torch.tensor(np.stack([th, th]), device=cuda_device)
     gg = eng.grad(tt)[0].cpu().numpy()
@@ -214,22 +217,24 @@ def test_gram_precision_vs_fit(noise, cuda_device):
     gres = gres[0].cpu().numpy()
     lay = deeponet_layout(spec.in_branch, spec.width_branch, spec.depth_branch, spec.in_trunk, spec.width_trunk,
                           spec.depth_trunk, spec.out)
-    rl, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, 0.0, 0.1, "NLL", 1.0)
+    rl, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, 0.0, sd, "NLL", 1.0)
     # fit ratio from the log-likelihood: ll = -0.5 sum r^2 (v = 1: the log v term is 0); prior part removed
-    prior = float(np.sum(-0.5 * (th.astype(np.float64) / 0.1) ** 2 - np.log(0.1) - 0.5 * np.log(2 * np.pi)))
+    prior = float(np.sum(-0.5 * (th.astype(np.float64) / sd) ** 2 - np.log(sd) - 0.5 * np.log(2 * np.pi)))
     ssr = -2.0 * (rl - prior)
     fit = ssr / float(np.sum(p.y.astype(np.float64) ** 2))
     e_gram, e_res = rel_norm(gg, rg), rel_norm(gres, rg)
-    row = {"noise": noise, "fit_ratio": fit, "gram_relnorm": e_gram, "residual_relnorm": e_res,
-           "gram_elem": float(np.abs(gg - rg).max() / np.abs(rg).max()),
+    row = {"noise": noise, "fit_ratio": fit, "grad_norm": float(np.linalg.norm(rg)), "gram_relnorm": e_gram,
+           "residual_relnorm": e_res, "gram_elem": float(np.abs(gg - rg).max() / np.abs(rg).max()),
            "residual_elem": float(np.abs(gres - rg).max() / np.abs(rg).max())}
     print(json.dumps(row))
     os.makedirs(os.path.dirname(FIT_TABLE), exist_ok=True)
     rows = json.load(open(FIT_TABLE)) if os.path.exists(FIT_TABLE) else []
     rows = [r for r in rows if r["noise"] != noise] + [row]
     json.dump(sorted(rows, key=lambda r: -r["noise"]), open(FIT_TABLE, "w"), indent=1)
-    parity.check("grad_relnorm", e_gram, f"gram, noise {noise:g}, fit {fit:.1e}")
     parity.check("grad_relnorm", e_res, f"residual, noise {noise:g}, fit {fit:.1e}")
+    if fit >= 10.0 ** -k_default:
+        # above the default guard threshold the Gram form is what runs: it must stay within 4x the residual form
+        assert e_gram <= 4 * e_res + 1e-7, row
 
 
 def _teacher_problem():
