@@ -5,3 +5,6 @@ VIHMC_GUARD=1 timeout -k 10 600 python -u -m pytest tests -m gpu -v -x --timeout
 echo "guard tests rc=$rc"; tail -3 gpurun_out/${TAG}_guard_tests.txt
 [ $rc -ne 0 ] && exit $rc
 TAG=$TAG bash profiles/scripts/gpu_round.sh
+rc=$?
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u profiles/scripts/probes/probe_groups.py --groups 1 2 4 --steps 20 --reps 2 > gpurun_out/${TAG}_groups.txt 2>&1

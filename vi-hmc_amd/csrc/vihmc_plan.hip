@@ -19,6 +19,7 @@
 #include "vihmc.h"
 #include "vihmc_internal.h"
 #include <cstdlib>
+#include <cstdio>
 
 using namespace vihmc;
 
@@ -116,6 +117,14 @@ struct vihmc_plan {
         if ((e = hipMemSetAccess(b.base, m, &ad, 1)) != hipSuccess) return e;
         vmm.push_back(b);
         *out = static_cast<unsigned char*>(b.base) + (m - (sz + 255) / 256 * 256);
+        // VIHMC_GUARD_POISON=k: the bytes of allocation k (-1: every allocation) behind its end, up to the guard, read
+        // as NaN (0xFF) -- a kernel that uses them poisons its result (the alloc zeroes [ptr, ptr + sz) afterwards)
+        const char* pe = std::getenv("VIHMC_GUARD_POISON");
+        const int poison = pe ? std::atoi(pe) : -2;
+        const int k = (int)vmm.size() - 1;
+        if (poison == -1 || poison == k)
+            if ((e = hipMemset(b.base, 0xFF, m)) != hipSuccess) return e;
+        if (std::getenv("VIHMC_GUARD_VERBOSE")) fprintf(stderr, "vihmc guard alloc #%d: %zu bytes\n", k, sz);
         return hipSuccess;
     }
 
