@@ -231,10 +231,12 @@ def test_gram_precision_vs_fit(noise, cuda_device):
     rows = json.load(open(FIT_TABLE)) if os.path.exists(FIT_TABLE) else []
     rows = [r for r in rows if r["noise"] != noise] + [row]
     json.dump(sorted(rows, key=lambda r: -r["noise"]), open(FIT_TABLE, "w"), indent=1)
-    parity.check("grad_relnorm", e_res, f"residual, noise {noise:g}, fit {fit:.1e}")
-    if fit >= 10.0 ** -k_default:
-        # above the default guard threshold the Gram form is what runs: it must stay within 4x the residual form
-        assert e_gram <= 4 * e_res + 1e-7, row
+    # Both forms lose precision on the likelihood gradient at the same rate as the fit improves (the fp32 rounding of
+    # S - y or of the Gram terms, relative to a gradient that shrinks with the residual): measured gram / residual
+    # 1.65-1.7 from fit 0.13 down to 1.5e-9 (profiles/r04_gram_fit_table.json), so the Gram form is never more than
+    # ~2x the reference's own fp32 arithmetic. Bound: 2.5x at every fit, above and below the guard threshold.
+    assert e_gram <= 2.5 * e_res + 1e-7, row
+    assert k_default > 0
 
 
 def _teacher_problem():
@@ -321,8 +323,9 @@ def test_gram_guard_fused_trajectory_bitwise_equals_stepwise(cuda_device):
         counts.append((eng.get_option("grad_evals"), eng.get_option("gram_evals"), eng.get_option("gram_chain_evals")))
     a, b = out
     assert counts[0] == counts[1], counts
-    # trajectories 1-2: no decision yet (all 4 chains in Gram form); 3-5: the 2 teacher chains guarded
-    assert counts[0] == (1 + S * L, S * (L - 1), 2 * (L - 1) * 4 + 3 * (L - 1) * 2), counts
+    # trajectory 1: one snapshot only (the opening evaluation), all 4 chains in Gram form; trajectories 2-5 decide from
+    # the previous-but-one snapshot (the opening evaluation, then each end point): the 2 teacher chains guarded
+    assert counts[0] == (1 + S * L, S * (L - 1), (L - 1) * 4 + (S - 1) * (L - 1) * 2), counts
     assert torch.equal(a.accepted, b.accepted)
     assert torch.equal(a.samples[:, :int(a.counts.max())], b.samples[:, :int(b.counts.max())])
     assert torch.equal(a.logp_trace, b.logp_trace)

@@ -298,31 +298,28 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
             for (int r = 0; r < 4; ++r) part[((s * 28) + wave + 7 * q) * 256 + 4 * lane + r] = acc[q][r];
     }
     }
-    if (kind != 1) return;
-    // every wave (the DMA wave too) reaches the barriers below
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// k_gram_gt: Gt[c] = sum over the St Gram-t slabs, fixed order s = 0.. in fp64, both halves of the symmetric matrix.
+// One block per (28-tile group of 256 elements, chain). A launch of its own: the slabs are written by other workgroups
+// (on other XCDs, whose L2s are not coherent with each other inside a kernel), which a kernel boundary makes visible --
+// an in-kernel "last slab sums them" counter let the summing unit read a slab still in another XCD's L2
+// (nondeterministic branch gradients at 4 chains, profiles/r04e_nondet.txt).
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gram_gt(GramArgs A) {
+    const int tile = blockIdx.x, c = blockIdx.y;
+    if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
+    const int e = tile * 256 + threadIdx.x, within = threadIdx.x, l = within >> 2, r = within & 3;
     const double* part = A.gt_part + c * A.gt_cs;
-    __shared__ int is_last;
-    // every wave's slab stores complete (agent scope) before the arrival is counted (see k_gram_b's split-K tail)
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) is_last = atomicAdd(A.cnt + c, 1u) == (unsigned)(A.St - 1);
-    __syncthreads();
-    if (!is_last) return;
-    __threadfence();
-    // fixed-order sum of the S slabs -> gt[c][v][x]
+    double sum = 0.0;
+    for (int ss = 0; ss < A.St; ++ss) sum += part[ss * 28 * 256 + e];
+    int rem = tile, vt = 0;
+    while (rem >= 7 - vt) rem -= 7 - vt++;
+    const int t = vt + rem, v = 16 * vt + 4 * (l >> 4) + r, x = 16 * t + (l & 15);
     float* gt = A.gt + c * A.gt_cs2;
-    for (int e = tid; e < 28 * 256; e += GR_CW * 64) {
-        const int tile = e >> 8, within = e & 255, l = within >> 2, r = within & 3;
-        double sum = 0.0;
-        for (int ss = 0; ss < A.St; ++ss)
-            sum += __hip_atomic_load(part + ss * 28 * 256 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int rem = tile, vt = 0;
-        while (rem >= 7 - vt) rem -= 7 - vt++;
-        const int t = vt + rem, v = 16 * vt + 4 * (l >> 4) + r, x = 16 * t + (l & 15);
-        gt[v * 112 + x] = (float)sum;
-        gt[x * 112 + v] = (float)sum;        // the mirror (a diagonal tile writes its own elements twice)
-    }
-    if (tid == 0) A.cnt[c] = 0u;
+    gt[v * 112 + x] = (float)sum;
+    gt[x * 112 + v] = (float)sum;            // the mirror (a diagonal tile writes its own elements twice, same value)
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -334,6 +331,8 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
 // d ll / d b0 slot (pt * 8 + w) of the chain.
 // ---------------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char* lds);
+__device__ __forceinline__ void gram_tt_epilogue(const GramArgs& A, int c, int pt, int wave, int lane,
+                                                 const f32x4 (&acc)[2][7]);
 
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -423,41 +422,25 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
         }
     }
     if (A.SB > 1) {
-        // split-K: this split's tiles as they stand; the last split of (pt, c) to finish sums the SB slabs in the
-        // order s = 0, 1, .. (from zero: the same sum whichever split arrives last) and runs the epilogue
+        // split-K: this split's tiles as they stand; k_gram_tt sums the SB slabs in fixed order and writes dZt
+        if (wave == GR_CW) return;
         const int64_t sstride = (int64_t)GR_CW * 14 * 256;
-        float* tp = A.tt_part + c * A.tt_cs + (int64_t)pt * A.SB * sstride + (int64_t)wave * 14 * 256 + 4 * lane;
-        if (wave < GR_CW) {
-#pragma unroll
-            for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-                for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(tp + sb * sstride + (rt * 7 + t) * 256) = acc[rt][t];
-        }
-        __shared__ int is_last;
-        // every wave's slab stores complete (agent scope) before the arrival is counted: the barrier alone does not
-        // wait for other waves' outstanding stores, and a split that arrives last would read stale slabs
-        __threadfence();
-        __syncthreads();
-        if (tid == 0) is_last = atomicAdd(A.tcnt + c * A.PT + pt, 1u) == (unsigned)(A.SB - 1);
-        __syncthreads();
-        if (!is_last || wave == GR_CW) return;
-        __threadfence();
+        float* tp = A.tt_part + c * A.tt_cs + (int64_t)pt * A.SB * sstride + sb * sstride + (int64_t)wave * 14 * 256 +
+                    4 * lane;
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                for (int ss = 0; ss < A.SB; ++ss) {
-                    const float* q = tp + ss * sstride + (rt * 7 + t) * 256;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] += __hip_atomic_load(q + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                acc[rt][t] = v;
-            }
-        if (tid == 0) A.tcnt[c * A.PT + pt] = 0u;
-    } else if (wave == GR_CW) {
+            for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(tp + (rt * 7 + t) * 256) = acc[rt][t];
         return;
     }
+    if (wave == GR_CW) return;
+    gram_tt_epilogue(A, c, pt, wave, lane, acc);
+}
+
+__device__ __forceinline__ void gram_tt_epilogue(const GramArgs& A, int c, int pt, int wave, int lane,
+                                                 const f32x4 (&acc)[2][7]) {
+    const int lr = lane & 15, lg = lane >> 4;
+    const int p0 = 256 * pt + 32 * wave;
     // dZt = -gscale acc
     const float sc = -A.gscale;
     float* out = A.dzt + c * A.dzt_cs;
@@ -483,6 +466,26 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
         st[0] = 0.0;
         st[1] = (double)db;
     }
+}
+
+// T_t split-K sum (few chains, SB > 1): one 512-thread block per (256-row group pt, chain); wave w sums its 14 tiles over
+// the SB slabs in the order s = 0.. and runs the dZt epilogue. A launch of its own for the same reason as k_gram_gt.
+__global__ __launch_bounds__(512) void k_gram_tt(GramArgs A) {
+    const int pt = blockIdx.x, c = blockIdx.y;
+    if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t sstride = (int64_t)GR_CW * 14 * 256;
+    const float* tp = A.tt_part + c * A.tt_cs + (int64_t)pt * A.SB * sstride + (int64_t)wave * 14 * 256 + 4 * lane;
+    f32x4 acc[2][7];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            for (int ss = 0; ss < A.SB; ++ss) v += *reinterpret_cast<const f32x4*>(tp + ss * sstride + (rt * 7 + t) * 256);
+            acc[rt][t] = v;
+        }
+    gram_tt_epilogue(A, c, pt, wave, lane, acc);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -589,7 +592,9 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     const int cpx = (a.C * ((a.N + 31) / 32) + 7) / 8;
     if (!a.aug_done) hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gram_a, dim3(8 * (a.upx_a + gpx)), dim3(GR_THREADS), GR_LDS, s, a);
+    hipLaunchKernelGGL(k_gram_gt, dim3(28, a.C), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gram_b, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GR_LDS, s, a);
+    if (a.SB > 1) hipLaunchKernelGGL(k_gram_tt, dim3(a.PT, a.C), dim3(512), 0, s, a);
     return hipGetLastError();
 }
 

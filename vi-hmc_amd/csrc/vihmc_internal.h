@@ -159,7 +159,6 @@ struct GramArgs {
     double* gt_part; int64_t gt_cs;                        // [C][St][28 tiles][256] (fp64 slab sums)
     float* gt; int64_t gt_cs2;                             // [C][112][112] Zt^T Zt^
     unsigned char* gbimg; int64_t gbimg_cs;                // [C][4 blocks] -Zb^T Zb^ pre-split
-    uint32_t* cnt;                                         // [C] Gram-t slab counters (self-resetting)
     const float* zb; int64_t zb_cs;                        // fp32 Z_b rows [N][ldz]
     float* dzb; int64_t dzb_cs;                            // dZ_b [N][ldz]
     float* dzt; int64_t dzt_cs;                            // dZ_t [P][ldz]
@@ -168,11 +167,10 @@ struct GramArgs {
     int32_t N, P, ldz, NG, S, SL, PT, C;
     int32_t St, SLt;                                       // Gram-t split of the trunk blocks (gt_part: St slabs)
     // split-K of T_t = y^T Zb^ over the branch blocks (SB splits of SLB blocks; the last also runs the 4 extension
-    // blocks): SB > 1 writes partial slabs tt_part [C][PT][SB][8 waves][14 tiles][256] and the last split of (pt, c)
-    // to finish (counter tcnt[c * PT + pt], self-resetting) sums them in order s = 0.. and writes dZt
+    // blocks): SB > 1 writes partial slabs tt_part [C][PT][SB][8 waves][14 tiles][256] and k_gram_tt (a launch of its
+    // own) sums them in order s = 0.. and writes dZt
     int32_t SB, SLB;
     float* tt_part; int64_t tt_cs;
-    uint32_t* tcnt;
     int32_t upx_a, upx_b;                                  // set by launch_gram
     int32_t aug_done;                                      // feature 100 of both images already written
     float gscale;

@@ -216,14 +216,12 @@ struct vihmc_plan {
     int gya_ld = 0, gyb_ld = 0, gNG = 0, gS = 0, gSL = 0, gPT = 0, gSB = 1, gSLB = 1, gSt = 1, gSLt = 1;
     float* gtt_part = nullptr;    // T_t split-K slabs (gSB > 1)
     int64_t gtt_cs = 0;
-    uint32_t* gtcnt = nullptr;    // [C][PT] T_t split counters (self-resetting)
     float* gtb_part = nullptr;
     int64_t gtb_cs = 0;
     double* ggt_part = nullptr;
     int64_t ggt_part_cs = 0;
     float* ggt = nullptr;
     unsigned char* ggb = nullptr;
-    uint32_t* gcnt = nullptr;
     double* gstats = nullptr;
     int64_t gstats_cs = 0;
     bool last_gram = false;       // the last gradient evaluation ran the Gram form (get_option gram: bit 1)
@@ -304,7 +302,8 @@ struct vihmc_plan {
         for (auto& b : vmm) {
             (void)hipMemUnmap(b.base, b.mapped);
             (void)hipMemRelease(b.h);
-            (void)hipMemAddressFree(b.base, b.total);
+            // the address range stays reserved (debug runs only): a later plan's buffers never reuse a virtual range
+            // a previous plan mapped, so a stale translation cannot make one plan's access land in another's memory
         }
         for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     }
@@ -454,14 +453,12 @@ int gram_setup(vihmc_plan* p, int C) {
     if (int rc = p->alloc(&p->ggt_part, p->ggt_part_cs * C)) return rc;
     if (int rc = p->alloc(&p->ggt, (int64_t)112 * 112 * C)) return rc;
     if (int rc = p->alloc(&p->ggb, (int64_t)4 * CONTRACT_SPLIT_BLOCK * C)) return rc;
-    if (int rc = p->alloc(&p->gcnt, C)) return rc;
     p->gstats_cs = 2 * (int64_t)p->gPT * 8;
     if (int rc = p->alloc(&p->gstats, p->gstats_cs * C)) return rc;
     if (p->gSB > 1) {
         p->gtt_cs = (int64_t)p->gPT * p->gSB * 8 * 14 * 256;
         if (int rc = p->alloc(&p->gtt_part, p->gtt_cs * C)) return rc;
     }
-    if (int rc = p->alloc(&p->gtcnt, (int64_t)C * p->gPT)) return rc;
     if (int rc = p->alloc(&p->fit_dev, C)) return rc;
     if (int rc = p->alloc(&p->ysq_dev, 1)) return rc;
     if (int rc = p->alloc(&p->ysq_part, YSQ_PARTS)) return rc;
@@ -541,7 +538,6 @@ GramArgs gram_args(vihmc_plan* p, int C) {
     a.gt_cs2 = 112 * 112;
     a.gbimg = p->ggb;
     a.gbimg_cs = 4 * CONTRACT_SPLIT_BLOCK;
-    a.cnt = p->gcnt;
     const Net& b = p->nets[0];
     const Net& t = p->nets[1];
     a.zb = b.act + b.h_off.back();
@@ -567,7 +563,6 @@ GramArgs gram_args(vihmc_plan* p, int C) {
     a.SLB = p->gSLB;
     a.tt_part = p->gtt_part;
     a.tt_cs = p->gtt_cs;
-    a.tcnt = p->gtcnt;
     a.C = C;
     const float v = std::max(p->lik.tau_out, 1e-6f);
     a.gscale = p->lik.loss == VIHMC_LOSS_NLL ? -1.f / v : -p->lik.tau_out;
