@@ -131,15 +131,45 @@ def test_gram_after_set_data_and_trunk_rows(cuda_device):
 
 @pytest.mark.parametrize("C", [1, 2, 4])
 def test_gram_deterministic(C, cuda_device):
-    """Fixed-order reductions only (split-K slabs, Gram slabs, T_t split-K with its arrival counter at C = 1 / 2, d ll /
-    d b0 slots): repeated calls are bitwise equal."""
+    """Fixed-order reductions only (split-K slabs, Gram-t slabs in k_gram_gt, T_t split-K in k_gram_tt at C = 1 / 2,
+    d ll / d b0 slots), no element written twice: repeated calls are bitwise equal, with DISTINCT chains (identical
+    chains hide a cross-chain or per-chain race) and both backward forms, interleaved with log-prob evaluations."""
     c = deeponet_case("deeponet_burgers")
-    eng = engine_for(c, C, cuda_device)
-    th = torch.tensor(np.stack([c.thetas[i % len(c.thetas)] for i in range(C)]), device=cuda_device)
+    base = np.stack([c.thetas[i % len(c.thetas)] for i in range(C)]).astype(np.float32)
+    rng = np.random.default_rng(17)
+    th = torch.tensor(base + 0.02 * np.arange(C, dtype=np.float32)[:, None] * rng.standard_normal(base.shape,
+                                                                                                  dtype=np.float32),
+                      device=cuda_device)
+    for bwd_chain in (1, 0):
+        eng = engine_for(c, C, cuda_device)
+        eng.option("bwd_chain", bwd_chain)
+        a = eng.grad(th).clone()
+        assert eng.get_option("gram") & 2
+        for k in range(4):
+            if k == 2:
+                eng.logp_grad(th)
+            assert torch.equal(eng.grad(th), a), (bwd_chain, k)
+
+
+def test_gram_deterministic_teacher_shape(cuda_device):
+    """The shape that exposed the diagonal-tile race of Gt (64 functions x 21 x 21 points, 4 distinct chains, the
+    layer-wise backward; profiles/r04j_nondet3.txt: one element of chain 2's Gt written by two threads with values one
+    ulp apart, so calls differed at random): 6 repeated calls bitwise equal, Gt included."""
+    p = _teacher_problem()
+    C = 4
+    eng = _guard_engine(p, C, cuda_device)
+    eng.option("gram_guard", 0)
+    eng.option("bwd_chain", 0)
+    t = p.teacher[p.grad_ind].astype(np.float32)
+    rng = np.random.default_rng(4)
+    pert = [(t + 0.05 * rng.standard_normal(t.size)).astype(np.float32) for _ in range(2)]
+    th = torch.tensor(np.stack([t, t] + pert), device=cuda_device)
     a = eng.grad(th).clone()
+    gt0 = eng.debug_buffer("gram_gt")
     assert eng.get_option("gram") & 2
-    for _ in range(3):
+    for _ in range(5):
         assert torch.equal(eng.grad(th), a)
+        assert np.array_equal(eng.debug_buffer("gram_gt"), gt0)
 
 
 @pytest.mark.parametrize("form", ["gram", "residual"])

@@ -18,11 +18,12 @@
 // Kernels (one evaluation, C chains):
 //   k_gram_aug   feature 100 of the pre-split output images: 1 (branch rows < N), b0 (trunk rows < P) -- only when
 //                the fused forward did not write the images (it writes that column itself, FusedNet::aug)
-//   k_gram_a     T_b = y Zt^ over the trunk image (split-K partial slabs), Gt = Zt^T Zt^ (split-K, the last
-//                slab of a chain sums them in fixed order), Gb = Zb^T Zb^ (written negated, pre-split, as the
-//                B blocks of k_gram_b's extension)
+//   k_gram_a     T_b = y Zt^ over the trunk image (split-K partial slabs), Gt = Zt^T Zt^ (split-K slabs), Gb =
+//                Zb^T Zb^ (written negated, pre-split, as the B blocks of k_gram_b's extension)
+//   k_gram_gt    Gt = fixed-order sum of the Gram-t slabs (both halves)
 //   k_gram_b     dZt = -gscale (y^T Zb^ - Zt^ Gb) over the branch image + 4 extension blocks; d ll / d b0 slots
 //   (k_gram_b)   dZb = gscale (Zb^ Gt - sum_s T_b slab s): epilogue units after the T_t units of k_gram_b
+//   k_gram_tt    (T_t split over the branch blocks, few chains) fixed-order sum of the T_t slabs, dZt, d ll / d b0
 // Images: the contraction's pre-split blocks (k_split_blocks' layout, written by the fused forward): block =
 // 3 planes [32 rows][112 features] bf16, 224-B rows. The B operand (rows = k) is read with ds_read_b64_tr_b16
 // (bf6::tr_frag), which delivers k rows 4lg..4lg+3 and 16+4lg..+3 of a 32-row block; the pre-split data images
@@ -150,8 +151,8 @@ __global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
 //   T_b unit (ng, s, c): rows n0 = 256 ng + 32 w of wave w, trunk blocks [s SL, (s+1) SL): acc[2][7] tiles, stored
 //     tile-major to tb_part[c][s][ng][w][rt][t] (256 floats = 64 lanes x float4 each).
 //   Gram-t (c, s): the 28 upper 16x16 tiles of Zt^T Zt^ over the slab (4 per wave, A = the B fragment of the tile's
-//     row); stored to gt_part[c][s][28][256] (fp64); the last slab of chain c to finish sums the S slabs in order
-//     s = 0.. into gt[c] ([112 v][112 w] fp32, both halves) and resets the counter.
+//     row); stored to gt_part[c][s][28][256] (fp64); k_gram_gt sums the St slabs in order s = 0.. into gt[c]
+//     ([112 v][112 w] fp32, both halves).
 //   Gram-b (c): the same over all branch blocks; -Gb written pre-split as 4 blocks (rows v, k of the extension).
 // ---------------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
@@ -319,7 +320,10 @@ __global__ __launch_bounds__(256) void k_gram_gt(GramArgs A) {
     const int t = vt + rem, v = 16 * vt + 4 * (l >> 4) + r, x = 16 * t + (l & 15);
     float* gt = A.gt + c * A.gt_cs2;
     gt[v * 112 + x] = (float)sum;
-    gt[x * 112 + v] = (float)sum;            // the mirror (a diagonal tile writes its own elements twice, same value)
+    // the mirror, off the diagonal tiles only: a diagonal tile holds both (v, x) and (x, v), computed in different
+    // product orders (not bitwise equal), and mirroring there made two threads write one element with different
+    // values -- the nondeterminism of profiles/r04e_nondet.txt / r04j_nondet3.txt (one element of Gt, then dZb)
+    if (vt != t) gt[x * 112 + v] = (float)sum;
 }
 
 // ---------------------------------------------------------------------------------------------------------------

@@ -1905,6 +1905,39 @@ int vihmc_plan_check_canaries(vihmc_plan* p, int64_t* corrupted) {
     });
 }
 
+// diagnostics: copy one internal buffer (all chains) to host memory; dst == null returns its size in *bytes
+int vihmc_plan_debug_copy(vihmc_plan* p, const char* name, void* dst, int64_t* bytes) {
+    return guarded([&]() -> int {
+        if (!p || !name || !bytes) return fail("null argument");
+        if (p->kind != 0) return fail("vihmc_plan_debug_copy: DeepONet plans only");
+        const std::string k(name);
+        const void* src = nullptr;
+        int64_t n = 0;
+        const Net& b = p->nets[0];
+        const Net& t = p->nets[1];
+        const int64_t C = p->maxC;
+        if (k == "dzb") src = b.delta[0], n = 4 * b.delta_cs * C;
+        else if (k == "dzt") src = t.delta[0], n = 4 * t.delta_cs * C;
+        else if (k == "act_b") src = b.act, n = 4 * b.act_cs * C;
+        else if (k == "act_t") src = t.act, n = 4 * t.act_cs * C;
+        else if (k == "bimg") src = p->qsplitA, n = p->qsplitA_cs * C;
+        else if (k == "timg") src = p->qsplitB, n = p->qsplitB_cs * C;
+        else if (k == "gram_tb") src = p->gtb_part, n = 4 * p->gtb_cs * C;
+        else if (k == "gram_gt_part") src = p->ggt_part, n = 8 * p->ggt_part_cs * C;
+        else if (k == "gram_gt") src = p->ggt, n = 4 * 112 * 112 * C;
+        else if (k == "gram_gb") src = p->ggb, n = 4 * (int64_t)CONTRACT_SPLIT_BLOCK * C;
+        else if (k == "gram_tt") src = p->gtt_part, n = 4 * p->gtt_cs * C;
+        else if (k == "gram_stats") src = p->gstats, n = 8 * p->gstats_cs * C;
+        else return fail("vihmc_plan_debug_copy: unknown buffer " + k);
+        if (!src) n = 0;
+        *bytes = n;
+        if (!dst || !n) return 0;
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(dst, src, (size_t)n, hipMemcpyDeviceToHost));
+        return 0;
+    });
+}
+
 int vihmc_clock_stamp(uint64_t* out, void* stream) {
     return guarded([&]() -> int {
         if (!out) return fail("null argument");

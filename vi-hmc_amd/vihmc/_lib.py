@@ -75,6 +75,7 @@ SIGNATURES = {
     "vihmc_timing_reset": (c_int, [c_void_p]),
     "vihmc_clock_stamp": (c_int, [c_void_p, c_void_p]),
     "vihmc_plan_check_canaries": (c_int, [c_void_p, ctypes.POINTER(c_int64)]),
+    "vihmc_plan_debug_copy": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, ctypes.POINTER(c_int64)]),
     "vihmc_plan_destroy": (None, [c_void_p]),
     "vihmc_last_error": (c_char_p, []),
     "vihmc_version": (c_char_p, []),

@@ -292,6 +292,19 @@ class _Engine:
         _lib.check(self.L.vihmc_plan_check_canaries(self._plan, ctypes.byref(n)), "vihmc_plan_check_canaries")
         return n.value
 
+    def debug_buffer(self, name: str):
+        """vihmc_plan_debug_copy: the named internal buffer (all chains) as raw bytes (numpy uint8), or None when the
+        plan has not allocated it; syncs the device. Diagnostics only."""
+        import numpy as np
+        n = ctypes.c_int64()
+        _lib.check(self.L.vihmc_plan_debug_copy(self._plan, name.encode(), None, ctypes.byref(n)), "vihmc_plan_debug_copy")
+        if n.value == 0:
+            return None
+        out = np.empty(n.value, dtype=np.uint8)
+        _lib.check(self.L.vihmc_plan_debug_copy(self._plan, name.encode(), out.ctypes.data_as(ctypes.c_void_p),
+                                                ctypes.byref(n)), "vihmc_plan_debug_copy")
+        return out
+
     def timing_read(self):
         """(total ms, launches) over every recorded class; discards the events."""
         ms, n = ctypes.c_double(), ctypes.c_int64()
