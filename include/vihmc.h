@@ -229,8 +229,8 @@ int vihmc_plan_check_canaries(vihmc_plan* p, int64_t* corrupted);
 
 /* Diagnostics (new; no reference counterpart): synchronise the device and copy the named internal buffer of a
  * DeepONet plan (all max_chains chains) into host memory dst; dst == NULL only returns its size in *bytes (0: not
- * allocated). Names: dzb, dzt, act_b, act_t, bimg, timg, gram_tb, gram_gt_part, gram_gt, gram_gb, gram_tt,
- * gram_stats. */
+ * allocated). Names: dzb, dzt, act_b, act_t, bimg, timg, gram_tb, gram_tb_sum, gram_gt_part, gram_gb_part, gram_gt,
+ * gram_gb, gram_tt, gram_stats. */
 int vihmc_plan_debug_copy(vihmc_plan* p, const char* name, void* dst, int64_t* bytes);
 
 /* Measurement (new; no reference counterpart): enqueue on `stream` one stamp of the shader clock. out is DEVICE

@@ -18,9 +18,9 @@
 // Kernels (one evaluation, C chains):
 //   k_gram_aug   feature 100 of the pre-split output images: 1 (branch rows < N), b0 (trunk rows < P) -- only when
 //                the fused forward did not write the images (it writes that column itself, FusedNet::aug)
-//   k_gram_a     T_b = y Zt^ over the trunk image (split-K partial slabs), Gt = Zt^T Zt^ (split-K slabs), Gb =
-//                Zb^T Zb^ (written negated, pre-split, as the B blocks of k_gram_b's extension)
-//   k_gram_gt    Gt = fixed-order sum of the Gram-t slabs (both halves)
+//   k_gram_a     T_b = y Zt^ over the trunk image, Gt = Zt^T Zt^, Gb = Zb^T Zb^: split-K partial slabs
+//   k_gram_sum   fixed-order slab sums: Gt (both halves), -Gb pre-split as the B blocks of k_gram_b's extension,
+//                and (more than GRAM_TB_DIRECT T_b slabs) the T_b sum the dZb epilogue units read
 //   k_gram_b     dZt = -gscale (y^T Zb^ - Zt^ Gb) over the branch image + 4 extension blocks; d ll / d b0 slots
 //   (k_gram_b)   dZb = gscale (Zb^ Gt - sum_s T_b slab s): epilogue units after the T_t units of k_gram_b
 //   k_gram_tt    (T_t split over the branch blocks, few chains) fixed-order sum of the T_t slabs, dZt, d ll / d b0
@@ -58,20 +58,27 @@ __host__ __device__ inline int kpos(int k) { return k < 16 ? 8 * (k >> 2) + (k &
 #define GRAM_DMA_PIECES(SRC, BUF)                                                                             \
     for (int k = 0; k < GR_PIECES; ++k) bf6::glds16_asm((SRC) + k * 1024 + lane * 16, lds + (BUF) * GR_BLK + k * 1024);
 
-template <typename F>
-__device__ __forceinline__ void dma_role(unsigned char* lds, int lane, int nb, F src) {
+struct NoStamp {
+    __device__ void operator()(int, int) const {}
+};
+template <typename F, typename ST = NoStamp>
+__device__ __forceinline__ void dma_role(unsigned char* lds, int lane, int nb, F src, ST st = ST{}) {
     if (nb > 0) { GRAM_DMA_PIECES(src(0), 0) }
     if (nb > 1) { GRAM_DMA_PIECES(src(1), 1) }
     if (nb > 1) asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int i = 0; i < nb; ++i) {
         __syncthreads();
+        st(i, 0);
         if (i + 2 < nb) {
             GRAM_DMA_PIECES(src(i + 2), (i + 2) % GR_NBUF)
+            st(i, 1);
             asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
         } else {
+            st(i, 1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        st(i, 2);
     }
 }
 
@@ -84,16 +91,42 @@ __device__ __forceinline__ void load_b(const unsigned char* buf, int tro, int t,
 #define GR_ABL 0   // timing-only ablations (wrong results): 1 = no A loads in the main loops, 2 = one B fragment per
                    // block (no per-tile LDS reads), 3 = both
 #endif
+#ifndef GR_STAMP
+#define GR_STAMP 0   // timing-only instrumentation (variant builds): per-block phase stamps of k_gram_a's T_b units
+#endif
+#if GR_STAMP
+// every 16th T_b unit (at most 32) of the last k_gram_a launch: per wave (8 compute + the DMA wave) and k block
+// s_memtime at the barrier exit [0], after the next block's loads / DMA pieces are issued [1], after the block's MFMAs
+// are issued (compute) or the DMA wait (DMA wave) [2]; per workgroup s_memtime / s_memrealtime at start and end
+// (profiles/scripts/diag/stamps_gram.py)
+constexpr int GRS_WG = 32, GRS_BLK = 48;
+__device__ unsigned long long gr_stamps[GRS_WG][GR_CW + 1][GRS_BLK][3];
+__device__ unsigned long long gr_real[GRS_WG][2][2];
+#define GR_ST(I, K)                                                                                             \
+    if (gr_samp && lane == 0 && (I) < GRS_BLK) gr_stamps[gr_sidx][wave][(I)][(K)] = __builtin_amdgcn_s_memtime();
+#else
+#define GR_ST(I, K)
+#endif
+
 // one 32-long k block of a wave's 32 x 112 tile: B fragments of column tile t+1 read while tile t's 12 MFMAs run
 // (double-buffered fragments, so the wait before tile t's products leaves the next tile's reads in flight)
+// pre(t) runs before tile t's products: the T_b / T_t loops issue one of the next block's six A loads there, so
+// the loads spread over the block's MFMAs. Issued all at once after the barrier (with the DMA wave's 21 pieces), the
+// loads queued behind each other for ~1,200 cycles before the first MFMA of a 4,400-cycle block period (stamps:
+// profiles/r04s_stamps_gram.txt).
+struct NoPre {
+    __device__ void operator()(int) const {}
+};
+template <typename PRE = NoPre>
 __device__ __forceinline__ void mma_block(const unsigned char* buf, int tro, const bf16x8 (&a)[2][3],
-                                          f32x4 (&acc)[2][7]) {
+                                          f32x4 (&acc)[2][7], PRE pre = PRE{}) {
     bf16x8 b[2][3];
     load_b(buf, tro, 0, b[0]);
     if (GR_ABL & 2) load_b(buf, tro, 1, b[1]);
 #pragma unroll
     for (int t = 0; t < 7; ++t) {
         if (t < 6 && !(GR_ABL & 2)) load_b(buf, tro, t + 1, b[(t + 1) & 1]);
+        pre(t);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b[t & 1], acc[rt][t]);
     }
@@ -151,14 +184,15 @@ __global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
 //   T_b unit (ng, s, c): rows n0 = 256 ng + 32 w of wave w, trunk blocks [s SL, (s+1) SL): acc[2][7] tiles, stored
 //     tile-major to tb_part[c][s][ng][w][rt][t] (256 floats = 64 lanes x float4 each).
 //   Gram-t (c, s): the 28 upper 16x16 tiles of Zt^T Zt^ over the slab (4 per wave, A = the B fragment of the tile's
-//     row); stored to gt_part[c][s][28][256] (fp64); k_gram_gt sums the St slabs in order s = 0.. into gt[c]
+//     row); stored to gt_part[c][s][28][256] (fp64); k_gram_sum adds the St slabs up in order s = 0.. into gt[c]
 //     ([112 v][112 w] fp32, both halves).
-//   Gram-b (c): the same over all branch blocks; -Gb written pre-split as 4 blocks (rows v, k of the extension).
+//   Gram-b (c, s): the same over the branch blocks [s SLb, (s+1) SLb) into gb_part; k_gram_sum writes -Gb pre-split
+//     as 4 blocks (rows v, k of the extension).
 // ---------------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     int list, u;
-    unit_of(blockIdx.x, A.upx_a, A.NG * A.S * A.C, A.C * A.St + A.C, list, u);
+    unit_of(blockIdx.x, A.upx_a, A.NG * A.S * A.C, A.C * (A.St + A.Sb), list, u);
     if (list < 0) return;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     // decode the unit
@@ -174,15 +208,18 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         s = u - c * A.St;
         kind = 1;
     } else {
-        c = u - A.C * A.St;
+        const int u2 = u - A.C * A.St;
+        c = u2 / A.Sb;
+        s = u2 - c * A.Sb;
         kind = 2;
     }
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain (unit-uniform)
     const unsigned char* src0;
     int nb, kb0 = 0;
     if (kind == 2) {
-        src0 = A.bimg + c * A.bimg_cs;
-        nb = A.nblkN;
+        kb0 = s * A.SLb;                  // Gram-b slab s: SLb branch blocks
+        nb = min(A.SLb, A.nblkN - kb0);
+        src0 = A.bimg + c * A.bimg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
     } else if (kind == 1) {
         kb0 = s * A.SLt;                  // Gram-t slab s: its own split (St, SLt) of the trunk blocks
         nb = min(A.SLt, A.nblkP - kb0);
@@ -193,8 +230,21 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         src0 = A.timg + c * A.timg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
     }
     const int tro = bf6::tr_lane_off(lr, lg);
+#if GR_STAMP
+    const bool gr_samp = kind == 0 && (u & 15) == 0 && (u >> 4) < GRS_WG;
+    const int gr_sidx = u >> 4;
+    if (gr_samp && tid == 0) {
+        gr_real[gr_sidx][0][0] = __builtin_amdgcn_s_memtime();
+        gr_real[gr_sidx][0][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     if (wave == GR_CW) {
+#if GR_STAMP
+        dma_role(lds, lane, nb, [&](int i) { return src0 + (int64_t)i * CONTRACT_SPLIT_BLOCK; },
+                 [&](int i, int k) { GR_ST(i, k) });
+#else
         dma_role(lds, lane, nb, [&](int i) { return src0 + (int64_t)i * CONTRACT_SPLIT_BLOCK; });
+#endif
     } else if (kind == 0) {
         // ---------------- T_b = y Zt^ (A = YA rows, 16-B loads one block ahead in two register sets) ----------
         const int n0 = 256 * ng + 32 * wave;
@@ -216,9 +266,21 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
             for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
             __syncthreads();
-            load_a(an, i + 1);
-            __builtin_amdgcn_sched_barrier(0);     // issue the next block's A loads here, a whole block ahead
-            mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc);
+            GR_ST(i, 0)
+            const int ii = (GR_ABL & 1) ? 0 : min(i + 1, nb - 1);
+            GR_ST(i, 1)
+            // the next block's A loads, one per tile under this block's MFMAs
+            mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc, [&](int t) __attribute__((always_inline)) {
+                if (t < 6) {
+                    const int rt = t / 3, pl = t % 3;
+                    an[rt][pl] = *reinterpret_cast<const bf16x8*>(ya + pl * A.ya_plane + rt * rt16 + 32 * ii);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            });
+#if GR_STAMP
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            GR_ST(i, 2)
         };
         load_a(a0, 0);
         int i = 0;
@@ -232,6 +294,12 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
             for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(dst + (rt * 7 + t) * 256) = acc[rt][t];
+#if GR_STAMP
+        if (gr_samp && tid == 0) {
+            gr_real[gr_sidx][1][0] = __builtin_amdgcn_s_memtime();
+            gr_real[gr_sidx][1][1] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
     } else {
     // ---------------- Gram tiles: the 28 tiles (vt <= t) of the symmetric 112 x 112 matrix, 4 per wave ------------
     // Every element of Gt / Gb enters all N (P) rows of the other side's correction product, so its rounding error
@@ -265,34 +333,9 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
             }
         }
     }
-    if (kind == 2) {
-        // -Gb pre-split into the extension blocks: element (v, x) -> block v / 32, row v % 32, feature x; both halves
-        if (wave < 7) {
-            unsigned char* gb = A.gbimg + c * A.gbimg_cs;
-            auto put = [&](int v, int x, float val) __attribute__((always_inline)) {
-                const __bf16 p0 = (__bf16)val;
-                const float rr = val - (float)p0;
-                const __bf16 p1 = (__bf16)rr;
-                unsigned char* e = gb + (v / 32) * CONTRACT_SPLIT_BLOCK + (v % 32) * bf6::PITCH + 2 * x;
-                *reinterpret_cast<__bf16*>(e) = p0;
-                *reinterpret_cast<__bf16*>(e + GR_PL) = p1;
-                *reinterpret_cast<__bf16*>(e + 2 * GR_PL) = (__bf16)(rr - (float)p1);
-            };
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int v = 16 * tvt[q] + 4 * lg + r, x = 16 * tt[q] + lr;
-                    const float val = (float)-acc[q][r];
-                    put(v, x, val);
-                    if (tvt[q] != tt[q]) put(x, v, val);
-                }
-        }
-        return;
-    }
     if (wave < 7) {
-        // Gram-t slab s of chain c: the 28 upper tiles
-        double* part = A.gt_part + c * A.gt_cs;
+        // Gram-t / Gram-b slab s of chain c: the 28 upper tiles
+        double* part = kind == 1 ? A.gt_part + c * A.gt_cs : A.gb_part + c * A.gb_cs;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -302,28 +345,59 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// k_gram_gt: Gt[c] = sum over the St Gram-t slabs, fixed order s = 0.. in fp64, both halves of the symmetric matrix.
-// One block per (28-tile group of 256 elements, chain). A launch of its own: the slabs are written by other workgroups
-// (on other XCDs, whose L2s are not coherent with each other inside a kernel), which a kernel boundary makes visible --
-// an in-kernel "last slab sums them" counter let the summing unit read a slab still in another XCD's L2
-// (nondeterministic branch gradients at 4 chains, profiles/r04e_nondet.txt).
+// k_gram_sum: the slab sums, fixed order s = 0.. (fp64 for the Gram slabs), block (x, chain):
+//   x < 28       Gt tile x: Gt = sum of the St Gram-t slabs, fp32, both halves
+//   28 <= x < 56 Gb tile x - 28: -sum of the Sb Gram-b slabs, pre-split into the 4 extension blocks of k_gram_b
+//   x >= 56      (S > GRAM_TB_DIRECT only) 4 T_b tiles: tb_sum = sum of the S T_b slabs, for the dZb epilogue units
+// A launch of its own: the slabs come from workgroups on all 8 XCDs, and a kernel boundary makes them visible.
+// The mirror half is written off the diagonal tiles only: a diagonal tile holds both (v, x) and (x, v), computed in
+// different product orders (not bitwise equal), and mirroring there made two threads write one element with different
+// values -- the nondeterminism of profiles/r04e_nondet.txt / r04j_nondet3.txt (one element of Gt, then dZb).
 // ---------------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gram_gt(GramArgs A) {
-    const int tile = blockIdx.x, c = blockIdx.y;
+__global__ __launch_bounds__(256) void k_gram_sum(GramArgs A) {
+    const int x0 = blockIdx.x, c = blockIdx.y;
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
-    const int e = tile * 256 + threadIdx.x, within = threadIdx.x, l = within >> 2, r = within & 3;
-    const double* part = A.gt_part + c * A.gt_cs;
+    if (x0 >= 56) {
+        const int64_t sstride = (int64_t)A.NG * GR_CW * 14 * 256;
+        const int64_t e = ((int64_t)(x0 - 56) * 256 + threadIdx.x) * 4;
+        const float* src = A.tb_part + c * A.tb_cs + e;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 16
+        for (int ss = 0; ss < A.S; ++ss) v += *reinterpret_cast<const f32x4*>(src + ss * sstride);
+        *reinterpret_cast<f32x4*>(A.tb_sum + c * A.tbs_cs + e) = v;
+        return;
+    }
+    const bool gb = x0 >= 28;
+    const int tile = gb ? x0 - 28 : x0;
+    const int e = tile * 256 + threadIdx.x, l = threadIdx.x >> 2, r = threadIdx.x & 3;
+    const double* part = gb ? A.gb_part + c * A.gb_cs : A.gt_part + c * A.gt_cs;
+    const int ns = gb ? A.Sb : A.St;
     double sum = 0.0;
-    for (int ss = 0; ss < A.St; ++ss) sum += part[ss * 28 * 256 + e];
+#pragma unroll 16
+    for (int ss = 0; ss < ns; ++ss) sum += part[ss * 28 * 256 + e];
     int rem = tile, vt = 0;
     while (rem >= 7 - vt) rem -= 7 - vt++;
     const int t = vt + rem, v = 16 * vt + 4 * (l >> 4) + r, x = 16 * t + (l & 15);
-    float* gt = A.gt + c * A.gt_cs2;
-    gt[v * 112 + x] = (float)sum;
-    // the mirror, off the diagonal tiles only: a diagonal tile holds both (v, x) and (x, v), computed in different
-    // product orders (not bitwise equal), and mirroring there made two threads write one element with different
-    // values -- the nondeterminism of profiles/r04e_nondet.txt / r04j_nondet3.txt (one element of Gt, then dZb)
-    if (vt != t) gt[x * 112 + v] = (float)sum;
+    if (!gb) {
+        float* gt = A.gt + c * A.gt_cs2;
+        gt[v * 112 + x] = (float)sum;
+        if (vt != t) gt[x * 112 + v] = (float)sum;
+        return;
+    }
+    // -Gb pre-split: element (v, x) -> extension block v / 32, row v % 32, feature x
+    unsigned char* gbi = A.gbimg + c * A.gbimg_cs;
+    const float val = (float)-sum;
+    auto put = [&](int vv, int xx) __attribute__((always_inline)) {
+        const __bf16 p0 = (__bf16)val;
+        const float rr = val - (float)p0;
+        const __bf16 p1 = (__bf16)rr;
+        unsigned char* q = gbi + (vv / 32) * CONTRACT_SPLIT_BLOCK + (vv % 32) * bf6::PITCH + 2 * xx;
+        *reinterpret_cast<__bf16*>(q) = p0;
+        *reinterpret_cast<__bf16*>(q + GR_PL) = p1;
+        *reinterpret_cast<__bf16*>(q + 2 * GR_PL) = (__bf16)(rr - (float)p1);
+    };
+    put(v, x);
+    if (vt != t) put(x, v);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -385,9 +459,15 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
             for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
             __syncthreads();
-            load_a(an, i + 1);
-            __builtin_amdgcn_sched_barrier(0);
-            mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc);
+            const int ii = (GR_ABL & 1) ? 0 : min(i + 1, nbm - 1);
+            // the next block's A loads, one per tile under this block's MFMAs (see mma_block)
+            mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc, [&](int t) __attribute__((always_inline)) {
+                if (t < 6) {
+                    const int rt = t / 3, pl = t % 3;
+                    an[rt][pl] = *reinterpret_cast<const bf16x8*>(yb + pl * A.yb_plane + rt * rt16 + 32 * ii);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            });
         };
         load_a(a0, 0);
         int i = 0;
@@ -472,23 +552,32 @@ __device__ __forceinline__ void gram_tt_epilogue(const GramArgs& A, int c, int p
     }
 }
 
-// T_t split-K sum (few chains, SB > 1): one 512-thread block per (256-row group pt, chain); wave w sums its 14 tiles over
-// the SB slabs in the order s = 0.. and runs the dZt epilogue. A launch of its own for the same reason as k_gram_gt.
-__global__ __launch_bounds__(512) void k_gram_tt(GramArgs A) {
-    const int pt = blockIdx.x, c = blockIdx.y;
+// T_t split-K sum (few chains, SB > 1): one one-wave block per (256-row group pt, 32-row wave slot w, chain) sums
+// its 14 tiles over the SB slabs in the order s = 0.. and runs the dZt epilogue. A launch of its own (k_gram_sum).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void k_gram_tt(GramArgs A) {
+    const int pt = blockIdx.x >> 3, wave = blockIdx.x & 7, c = blockIdx.y, lane = threadIdx.x;
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t sstride = (int64_t)GR_CW * 14 * 256;
     const float* tp = A.tt_part + c * A.tt_cs + (int64_t)pt * A.SB * sstride + (int64_t)wave * 14 * 256 + 4 * lane;
     f32x4 acc[2][7];
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-        for (int t = 0; t < 7; ++t) {
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            for (int ss = 0; ss < A.SB; ++ss) v += *reinterpret_cast<const f32x4*>(tp + ss * sstride + (rt * 7 + t) * 256);
-            acc[rt][t] = v;
-        }
+        for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // slab-major: the 14 tile loads of one slab are issued together (a tile-major loop waited out one load latency
+    // per (tile, slab): 24 us at one chain, profiles/r04q_c1_kstats.txt); per element the order is still s = 0..
+    for (int ss = 0; ss < A.SB; ++ss) {
+        f32x4 v[2][7];
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) v[rt][t] = *reinterpret_cast<const f32x4*>(tp + ss * sstride + (rt * 7 + t) * 256);
+        __builtin_amdgcn_sched_barrier(0);        // keep the 14 loads ahead of the adds (hipcc paired them)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) acc[rt][t] += v[rt][t];
+    }
     gram_tt_epilogue(A, c, pt, wave, lane, acc);
 }
 
@@ -518,13 +607,16 @@ __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char
     }
     __syncthreads();
     const int n32 = 32 * m, ng = n32 / 256, w8 = (n32 % 256) / 32;
-    const float* tb = A.tb_part + c * A.tb_cs + ((int64_t)(ng * GR_CW + w8) * 14) * 256 + 4 * lane;
+    const bool pre = A.tb_sum != nullptr;                 // S > GRAM_TB_DIRECT: k_gram_sum added the slabs up
+    const float* tb = (pre ? A.tb_sum + c * A.tbs_cs : A.tb_part + c * A.tb_cs) +
+                      ((int64_t)(ng * GR_CW + w8) * 14) * 256 + 4 * lane;
     const int64_t sstride = (int64_t)A.NG * GR_CW * 14 * 256;
+    const int nslab = pre ? 1 : A.S;
     float* out = A.dzb + c * A.dzb_cs;
     for (int tile = wv; tile < 14; tile += GR_THREADS / 64) {
         const int rt = tile / 7, t = tile - rt * 7;
         f32x4 ts = {0.f, 0.f, 0.f, 0.f};
-        for (int ss = 0; ss < A.S; ++ss) {
+        for (int ss = 0; ss < nslab; ++ss) {
             const f32x4 v = *reinterpret_cast<const f32x4*>(tb + ss * sstride + tile * 256);
             ts += v;
         }
@@ -578,8 +670,17 @@ hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya
 }
 
 
+#if GR_STAMP
+extern "C" int vihmc_debug_gram_stamps(void* stamps, size_t stamp_bytes, void* real, size_t real_bytes) {
+    if (stamp_bytes != sizeof(gr_stamps) || real_bytes != sizeof(gr_real)) return -1;
+    hipError_t e = hipMemcpyFromSymbol(stamps, HIP_SYMBOL(gr_stamps), stamp_bytes, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(real, HIP_SYMBOL(gr_real), real_bytes, 0, hipMemcpyDeviceToHost);
+    return (int)e;
+}
+#endif
+
 // timing-only switches this translation unit was built with (0 = product build)
-int diag_switches_gram() { return GR_ABL; }
+int diag_switches_gram() { return GR_ABL | (GR_STAMP << 8); }
 
 hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     GramArgs a = a0;
@@ -589,16 +690,19 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     if (a.SB < 1 || a.SLB < 1 || a.SB * a.SLB < a.nblkN || (a.SB - 1) * a.SLB >= a.nblkN || (a.SB > 1 && !a.tt_part))
         return hipErrorInvalidValue;
     if (a.St < 1 || a.SLt < 1 || a.St * a.SLt < a.nblkP || (a.St - 1) * a.SLt >= a.nblkP) return hipErrorInvalidValue;
-    const int n1 = a.NG * a.S * a.C, n2 = a.C * a.St + a.C;
+    if (a.Sb < 1 || a.SLb < 1 || a.Sb * a.SLb < a.nblkN || (a.Sb - 1) * a.SLb >= a.nblkN || !a.gb_part)
+        return hipErrorInvalidValue;
+    if (a.S > GRAM_TB_DIRECT ? !a.tb_sum : a.tb_sum != nullptr) return hipErrorInvalidValue;
+    const int n1 = a.NG * a.S * a.C, n2 = a.C * (a.St + a.Sb);
     a.upx_a = (n1 + 7) / 8;
     const int gpx = (n2 + 7) / 8;
     a.upx_b = (a.PT * a.SB * a.C + 7) / 8;
     const int cpx = (a.C * ((a.N + 31) / 32) + 7) / 8;
     if (!a.aug_done) hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gram_a, dim3(8 * (a.upx_a + gpx)), dim3(GR_THREADS), GR_LDS, s, a);
-    hipLaunchKernelGGL(k_gram_gt, dim3(28, a.C), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gram_sum, dim3(56 + (a.tb_sum ? a.NG * 28 : 0), a.C), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gram_b, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GR_LDS, s, a);
-    if (a.SB > 1) hipLaunchKernelGGL(k_gram_tt, dim3(a.PT, a.C), dim3(512), 0, s, a);
+    if (a.SB > 1) hipLaunchKernelGGL(k_gram_tt, dim3(a.PT * GR_CW, a.C), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

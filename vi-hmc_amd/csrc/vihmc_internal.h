@@ -157,6 +157,8 @@ struct GramArgs {
     const __bf16* yb; int64_t yb_plane; int32_t yb_ld;     // y^T [PT*256 rows p][32 nblkN], 3 planes
     float* tb_part; int64_t tb_cs;                         // [C][S][NG][8 waves][14 tiles][256]
     double* gt_part; int64_t gt_cs;                        // [C][St][28 tiles][256] (fp64 slab sums)
+    double* gb_part; int64_t gb_cs; int32_t Sb, SLb;       // [C][Sb][28 tiles][256] Gram-b slabs of SLb branch blocks
+    float* tb_sum; int64_t tbs_cs;                         // [C][NG][8][14][256] sum of the S T_b slabs (S > 8), else null
     float* gt; int64_t gt_cs2;                             // [C][112][112] Zt^T Zt^
     unsigned char* gbimg; int64_t gbimg_cs;                // [C][4 blocks] -Zb^T Zb^ pre-split
     const float* zb; int64_t zb_cs;                        // fp32 Z_b rows [N][ldz]
@@ -176,6 +178,7 @@ struct GramArgs {
     float gscale;
     int32_t sel; ChainBits bits;                           // sel = 1: chains whose bit is set exit (residual form)
 };
+constexpr int GRAM_TB_DIRECT = 8;   // up to this many T_b slabs the dZb epilogue units sum them themselves
 hipError_t launch_gram(const GramArgs& a, hipStream_t s);
 hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld, __bf16* yb,
                             int64_t yb_plane, int yb_ld, hipStream_t s);

@@ -220,6 +220,11 @@ struct vihmc_plan {
     int64_t gtb_cs = 0;
     double* ggt_part = nullptr;
     int64_t ggt_part_cs = 0;
+    int gSb = 1, gSLb = 1;        // Gram-b slabs (ggb_part) of gSLb branch blocks
+    double* ggb_part = nullptr;
+    int64_t ggb_part_cs = 0;
+    float* gtb_sum = nullptr;     // summed T_b slabs (gS > GRAM_TB_DIRECT)
+    int64_t gtbs_cs = 0;
     float* ggt = nullptr;
     unsigned char* ggb = nullptr;
     double* gstats = nullptr;
@@ -433,10 +438,13 @@ int gram_setup(vihmc_plan* p, int C) {
     p->gS = std::min(p->gS, nblkP);
     p->gSL = cdiv(nblkP, p->gS);
     p->gS = cdiv(nblkP, p->gSL);
-    // Gram-t slabs: their own split (<= 16 slabs, so the last slab's fixed-order sum stays short)
-    p->gSt = std::min(p->gS, 16);
-    p->gSLt = cdiv(nblkP, p->gSt);
-    p->gSt = cdiv(nblkP, p->gSLt);
+    // Gram-t slabs: the T_b split (k_gram_sum adds them up); Gram-b slabs: the branch blocks cut to the same slab
+    // length, so no k_gram_a unit runs longer than a T_b unit (one unit of all nblkN blocks at one chain set
+    // k_gram_a's time: 45 us, profiles/r04n_c1)
+    p->gSt = p->gS;
+    p->gSLt = p->gSL;
+    p->gSLb = std::min(p->gSL, nblkN);
+    p->gSb = cdiv(nblkN, p->gSLb);
     const int ngrp = cdiv(p->N, 32);
     p->gSB = std::max(1, std::min(nblkN, (256 - std::min(ngrp * C, 128)) / (p->gPT * C)));
     p->gSLB = cdiv(nblkN, p->gSB);
@@ -451,6 +459,13 @@ int gram_setup(vihmc_plan* p, int C) {
     if (int rc = p->alloc(&p->gtb_part, p->gtb_cs * C)) return rc;
     p->ggt_part_cs = (int64_t)p->gSt * 28 * 256;         // the 28 upper tiles per slab
     if (int rc = p->alloc(&p->ggt_part, p->ggt_part_cs * C)) return rc;
+    p->ggb_part_cs = (int64_t)p->gSb * 28 * 256;
+    if (int rc = p->alloc(&p->ggb_part, p->ggb_part_cs * C)) return rc;
+    // more than GRAM_TB_DIRECT T_b slabs: k_gram_sum adds them up once (fixed order) for the dZb epilogue units
+    if (p->gS > GRAM_TB_DIRECT) {
+        p->gtbs_cs = (int64_t)p->gNG * 8 * 14 * 256;
+        if (int rc = p->alloc(&p->gtb_sum, p->gtbs_cs * C)) return rc;
+    }
     if (int rc = p->alloc(&p->ggt, (int64_t)112 * 112 * C)) return rc;
     if (int rc = p->alloc(&p->ggb, (int64_t)4 * CONTRACT_SPLIT_BLOCK * C)) return rc;
     p->gstats_cs = 2 * (int64_t)p->gPT * 8;
@@ -534,6 +549,12 @@ GramArgs gram_args(vihmc_plan* p, int C) {
     a.tb_cs = p->gtb_cs;
     a.gt_part = p->ggt_part;
     a.gt_cs = p->ggt_part_cs;
+    a.gb_part = p->ggb_part;
+    a.gb_cs = p->ggb_part_cs;
+    a.Sb = p->gSb;
+    a.SLb = p->gSLb;
+    a.tb_sum = p->gtb_sum;
+    a.tbs_cs = p->gtbs_cs;
     a.gt = p->ggt;
     a.gt_cs2 = 112 * 112;
     a.gbimg = p->ggb;
@@ -1924,6 +1945,8 @@ int vihmc_plan_debug_copy(vihmc_plan* p, const char* name, void* dst, int64_t* b
         else if (k == "timg") src = p->qsplitB, n = p->qsplitB_cs * C;
         else if (k == "gram_tb") src = p->gtb_part, n = 4 * p->gtb_cs * C;
         else if (k == "gram_gt_part") src = p->ggt_part, n = 8 * p->ggt_part_cs * C;
+        else if (k == "gram_gb_part") src = p->ggb_part, n = 8 * p->ggb_part_cs * C;
+        else if (k == "gram_tb_sum") src = p->gtb_sum, n = 4 * p->gtbs_cs * C;
         else if (k == "gram_gt") src = p->ggt, n = 4 * 112 * 112 * C;
         else if (k == "gram_gb") src = p->ggb, n = 4 * (int64_t)CONTRACT_SPLIT_BLOCK * C;
         else if (k == "gram_tt") src = p->gtt_part, n = 4 * p->gtt_cs * C;
