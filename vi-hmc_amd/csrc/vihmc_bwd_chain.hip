@@ -9,14 +9,14 @@
 // per evaluation and bitwise equal: every product and every accumulation order is k_bwd_bf2's.
 //
 // One 768-thread workgroup (8 dX + 4 dW waves, 3 per SIMD) per 64-row chunk of one net of one chain -- the
-// plan's chunk when a single chain's rows fill the chip in one round (C = 1: 16 + 160 workgroups). LDS (85 KB):
-//   2 sub-tiles x [delta_j planes [3][32][224 B] | h_{j-1} planes [3][32][224 B] | delta_j fp32 tail [32][4]]
+// plan's chunk when a single chain's rows fill the chip in one round (C = 1: 16 + 160 workgroups). LDS (127 KB):
+//   2 sub-tiles x [delta_j planes [3][32][224 B] | delta_j fp32 tail [32][4]], 2 h sets x 2 sub-tiles x planes
 // W_j^T never touches LDS: each dX wave keeps the fragments of its two input tiles in registers, loaded from the
 // pre-split W^T image (BWD_WTIMG, kept current by the scatter) right after its last MFMA of the layer before, so
 // they land while the workgroup writes the next deltas.
-// Per layer: [A] the dX waves issue the loads of the next h rows, compute delta_{j-1} (kept in registers) and
-// load the next W^T fragments, while the dW waves compute the weight gradient of both sub-tiles; [B] the dX waves
-// split delta_{j-1} and the next h rows into the planes, the dW waves store the partial slab; loop.
+// Per layer: [A] the dX waves issue the loads of the next h rows, compute delta_{j-1} (kept in registers), load the
+// next W^T fragments and split the next h rows into the other h set, while the dW waves compute the weight gradient
+// of both sub-tiles; [B] the dX waves split delta_{j-1} into the planes, the dW waves store the partial slab; loop.
 #include "vihmc_internal.h"
 #include "vihmc_bf16x6.h"
 #include <type_traits>
@@ -35,12 +35,17 @@ constexpr int CH_SUB = BWD_SUB;                        // 32 rows per sub-tile
 constexpr int CH_ROWS = 2 * CH_SUB;                    // rows per workgroup
 constexpr int CH_PITCH = bf6::PITCH;                   // 224 B
 constexpr int CH_PLANE = CH_SUB * CH_PITCH;            // 7168
+// LDS: per sub-tile s a delta buffer [planes [3][32][224 B] | fp32 tail [32][4]] at s CH_BUF, then two h sets
+// (k = 0, 1) of per-sub-tile planes [3][32][224 B] at CH_HOFF + (2 k + s) CH_HSUB: layer j reads h_{j-1} from set
+// k while the dX waves write h_{j-2} into set k ^ 1 before barrier B (their slack while the dW waves finish), so the
+// write phase after B only splits the next deltas
 constexpr int CH_DP = 0;
-constexpr int CH_HP = 3 * CH_PLANE;
-constexpr int CH_DT = 6 * CH_PLANE;
-constexpr int CH_BUF = CH_DT + CH_SUB * 16;            // 43520 per sub-tile
-constexpr int CH_LDS = 2 * CH_BUF;                     // 87040
-static_assert(CH_BUF + 2 * CH_PLANE < 65536, "LDS store offsets fit the ds_write immediate");
+constexpr int CH_DT = 3 * CH_PLANE;
+constexpr int CH_BUF = CH_DT + CH_SUB * 16;            // 22016 per sub-tile
+constexpr int CH_HSUB = 3 * CH_PLANE;                  // 21504
+constexpr int CH_HOFF = 2 * CH_BUF;                    // 44032
+constexpr int CH_LDS = CH_HOFF + 4 * CH_HSUB;          // 130048
+static_assert(CH_LDS <= 160 * 1024, "LDS");
 constexpr int CH_THREADS = 768;
 constexpr int CH_HSLOTS = 4;                           // h float4 per dX lane: 64 rows x <= 32 float4 / 512
 
@@ -96,14 +101,16 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
 #endif
 
     // rows [r0, r0 + 64) of a [M][ld] fp32 matrix, float4 item e = row * q + c4 -> (global byte offset, LDS plane
-    // offset); rows past M read 0 through the buffer resource
-    auto item_offsets = [&](int e, int q, int ld, uint32_t& voff, uint32_t& loff, int& c4o, int& rowo) {
+    // offset in the delta buffers (HS < 0) or in h set HS); rows past M read 0 through the buffer resource
+    auto item_offsets = [&](int e, int q, int ld, int hs, uint32_t& voff, uint32_t& loff, int& c4o, int& rowo) {
         const int row = e / q, c4 = e - row * q;
         voff = (uint32_t)(row * ld + 4 * c4) * 4u;
-        loff = (uint32_t)((row >> 5) * CH_BUF + (row & 31) * CH_PITCH + 8 * c4);
+        loff = (uint32_t)((hs < 0 ? (row >> 5) * CH_BUF : CH_HOFF + (2 * hs + (row >> 5)) * CH_HSUB) +
+                          (row & 31) * CH_PITCH + 8 * c4);
         c4o = c4;
         rowo = row;
     };
+    auto hset = [&](int hs, int s) { return sm + CH_HOFF + (2 * hs + s) * CH_HSUB; };
     auto store_planes = [&](unsigned char* base, f32x4 x) {
         bf16x4 p0, p1, p2;
         split4(x, p0, p1, p2);
@@ -111,10 +118,10 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
         *reinterpret_cast<bf16x4*>(base + CH_PLANE) = p1;
         *reinterpret_cast<bf16x4*>(base + 2 * CH_PLANE) = p2;
     };
-    // the db column of the h planes: constant one at column NI4 of both sub-tiles (planes 1, 0, 0)
-    auto db_column = [&](int ni4, int t) {
+    // the db column of h set hs: constant one at column NI4 of both sub-tiles (planes 1, 0, 0)
+    auto db_column = [&](int hs, int ni4, int t) {
         if (t < CH_ROWS) {
-            unsigned char* o = sm + (t >> 5) * CH_BUF + CH_HP + (t & 31) * CH_PITCH + 2 * ni4;
+            unsigned char* o = hset(hs, t >> 5) + (t & 31) * CH_PITCH + 2 * ni4;
             *reinterpret_cast<unsigned short*>(o) = 0x3F80;
             *reinterpret_cast<unsigned short*>(o + CH_PLANE) = 0;
             *reinterpret_cast<unsigned short*>(o + 2 * CH_PLANE) = 0;
@@ -133,7 +140,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
         for (int e = tid; e < CH_ROWS * 25; e += CH_THREADS) {
             uint32_t voff, loff;
             int c4, row;
-            item_offsets(e, 25, N.ldd, voff, loff, c4, row);
+            item_offsets(e, 25, N.ldd, -1, voff, loff, c4, row);
             const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(drs, voff, 0, 0));
             store_planes(sm + CH_DP + loff, x);
             if (c4 == 24) *reinterpret_cast<f32x4*>(sm + (row >> 5) * CH_BUF + CH_DT + (row & 31) * 16) = x;
@@ -141,11 +148,11 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
         for (int e = tid; e < CH_ROWS * hq; e += CH_THREADS) {
             uint32_t voff, loff;
             int c4, row;
-            item_offsets(e, hq, L.ldh, voff, loff, c4, row);
+            item_offsets(e, hq, L.ldh, 0, voff, loff, c4, row);
             const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hrs, voff, 0, 0));
-            store_planes(sm + CH_HP + loff, x);
+            store_planes(sm + loff, x);
         }
-        db_column(4 * hq, tid);
+        db_column(0, 4 * hq, tid);
     }
 
     if (wave < 8) {
@@ -179,6 +186,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
             };
             load_w(max(nl - 1, 1));
             for (int j = nl - 1; j >= 0; --j) {
+                const int hs = (nl - 1 - j) & 1;       // h set of this layer's h_{j-1}
                 __syncthreads();                       // A: delta_j, h_{j-1} in LDS
                 VIHMC_CH_STAMP(j, 0)
                 VIHMC_CH_STAMP(j, 1)
@@ -198,7 +206,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                         const int e = (tid + 512 * v) % tot;
                         uint32_t voff, loff;
                         int c4, row;
-                        item_offsets(e, hq_n, Ln.ldh, voff, loff, c4, row);
+                        item_offsets(e, hq_n, Ln.ldh, hs ^ 1, voff, loff, c4, row);
                         hl[v] = loff;
                         hx[v] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hrs, voff, 0, 0));
                     }
@@ -230,7 +238,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
 #pragma unroll
                         for (int u = 0; u < NU; ++u) {
                             const int col = 16 * (t0 + u) + 4 * lg;
-                            const unsigned char* hrow = buf + CH_HP + (16 * h + lr) * CH_PITCH + 2 * col;
+                            const unsigned char* hrow = hset(hs, s) + (16 * h + lr) * CH_PITCH + 2 * col;
                             bf16x4 hq[3];
 #pragma unroll
                             for (int p = 0; p < 3; ++p) hq[p] = *reinterpret_cast<const bf16x4*>(hrow + p * CH_PLANE);
@@ -247,11 +255,17 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                 // them above this layer's MFMAs (which would need a second set of 72 fragment registers)
                 __builtin_amdgcn_sched_barrier(0);
                 load_w(max(j - 1, 1));
+                // the next layer's h rows into the other h set (its last readers were layer j + 1's, before A)
+                if (dx) {
+#pragma unroll
+                    for (int v = 0; v < CH_HSLOTS; ++v) store_planes(sm + hl[v], hx[v]);
+                    db_column(hs ^ 1, 4 * hq_n, tid);
+                }
 #if CH_STAMP
                 asm volatile("" :: "v"(o[0][0]), "v"(o[1][0]));
 #endif
                 VIHMC_CH_STAMP(j, 2)
-                __syncthreads();                       // B: every read of delta_j / h_{j-1} done
+                __syncthreads();                       // B: every read of delta_j done
                 VIHMC_CH_STAMP(j, 3)
                 if (dx) {
 #pragma unroll
@@ -263,9 +277,6 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                             store_planes(buf + CH_DP + (16 * h + lr) * CH_PITCH + 2 * col, o[s][u]);
                             if (col == 96) *reinterpret_cast<f32x4*>(buf + CH_DT + (16 * h + lr) * 16) = o[s][u];
                         }
-#pragma unroll
-                    for (int v = 0; v < CH_HSLOTS; ++v) store_planes(sm + CH_HP + hl[v], hx[v]);
-                    db_column(4 * hq_n, tid);
                 }
                 VIHMC_CH_STAMP(j, 4)
             }
@@ -290,7 +301,7 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
         f32x4 acc[2][7];
         // weight gradient over the 64 rows (k = the rows, two 32-row blocks); instantiated for 7 column tiles (all
         // but an input layer), so the next tile's h reads stay in flight under this tile's MFMAs
-        auto dw_layer = [&](auto nt_c, int ntj) __attribute__((always_inline)) {
+        auto dw_layer = [&](auto nt_c, int ntj, int hs) __attribute__((always_inline)) {
             constexpr int NT = decltype(nt_c)::value;  // 0: ntj at run time
             const int nt = NT ? NT : ntj;
 #pragma unroll
@@ -300,19 +311,20 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
 #pragma unroll 1
             for (int s = 0; s < 2; ++s) {
                 const unsigned char* buf = sm + s * CH_BUF;
+                const unsigned char* hbuf = hset(hs, s);
                 bf16x8 da[2][3], hb[2][3];
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
                     da[0][p] = tr_frag(buf + CH_DP + p * CH_PLANE, tro, 16 * rta);
                     da[1][p] = tr_frag(buf + CH_DP + p * CH_PLANE, tro, 16 * rtb);
-                    hb[0][p] = tr_frag(buf + CH_HP + p * CH_PLANE, tro, 0);
+                    hb[0][p] = tr_frag(hbuf + p * CH_PLANE, tro, 0);
                 }
 #pragma unroll
                 for (int t = 0; t < 7; ++t) {
                     if (t >= nt) break;
                     if (t + 1 < nt) {
 #pragma unroll
-                        for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(buf + CH_HP + p * CH_PLANE, tro, 16 * (t + 1));
+                        for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(hbuf + p * CH_PLANE, tro, 16 * (t + 1));
                     }
                     if (CH_ABL == 1) {
                         asm volatile("" :: "v"(da[0][0]), "v"(da[1][0]), "v"(hb[t & 1][0]), "v"(hb[t & 1][1]), "v"(hb[t & 1][2]));
@@ -324,14 +336,15 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
             }
         };
         for (int j = nl - 1; j >= 0; --j) {
+            const int hs = (nl - 1 - j) & 1;
             __syncthreads();                           // A
             VIHMC_CH_STAMP(j, 0)
             VIHMC_CH_STAMP(j, 1)
             const BwdChainLayer& L = N.L[j];
             const int NI4 = (L.n_in + 3) & ~3;
             const int ntj = __builtin_amdgcn_readfirstlane((NI4 + 16) >> 4);
-            if (ntj == 7) dw_layer(std::integral_constant<int, 7>{}, 7);
-            else dw_layer(std::integral_constant<int, 0>{}, ntj);
+            if (ntj == 7) dw_layer(std::integral_constant<int, 7>{}, 7, hs);
+            else dw_layer(std::integral_constant<int, 0>{}, ntj, hs);
 #if CH_STAMP
             asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][6]));
 #endif
