@@ -429,6 +429,23 @@ __device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, co
     hn[6].x = v;
 }
 
+#ifndef FWD_STAMP
+#define FWD_STAMP 0   // timing-only instrumentation (variant builds): per-layer phase stamps of k_fwd_fused_bf
+#endif
+#if FWD_STAMP
+// every 8th workgroup (the first 16): per wave (compute, then DMA) and layer s_memtime after the layer's barrier [0],
+// after the operand split (compute) / the DMA issue (DMA waves) [1], after the layer's MFMAs + epilogue + h stores
+// are issued [2], after the wait before the next barrier [3]; per workgroup s_memtime / s_memrealtime at start and
+// end (profiles/scripts/diag/stamps_fwd.py)
+constexpr int FWS_WG = 16, FWS_L = 10;
+__device__ unsigned long long fw_stamps[FWS_WG][16][FWS_L][4];
+__device__ unsigned long long fw_real[FWS_WG][2][2];
+#define FW_ST(J, K) \
+    if (fw_samp && lane == 0 && (J) < FWS_L) fw_stamps[fw_sidx][wave][(J)][(K)] = __builtin_amdgcn_s_memtime();
+#else
+#define FW_ST(J, K)
+#endif
+
 // ND > 0 (images only): ND extra waves that only issue the weight-image DMA. With four compute waves (one chain) each
 // of them otherwise issues 17 one-KB DMA pieces per layer (~100 cycles each among its MFMAs).
 template <int NW, int ND = 0>
@@ -447,6 +464,14 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
     const int rowc = min(row, N.rows - 1);
     const bool rok = row < N.rows;
     const float* Wc = args.packed + c * args.dp;
+#if FWD_STAMP
+    const bool fw_samp = (blockIdx.x % 8) == 0 && blockIdx.x / 8 < FWS_WG;
+    const int fw_sidx = blockIdx.x / 8;
+    if (fw_samp && tid == 0) {
+        fw_real[fw_sidx][0][0] = __builtin_amdgcn_s_memtime();
+        fw_real[fw_sidx][0][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     if (ND > 0 && wave >= NW) {
         // DMA waves: image 0 before the first barrier, image j + 1 after barrier j, each drained before the barrier
         // that publishes it; the same barrier sequence as the compute waves (zero fill, one per layer, epilogue)
@@ -457,12 +482,15 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
         __syncthreads();
         for (int j = 0; j < N.nl; ++j) {
             __syncthreads();
+            FW_ST(j, 0)
             if (j + 1 < N.nl) {
                 for (int k = wave - NW; k < FWD_WIMG / 1024; k += ND)
                     bf6::glds16_asm(wimgd + (int64_t)(j + 1) * FWD_WIMG + k * 1024 + lane * 16,
                                     fsmb + ((j + 1) & 1) * FWD_WIMG + k * 1024);
             }
+            FW_ST(j, 1)
             bf6::wait_vmcnt0();
+            FW_ST(j, 3)
         }
         if (N.qimg != nullptr) __syncthreads();
         return;
@@ -549,6 +577,7 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
     const uint32_t obytes = (uint32_t)N.rows * (uint32_t)N.ldo * 4u;
     for (int j = 0; j < N.nl; ++j) {
         __syncthreads();
+        FW_ST(j, 0)
         if (dma) {
             if (j + 1 < N.nl) {
                 VIHMC_FB_DMA(j + 1, (j + 1) & 1)
@@ -565,11 +594,19 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
         if (FWD_TAILF32) {
             bf16x4 h6u[3];
             bf_split_operand(h, hp, h6u);          // tile 6 planes unused (the f32 MFMA takes h[6].x)
+#if FWD_STAMP
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            FW_ST(j, 1)
             const float* wtail = reinterpret_cast<const float*>(bbuf + FWD_WTAIL);
             const float h6f = h[6].x;
             if (act == ACT_TANH) tf_layer<ACT_TANH>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
             else if (act == ACT_RELU) tf_layer<ACT_RELU>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
             else tf_layer<ACT_ID>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
+#if FWD_STAMP
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            FW_ST(j, 2)
         } else {
             bf16x4 h6[3];
             bf_split_operand(h, hp, h6);
@@ -586,7 +623,14 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
             if (FWD_TAILF32) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
             else bf6::wait_vmcnt0();
         }
+        FW_ST(j, 3)
     }
+#if FWD_STAMP
+    if (fw_samp && tid == 0) {
+        fw_real[fw_sidx][1][0] = __builtin_amdgcn_s_memtime();
+        fw_real[fw_sidx][1][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     // the output layer's rows as the contraction's pre-split image (bit-identical to k_split_blocks on the fp32
     // rows just stored: same conversions), which saves that kernel's re-read of the outputs and its launch
     if (N.qimg != nullptr) {
@@ -733,6 +777,15 @@ size_t fwd_fused_bf_lds_bytes() { return 2 * (size_t)FWD_WIMG; }
 static_assert(BBUF <= FWD_WIMG && FWD_WTAIL + FW * 16 <= FWD_WIMG && FWD_WIMG % 1024 == 0 &&
               2 * FWD_WIMG <= 160 * 1024, "weight image");
 bool fwd_fused_bf_needs_wimg() { return FWD_TAILF32 != 0; }
+
+#if FWD_STAMP
+extern "C" int vihmc_debug_fwd_stamps(void* stamps, size_t stamp_bytes, void* real, size_t real_bytes) {
+    if (stamp_bytes != sizeof(fw_stamps) || real_bytes != sizeof(fw_real)) return -1;
+    hipError_t e = hipMemcpyFromSymbol(stamps, HIP_SYMBOL(fw_stamps), stamp_bytes, 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(real, HIP_SYMBOL(fw_real), real_bytes, 0, hipMemcpyDeviceToHost);
+    return (int)e;
+}
+#endif
 int fwd_fused_bf_waves() { return FWD_BF_NW; }
 
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, int nw, hipStream_t s) {
@@ -758,6 +811,6 @@ hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s) {
 }
 
 // timing-only / instrumentation switches this translation unit was built with (0 = product build)
-int diag_switches_fused() { return FWD_ABL; }
+int diag_switches_fused() { return FWD_ABL | (FWD_STAMP << 8); }
 
 }  // namespace vihmc
