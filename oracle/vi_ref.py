@@ -7,6 +7,9 @@ einsum, + b), loss_j = gaussian_nll(mean) * train_size + beta * KL(prior || post
 the mean over draws. Pinned by tests/golden/vi_deeponet_*.npz (the reference's own train_model).
 ``log_var`` (learn_noise, noise_type 0: main_VI_deeponet.py:154-156, metrics.py:21-25): the NLL variance is
 exp(log_var), a trainable scalar; elbo_step then also returns d loss / d log_var.
+Per-item trunk subsets (p < P, utils.py:39-41): NaN entries of y_grid are the grid points an item did not draw;
+the NLL and MSE means run over the remaining (item, point) pairs, as the reference's mean over its [B, p] batch.
+No reference fixture covers p < P (the golden batches carry the whole grid): that case is parity unpinned.
 """
 from __future__ import annotations
 
@@ -40,6 +43,7 @@ def elbo_step(layout, mu, rho, eps_list, branch_in, trunk_grid, y_grid, beta, tr
     xb = torch.tensor(np.asarray(branch_in, np.float64))
     ft = torch.tensor(trunk_feats_np(trunk_grid))
     y = torch.tensor(np.asarray(y_grid, np.float64))
+    m = ~torch.isnan(y)     # p < P (utils.py:39-41): an item's undrawn grid points are NaN and leave the mean
     lv = None if log_var is None else torch.tensor(float(log_var), dtype=torch.float64, requires_grad=True)
     sig = torch.log1p(torch.exp(rho_t))
     sp = torch.tensor(float(prior_sigma), dtype=torch.float64)
@@ -48,7 +52,7 @@ def elbo_step(layout, mu, rho, eps_list, branch_in, trunk_grid, y_grid, beta, tr
     for eps in eps_list:
         W = mu_t + torch.tensor(np.asarray(eps, np.float64)) * sig
         pred = _mlp(W, br, xb, act) @ _mlp(W, tr, ft, act).T + W[0]
-        nll = F.gaussian_nll_loss(pred, y, _var(y, noise_var, lv), reduction="mean")
+        nll = F.gaussian_nll_loss(pred[m], y[m], _var(y, noise_var, lv)[m], reduction="mean")
         total = total + nll * train_size + beta * kl
     loss = total / len(eps_list)
     if lv is None:
@@ -71,5 +75,6 @@ def eval_loss(layout, mu, rho, branch_in, trunk_grid, y_grid, beta, size, noise_
     y = torch.tensor(np.asarray(y_grid, np.float64))
     pred = _mlp(W, br, xb, act) @ _mlp(W, tr, ft, act).T + W[0]
     lv = None if log_var is None else torch.tensor(float(log_var), dtype=torch.float64)
-    nll = F.gaussian_nll_loss(pred, y, _var(y, noise_var, lv), reduction="mean")
-    return float(nll * size + beta * kl), float(torch.mean((pred - y) ** 2))
+    m = ~torch.isnan(y)
+    nll = F.gaussian_nll_loss(pred[m], y[m], _var(y, noise_var, lv)[m], reduction="mean")
+    return float(nll * size + beta * kl), float(torch.mean((pred - y)[m] ** 2))

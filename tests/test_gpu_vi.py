@@ -104,6 +104,76 @@ def test_burgers_shape_step_matches_oracle(cuda_device):
         eng.close()
 
 
+def _subset_batch(branch_in, grid, y_grid, p, seed):
+    """Items with their own p of the P grid points (utils.py:39-41: np.random.choice(P, p, replace=False) per
+    item): the batch as the reference's loader yields it, and y_grid with NaN at each item's undrawn points."""
+    rng = np.random.default_rng(seed)
+    B, P = y_grid.shape
+    ind = np.stack([rng.choice(P, p, replace=False) for _ in range(B)])
+    batch = (torch.from_numpy(np.ascontiguousarray(branch_in)).view(B, 1, -1), torch.from_numpy(grid[ind]),
+             torch.from_numpy(np.take_along_axis(y_grid, ind, 1)))
+    y_nan = np.full_like(y_grid, np.nan)
+    np.put_along_axis(y_nan, ind, np.take_along_axis(y_grid, ind, 1), 1)
+    return batch, y_nan
+
+
+@pytest.mark.parametrize("shape", ["small", "burgers"])
+def test_per_item_trunk_subsets_match_oracle(shape, cuda_device):
+    """p < P: every item carries its own random subset of the trunk grid. The engine runs the whole grid with the
+    undrawn (item, point) pairs as NaN targets (plan option y_masked: residual 0 there; lik_count = B p), so one
+    training step's loss and mu / rho gradients, the eval-mode loss and the MSE match the float64 oracle's mean over
+    the drawn pairs. small = the golden case's width-12 network (fp32 contraction), burgers = width 100, 101 x 101
+    grid (bf16x6 contraction). Parity unpinned against the reference itself: its golden batches carry p = P."""
+    from oracle.deeponet_ref import deeponet_layout
+    from oracle.vi_ref import eval_loss
+    from vihmc.vi import ELBO, BatchEngines, Bayesian_DeepONet, mse, train_model, validate_model
+    if shape == "small":
+        c = vi_case("vi_deeponet_tanh")
+        m = make_model(c)
+        grid = c.g["trunk_grid"].reshape(-1, 2)
+        y_grid, branch = c.g["y_grid"], c.g["branch_in"].reshape(c.B, -1)
+        lay, act, size = c.layout, c.act, c.train_size
+    else:
+        from vihmc.data import deeponet_problem
+        prob = deeponet_problem(seed=3, n=6)
+        grid = prob.trunk_in[0]
+        priors = {"prior_mu": 0, "prior_sigma": 0.1, "posterior_mu_initial": (0, 0.1),
+                  "posterior_rho_initial": (-5, 0.1)}
+        torch.manual_seed(7)
+        m = Bayesian_DeepONet(priors, 100, 100, 101, 5, 9, 9, 100, "tanh", 0, 0, impose_bc=True)
+        y_grid, branch = prob.y, prob.branch_in[:, 0]
+        lay, act, size = deeponet_layout(), "tanh", 1000 * grid.shape[0]
+    P = grid.shape[0]
+    batch, y_nan = _subset_batch(branch, grid, y_grid, P // 3, 11)
+    mu0, rho0 = m.mu_flat().detach().numpy().copy(), m.rho_flat().detach().numpy().copy()
+    m = m.to(cuda_device)
+    eng = BatchEngines(m.spec, grid, 1.0, 2, cuda_device)
+    try:
+        rec = GradRecorder(m)
+        torch.manual_seed(31)
+        eps = [m.draw_eps().numpy() for _ in range(2)]
+        torch.manual_seed(31)
+        lt = train_model([batch], m, ELBO(), rec, size, 1, 2, 1.0, engines=eng)
+        e0 = eng.get(batch[0].shape[0])
+        assert e0.get_option("y_masked") == 1 and e0.get_option("lik_count") == y_grid.shape[0] * (P // 3)
+        assert not (e0.get_option("gram") & 2)
+        loss, gm, gr = elbo_step(lay, mu0, rho0, eps, branch, grid, y_nan, 1.0, size, act=act)
+        assert lt == pytest.approx(loss, rel=2e-5)
+        assert rel_norm(rec.grads[0].cpu().numpy(), gm) < 2e-4
+        assert rel_norm(rec.grads[1].cpu().numpy(), gr) < 2e-4
+        lv_ref, mse_ref = eval_loss(lay, mu0, rho0, branch, grid, y_nan, 1.0, size, act=act)
+        lv = validate_model([batch], m, ELBO(), size, 1.0, 1, engines=eng)
+        assert lv == pytest.approx(lv_ref, rel=2e-5)
+        assert mse([batch], m, engines=eng) == pytest.approx(mse_ref, rel=1e-4)
+        # a whole-grid batch on the same plan clears the mask again
+        full = (batch[0], torch.from_numpy(np.broadcast_to(grid, (y_grid.shape[0],) + grid.shape).copy()),
+                torch.from_numpy(np.ascontiguousarray(y_grid, dtype=np.float32)))
+        eng.load(full)
+        assert e0.get_option("y_masked") == 0 and e0.get_option("lik_count") == y_grid.shape[0] * P
+    finally:
+        eng.close()
+
+
 def test_burgers_training_step_timing(cuda_device):
     """main_VI_deeponet's configuration: batch 128 functions x 10,201 points, num_ens 5, Adam."""
     from vihmc.data import deeponet_problem

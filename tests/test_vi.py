@@ -54,12 +54,37 @@ def test_canonical_undoes_item_permutations():
     from vihmc.vi import BatchEngines
     c = vi_case("vi_deeponet_tanh")
     be = BatchEngines(DeepONetSpec(12, 12, 7, 5, 3, 3, "tanh", 12), c.g["trunk_grid"], 1.0, 2, "cuda")
-    y = be.canonical(c.batch[1], c.batch[2])
+    y, count = be.canonical(c.batch[1], c.batch[2])
     assert torch.equal(y, torch.from_numpy(c.g["y_grid"]))
+    assert count == y.numel()
     bad = c.batch[1].clone()
-    bad[0, 0] = bad[0, 1]                      # a repeated point: not a permutation of the grid
-    with pytest.raises(NotImplementedError):
+    bad[0, 0] = bad[0, 1]                      # a repeated point: not distinct grid points
+    with pytest.raises(ValueError):
         be.canonical(bad, c.batch[2])
+
+
+def test_canonical_per_item_subsets():
+    """p < P (utils.py:39-41 draws p of the P trunk points per item): each item's targets land on its own grid
+    points, the points it did not draw hold NaN (the engine's masked plans skip them), count = B p."""
+    from vihmc.layout import DeepONetSpec
+    from vihmc.vi import BatchEngines
+    c = vi_case("vi_deeponet_tanh")
+    grid = c.g["trunk_grid"].reshape(-1, 2)
+    P = grid.shape[0]
+    be = BatchEngines(DeepONetSpec(12, 12, 7, 5, 3, 3, "tanh", 12), grid, 1.0, 2, "cuda")
+    rng = np.random.default_rng(3)
+    B, p = 4, P // 3
+    ind = np.stack([rng.choice(P, p, replace=False) for _ in range(B)])
+    yfull = rng.standard_normal((B, P)).astype(np.float32)
+    xt = torch.from_numpy(grid[ind])
+    yt = torch.from_numpy(np.take_along_axis(yfull, ind, 1))
+    y, count = be.canonical(xt, yt)
+    assert count == B * p
+    mask = np.zeros((B, P), bool)
+    np.put_along_axis(mask, ind, True, 1)
+    yn = y.numpy()
+    assert np.array_equal(np.isnan(yn), ~mask)
+    assert np.array_equal(yn[mask], yfull[mask])
 
 
 def test_elbo_module_matches_formula():

@@ -182,8 +182,9 @@ __global__ __launch_bounds__(256, 2) void k_contract2(ContractProb P) {
                     const float sv = sacc[s][r] + b0;
                     if (!GRAD && P.write_s && ok) sout[(int64_t)qq * P.ldout + oo] = sv;
                     const float rv = sv - yv[s][r];
-                    g[s][r] = ok ? P.gscale * rv : 0.f;
-                    if (ok) {
+                    const bool okm = ok && (!P.masked || yv[s][r] == yv[s][r]);   // NaN target: excluded pair
+                    g[s][r] = okm ? P.gscale * rv : 0.f;
+                    if (okm) {
                         ssq += (double)rv * (double)rv;
                         gsum += (double)g[s][r];
                     }
@@ -374,8 +375,9 @@ __global__ __launch_bounds__(512, 2) void k_contract_ws(ContractProb P) {
                         const int oo = o0 + 16 * s + lr;
                         const bool ok = (qq < q_hi) && (oo < P.Mo);
                         const float rv = sacc[s][r] + b0 - yv[s][r];
-                        g[s][r] = ok ? P.gscale * rv : 0.f;
-                        if (ok) {
+                        const bool okm = ok && (!P.masked || yv[s][r] == yv[s][r]);   // NaN target: excluded
+                        g[s][r] = okm ? P.gscale * rv : 0.f;
+                        if (okm) {
                             ssq += (double)rv * (double)rv;
                             gsum += (double)g[s][r];
                         }

@@ -174,7 +174,7 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
             VIHMC_CB_STAMP(i, 0)
             {
                 const int q0 = q_lo + i * CB_QC;
-                const bool nomask = q0 + CB_QC <= q_hi && wave_valid;   // wave-uniform
+                const bool nomask = q0 + CB_QC <= q_hi && wave_valid && !P.masked;   // wave-uniform
                 const unsigned char* img = smc + (i % CB_NQBUF) * CB_QIMG;
                 VIHMC_CB_YLOAD(yn, min(i + 1, nchunks - 1))
                 unsigned char* gimg = smc + CB_NQBUF * CB_QIMG + (i & 1) * CB_GIMG + w * (CB_GIMG / 8);
@@ -199,12 +199,14 @@ __global__ __launch_bounds__(CBA_THREADS, 1) void k_contract_bf(ContractProb P) 
                 }
                 if (!nomask) {
                     // a partial last chunk (branch rows past q_hi: zero image rows, so S = b0) or owner rows past Mo
-                    // (the last owner tile): those residuals are not the workgroup's
+                    // (the last owner tile): those residuals are not the workgroup's; a masked plan's NaN targets
+                    // (pairs outside an item's trunk subset) count as residual 0
 #pragma unroll
                     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
                         for (int r = 0; r < 4; ++r)
-                            rv[sub][r] = (ovalid && q0 + 16 * sub + 4 * lg + r < q_hi) ? rv[sub][r] : 0.f;
+                            rv[sub][r] = (ovalid && q0 + 16 * sub + 4 * lg + r < q_hi &&
+                                          (!P.masked || yv[sub][r] == yv[sub][r])) ? rv[sub][r] : 0.f;
                 }
 #pragma unroll
                 for (int sub = 0; sub < 2; ++sub) {

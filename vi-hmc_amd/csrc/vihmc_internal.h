@@ -137,6 +137,7 @@ struct ContractProb {
     int32_t o_tiles, q_chunks, q_per_chunk;   // o_tiles = ceil(Mo / CONTRACT_OWN_PER_WG)
     int32_t with_stats, write_s;
     int32_t load_g;                       // side B: Y holds G (already scaled); no S recompute
+    int32_t masked;                       // side A: a NaN target marks an excluded (row, point) pair (residual 0)
     int32_t xcd_group;                    // 1: the o_tiles workgroups sharing one Q chunk run on one XCD
                                           //    (requires C * q_chunks % 8 == 0; speed only)
     int32_t bf16x6;                       // side A, W = 100: products on the bf16 MFMA, 3-way split

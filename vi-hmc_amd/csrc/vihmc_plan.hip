@@ -241,6 +241,11 @@ struct vihmc_plan {
     // form when the ratio of its PREVIOUS-BUT-ONE snapshot is below the threshold -- a deterministic function of the
     // chain's own history (two evaluations of lag keep the host one trajectory ahead of the GPU without a stall).
     int gram_guard = 6;
+    // per-item target subsets (VI training with p < P): NaN targets mark the excluded (item, point) pairs, whose
+    // residual side A counts as 0; lik_count = the pairs that remain (0: N P). The Gram form and the fit guard are
+    // off for a masked plan (their data images and sum y^2 would take the NaNs).
+    int y_masked = 0;
+    int64_t lik_count = 0;
     float* fit_dev = nullptr;     // [maxC] fit ratios of the last all-residual evaluation
     double* ysq_dev = nullptr;    // sum y^2 (k_ysq, whenever the data images are rebuilt)
     double* ysq_part = nullptr;
@@ -492,8 +497,11 @@ int gram_images(vihmc_plan* p, hipStream_t s) {
     return 0;
 }
 
+// the number of (row, point) pairs in the likelihood
+double lik_count(const vihmc_plan* p) { return p->lik_count > 0 ? (double)p->lik_count : (double)p->N * (double)p->P; }
+
 bool guard_live(const vihmc_plan* p) {
-    return p->gram_alloc && p->gram_guard > 0 && p->maxC <= GUARD_MAXC && !p->capturing;
+    return p->gram_alloc && p->gram_guard > 0 && p->maxC <= GUARD_MAXC && !p->capturing && !p->y_masked;
 }
 
 // chains of this gradient-only evaluation that run the residual form: previous-but-one snapshot below the threshold
@@ -528,7 +536,8 @@ int guard_snapshot(vihmc_plan* p, int C, hipStream_t s) {
 // The form is a property of the plan (its max_chains), not of the call's chain count: a chain's trajectory does not
 // depend on how many chains share its launch (a ragged last rank, a partial batch) -- ADVICE r3.
 bool gram_on(const vihmc_plan* p) {
-    return p->gram && p->gram_alloc && p->W == 100 && p->contract_bf16x6 && p->maxC >= p->gram_min_chains;
+    return p->gram && p->gram_alloc && p->W == 100 && p->contract_bf16x6 && p->maxC >= p->gram_min_chains &&
+           !p->y_masked;
 }
 
 GramArgs gram_args(vihmc_plan* p, int C) {
@@ -1080,6 +1089,7 @@ ContractProb side_a(vihmc_plan* p, int C, bool grad, float* out) {
     q.ldq = p->ldz;
     q.Y = p->y;
     q.ldy = p->P;
+    q.masked = p->y_masked;
     q.b0 = p->packed;
     q.b0_cs = p->dp;
     if (grad) {
@@ -1225,7 +1235,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     // gradient evaluations: the statistics run as a slice of the weight-gradient reduce (nothing reads lik or
     // gp slot 0 before the gather)
     StatsJob stats_job{gram ? p->gstats : p->stats, gram ? p->gstats_cs : p->stats_cs, gram ? stats_waves : stats_waves_res,
-                       p->lik_buf, p->gp, p->dp, (double)p->N * (double)p->P, p->lik.loss, p->lik.tau_out};
+                       p->lik_buf, p->gp, p->dp, lik_count(p), p->lik.loss, p->lik.tau_out};
     if (mixed) {
         stats_job.stats2 = p->stats;
         stats_job.stats2_cs = p->stats_cs;
@@ -1856,7 +1866,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1875,6 +1885,12 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "gram_guard") {                               // threshold 10^-value (0: off); history restarts
         p->gram_guard = std::max(0, value);
         p->n_snap = 0;
+    }
+    else if (k == "y_masked" || k == "lik_count") {             // per-item target subsets (VI training, p < P)
+        if (p->kind != 0) return fail("plan option '" + k + "': DeepONet plans only");
+        if (k == "y_masked") p->y_masked = value ? 1 : 0;
+        else if (value < 0 || (double)value > (double)p->N * (double)p->P) return fail("lik_count must be in [0, N P]");
+        else p->lik_count = value;
     }
     else if (k == "grad_evals" || k == "gram_evals") {          // counters: any value resets both
         p->n_grad_calls = p->n_gram_calls = p->n_gram_chain_evals = 0;
@@ -1906,6 +1922,8 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "gram_chains") *value = p->last_gram_chains;
     else if (k == "gram_chain_evals") *value = (int)std::min<int64_t>(p->n_gram_chain_evals, INT32_MAX);
     else if (k == "gram_guard") *value = p->gram_guard;
+    else if (k == "y_masked") *value = p->y_masked;
+    else if (k == "lik_count") *value = (int)std::min<double>(lik_count(p), INT32_MAX);
     else return fail("unknown plan option '" + k + "' (" OPTION_KEYS ")");
     return 0;
 }

@@ -18,16 +18,17 @@ the engine's gradient. There is no torch forward of the network (no CPU fallback
 
 Weight-noise draws follow the reference's call order on the CPU generator (per forward: every branch
 layer's W_eps then bias_eps, the trunk layers, then the output bias; layers/BBB/BBBLinear.py:55-63,
-bayesian_model.py:100), so identical seeds give identical draws. Batches carry the whole trunk grid per
-function (config.py:30, p = 10201): the NLL is a sum over points, so each item's point permutation
-(utils.py:39-41) is undone by mapping its points onto the plan's grid order.
+bayesian_model.py:100), so identical seeds give identical draws. The reference config draws the whole
+trunk grid per function (config.py:30, p = 10201): the NLL is a sum over points, so each item's point permutation
+(utils.py:39-41) is undone by mapping its points onto the plan's grid order. With p < P every item draws its own
+subset: the plan still runs the whole grid, the undrawn (item, point) pairs carry NaN targets that side A counts as
+residual 0 (plan options y_masked / lik_count), and the NLL / MSE means run over the B p drawn pairs.
 ``learn_noise`` with ``noise_type`` 0 (main_VI_deeponet.py:154-156, metrics.py:21-25; off in the reference
 config, config.py:45-51): the NLL variance is exp(noise_param), one trainable scalar. The plans are then built
 with variance 1, so one evaluation gives 0.5 sum r^2 per draw and its gradient; the log-variance enters in torch
 (``elbo_loss``). Not supported: ``noise_type`` 1 (heteroscedastic head, bayesian_model.py:90-92) -- its
 einsum("bi,bi->b") takes 2-D branch and trunk outputs, so the reference itself cannot run it on the Burgers
-batches (3-D trunk output [B, p, W]); the Cone dataset it serves is out of scope. Per-item trunk
-subsets (p < P) in training.
+batches (3-D trunk output [B, p, W]); the Cone dataset it serves is out of scope.
 """
 from __future__ import annotations
 
@@ -283,11 +284,12 @@ class BatchEngines:
         dev = torch.device(self.device) if not isinstance(self.device, torch.device) else self.device
         return dev if dev.type == "cuda" and torch.cuda.is_available() else torch.device("cpu")
 
-    def canonical(self, x_trunk, y) -> torch.Tensor:
-        """y [B, P] in each item's point order -> the plan's grid order (on the plan's device when it has one).
-
-        Each item's (t, x) rows are located in the grid by their float bit patterns (a 64-bit key per row,
-        binary search in the sorted grid keys), then checked to be a permutation of the grid."""
+    def canonical(self, x_trunk, y):
+        """(y [B, p] in each item's point order) -> (y_grid [B, P] in the plan's grid order, pair count B p), on the
+        plan's device when it has one. Each item's (t, x) rows are located in the grid by their float bit patterns
+        (a 64-bit key per row, binary search in the sorted grid keys) and must be distinct grid points; with p < P
+        (utils.py:39-41 draws p of the P points per item, without replacement) the grid points an item did not draw
+        hold NaN, which the engine's masked plans count as excluded pairs."""
         dev = self._work_device()
         sk = self._sorted.get(dev)
         if sk is None:
@@ -295,22 +297,33 @@ class BatchEngines:
                   torch.from_numpy(self.order.astype(np.int64)).to(dev))
             self._sorted[dev] = sk
         skeys, order = sk
-        xt = torch.as_tensor(x_trunk).detach().to(dev, torch.float32).reshape(-1, self.P, 2)
-        B = xt.shape[0]
-        yy = torch.as_tensor(y).detach().to(dev, torch.float32).reshape(B, self.P)
-        keys = _ordered_keys(xt).reshape(B, self.P)
+        xt = torch.as_tensor(x_trunk).detach().to(dev, torch.float32)
+        B = torch.as_tensor(y).shape[0]
+        xt = xt.reshape(B, -1, 2)
+        p = xt.shape[1]
+        if p > self.P:
+            raise ValueError(f"an item carries {p} trunk points, the grid has {self.P}")
+        yy = torch.as_tensor(y).detach().to(dev, torch.float32).reshape(B, p)
+        keys = _ordered_keys(xt).reshape(B, p)
         pos = torch.searchsorted(skeys, keys).clamp_(max=self.P - 1)
         idx = order[pos]
         seen = torch.bincount((idx + self.P * torch.arange(B, device=dev)[:, None]).reshape(-1), minlength=B * self.P)
-        if not bool(torch.equal(skeys[pos], keys)) or not bool((seen == 1).all()):
-            raise NotImplementedError("every item must carry the whole trunk grid once (p = P); per-item trunk "
-                                      "subsets are not supported in training")
-        return torch.empty_like(yy).scatter_(1, idx, yy)
+        if not bool(torch.equal(skeys[pos], keys)) or bool((seen > 1).any()):
+            raise ValueError("every trunk point of an item must be a distinct point of the plan's grid")
+        yg = torch.full((B, self.P), float("nan"), device=dev) if p < self.P else torch.empty_like(yy)
+        return yg.scatter_(1, idx, yy), B * p
 
     def load(self, batch) -> DeepONetEngine:
+        """The batch's branch rows and targets into the plan of its size; p < P marks the plan's targets masked
+        (plan options y_masked / lik_count) and ``self.count`` is the batch's (item, point) pair count."""
         xb = torch.as_tensor(batch[0]).detach().to(torch.float32).reshape(-1, self.spec.in_branch)
         eng = self.get(xb.shape[0])
-        eng.set_data(xb, self.canonical(batch[1], batch[2]))
+        y, count = self.canonical(batch[1], batch[2])
+        eng.set_data(xb, y)
+        masked = count < xb.shape[0] * self.P
+        eng.option("y_masked", 1 if masked else 0)
+        eng.option("lik_count", count if masked else 0)
+        self.count = count
         return eng
 
     def close(self):
@@ -346,14 +359,15 @@ def elbo_loss(model: Bayesian_DeepONet, engines: BatchEngines, batch, beta, trai
     else:
         num_ens = 1
         W = mu[None]
+    count = float(engines.count)                          # (item, point) pairs: B P, or B p with p < P
     if log_var is None:
-        nll = _EngineNLL.apply(W, eng, float(train_size) / float(eng.N * eng.P))
+        nll = _EngineNLL.apply(W, eng, float(train_size) / count)
     else:
         if engines.tau_out != 1.0:
             raise ValueError("learn_noise needs engines built with variance 1 (BatchEngines(..., 1.0, ...))")
         half_sq = _EngineNLL.apply(W, eng, 1.0)              # 0.5 sum r^2 per draw
         v = _nll_var(log_var.to(dev)).reshape(())
-        nll = float(train_size) * (0.5 * torch.log(v) + half_sq / (v * float(eng.N * eng.P)))
+        nll = float(train_size) * (0.5 * torch.log(v) + half_sq / (v * count))
     return (nll + beta * model.kl()).sum() / num_ens
 
 
@@ -415,8 +429,8 @@ def mse(data_loader, model, noise_type=0, dataset="Burgers", engines: Optional[B
         eng = engines.load(batch_data)
         with torch.no_grad():
             _, out = eng.forward(model.mu_flat().detach()[None].to(eng.device))
-        y = engines.canonical(batch_data[1], batch_data[2]).to(eng.device)
-        l_total += torch.mean((out[0] - y) ** 2).item()
+        y = engines.canonical(batch_data[1], batch_data[2])[0].to(eng.device)
+        l_total += torch.nanmean((out[0] - y) ** 2).item()   # p < P: over each item's own points
     l_total = l_total / (i + 1)
     return l_total
 
