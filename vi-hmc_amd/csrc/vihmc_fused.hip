@@ -35,7 +35,7 @@ __device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c) {
 }
 
 #ifndef FWD_ABL
-#define FWD_ABL 0     // timing-only ablation (wrong results): 1 = no h stores in the bf16x6 forward
+#define FWD_ABL 0     // timing-only ablation (wrong results): 1 = no h stores in the bf16x6 forward, 2 = tanh -> identity
 #endif
 #ifndef FWD_TANH_CHEAP
 #define FWD_TANH_CHEAP 1   // 0: odd Taylor series below 0.25, exp-rcp above (<= 4 ulp, ~17 VALU)
@@ -62,7 +62,7 @@ __device__ __forceinline__ float tanh_f(float x) {
 
 template <int ACT>
 __device__ __forceinline__ float act_t(float z) {
-    if constexpr (ACT == ACT_TANH) return tanh_f(z);
+    if constexpr (ACT == ACT_TANH) return (FWD_ABL & 2) ? z : tanh_f(z);
     else if constexpr (ACT == ACT_RELU) return fmaxf(z, 0.f);
     else return z;
 }
@@ -313,7 +313,7 @@ __device__ __forceinline__ float4 bf_epi(const float* bias, int t, int lg, const
     // per-tile lane offsets hipcc hoisted seven of them out of the layer loop and spilled them at 168 VGPRs, and
     // each reload's vmcnt(0) then also waited for this wave's earlier h stores (OOB + 64 t stays out of range)
     const uint32_t off = (t < 6 || lg == 0) ? ooff + 16u * lg : OOB;
-#if FWD_ABL == 1
+#if FWD_ABL & 1
     asm volatile("" :: "v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w));
     (void)off;
     (void)orsrc;
@@ -421,7 +421,7 @@ __device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, co
     // tile 6: register 0 of lane (lr, lg) = pre-activation of h[lr][96 + lg]
     const f32x4 a6 = tf_tile(wb, wtail, 6, lr, lg, hp, h6);
     const float v = act_t<ACT>(a6[0] + bias[96 + lg]);
-#if FWD_ABL == 1
+#if FWD_ABL & 1
     asm volatile("" :: "v"(v));
 #else
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, ooff + 4u * lg, 4 * 96, 0);
