@@ -35,7 +35,8 @@ __device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c) {
 }
 
 #ifndef FWD_ABL
-#define FWD_ABL 0     // timing-only ablation (wrong results): 1 = no h stores in the bf16x6 forward, 2 = tanh -> identity
+#define FWD_ABL 0     // timing-only ablation (wrong results): 1 = no h stores in the bf16x6 forward, 2 = tanh -> identity,
+                      // 4 = the DMA waves issue no weight-image copies, 8 = no bf16 MFMAs in the 4-wave layer body
 #endif
 #ifndef FWD_TANH_CHEAP
 #define FWD_TANH_CHEAP 1   // 0: odd Taylor series below 0.25, exp-rcp above (<= 4 ulp, ~17 VALU)
@@ -427,6 +428,10 @@ __device__ __forceinline__ void tf_load(const __bf16* wb, const float* wtail, in
 // tf_tile's products in tf_tile's order (bitwise the same tile)
 __device__ __forceinline__ f32x4 tf_mma(const TfFrag& f, const bf16x8 (&hp)[3][3], float h6) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (FWD_ABL & 8) {
+        asm volatile("" :: "v"(f.w[0][0]), "v"(f.w[1][1]), "v"(f.w[2][2]), "v"(hp[0][0]), "v"(hp[2][2]));
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(f.wt, h6, acc, 0, 0, 0);
+    }
 #pragma unroll
     for (int kb = 0; kb < 3; ++kb) {
         acc = mfma32(f.w[kb][2], hp[0][kb], acc);
@@ -544,7 +549,7 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
         for (int j = 0; j < N.nl; ++j) {
             __syncthreads();
             FW_ST(j, 0)
-            if (j + 1 < N.nl) {
+            if (j + 1 < N.nl && !(FWD_ABL & 4)) {
                 for (int k = wave - NW; k < FWD_WIMG / 1024; k += ND)
                     bf6::glds16_asm(wimgd + (int64_t)(j + 1) * FWD_WIMG + k * 1024 + lane * 16,
                                     fsmb + ((j + 1) & 1) * FWD_WIMG + k * 1024);
