@@ -36,7 +36,7 @@ __device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c) {
 
 #ifndef FWD_ABL
 #define FWD_ABL 0     // timing-only ablation (wrong results): 1 = no h stores in the bf16x6 forward, 2 = tanh -> identity,
-                      // 4 = the DMA waves issue no weight-image copies, 8 = no bf16 MFMAs in the 4-wave layer body
+                      // 4 = the DMA waves issue no weight-image copies, 8 = no bf16 MFMAs in the layer body
 #endif
 #ifndef FWD_TANH_CHEAP
 #define FWD_TANH_CHEAP 1   // 0: odd Taylor series below 0.25, exp-rcp above (<= 4 ulp, ~17 VALU)
@@ -390,6 +390,7 @@ __device__ __forceinline__ f32x4 tf_tile(const __bf16* wb, const float* wtail, i
     const int n = tf_row(t, lr);
     const __bf16* row0 = wb + n * BROW;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (FWD_ABL & 8) return __builtin_amdgcn_mfma_f32_16x16x4f32(wtail[4 * n + lg], h6, acc, 0, 0, 0);
 #pragma unroll
     for (int kb = 0; kb < 3; ++kb) {
         const int o = kb * 32 + lg * 8;
@@ -408,75 +409,10 @@ __device__ __forceinline__ f32x4 tf_tile(const __bf16* wb, const float* wtail, i
     return __builtin_amdgcn_mfma_f32_16x16x4f32(wtail[4 * n + lg], h6, acc, 0, 0, 0);
 }
 
-// one tile's W fragments (3 k-blocks x 3 planes) and its fp32 k-tail weight
-struct TfFrag {
-    bf16x8 w[3][3];
-    float wt;
-};
-__device__ __forceinline__ void tf_load(const __bf16* wb, const float* wtail, int t, int lr, int lg, TfFrag& f) {
-    const int n = tf_row(t, lr);
-    const __bf16* row0 = wb + n * BROW;
-#pragma unroll
-    for (int kb = 0; kb < 3; ++kb) {
-        const int o = kb * 32 + lg * 8;
-        f.w[kb][0] = *reinterpret_cast<const bf16x8*>(row0 + o);
-        f.w[kb][1] = *reinterpret_cast<const bf16x8*>(row0 + BPLANE + o);
-        f.w[kb][2] = *reinterpret_cast<const bf16x8*>(row0 + 2 * BPLANE + o);
-    }
-    f.wt = wtail[4 * n + lg];
-}
-// tf_tile's products in tf_tile's order (bitwise the same tile)
-__device__ __forceinline__ f32x4 tf_mma(const TfFrag& f, const bf16x8 (&hp)[3][3], float h6) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (FWD_ABL & 8) {
-        asm volatile("" :: "v"(f.w[0][0]), "v"(f.w[1][1]), "v"(f.w[2][2]), "v"(hp[0][0]), "v"(hp[2][2]));
-        return __builtin_amdgcn_mfma_f32_16x16x4f32(f.wt, h6, acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int kb = 0; kb < 3; ++kb) {
-        acc = mfma32(f.w[kb][2], hp[0][kb], acc);
-        acc = mfma32(f.w[kb][1], hp[1][kb], acc);
-        acc = mfma32(f.w[kb][0], hp[2][kb], acc);
-        acc = mfma32(f.w[kb][1], hp[0][kb], acc);
-        acc = mfma32(f.w[kb][0], hp[1][kb], acc);
-        acc = mfma32(f.w[kb][0], hp[0][kb], acc);
-    }
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(f.wt, h6, acc, 0, 0, 0);
-}
-
-#ifndef FWD_PIPE
-#define FWD_PIPE 1    // the 4-wave forward (one chain): W fragments read one tile ahead of their MFMAs
-#endif
-// PIPE (the 4-wave forward of one chain, 2 waves per SIMD): tile t+1's ten fragment reads are issued before tile
-// t's 19 MFMAs, so no MFMA waits out an LDS read. Read per k-block just ahead of use (hipcc's schedule), every
-// k-block waited ~100+ cycles on its reads: a layer took ~5,000 cycles against ~2,200 of MFMA (one compute wave per
-// SIMD, profiles/r04z_stamps_fwd.txt; tanh -> identity saved only 6 %, no h stores nothing: r04ze). Same products
-// in the same order: bitwise the unpipelined form.
-template <int ACT, bool PIPE>
+template <int ACT>
 __device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, const float* wtail,
                                          const bf16x8 (&hp)[3][3], float h6, int lr, int lg,
                                          __amdgpu_buffer_rsrc_t orsrc, uint32_t ooff, float4 (&hn)[7]) {
-    if (PIPE) {
-        TfFrag F[2];
-        tf_load(wb, wtail, 0, lr, lg, F[0]);
-        f32x4 prev = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < 7; ++t) {
-            if (t < 6) tf_load(wb, wtail, t + 1, lr, lg, F[(t + 1) & 1]);
-            __builtin_amdgcn_sched_barrier(0);         // the next tile's reads stay ahead of this tile's MFMAs
-            const f32x4 a = tf_mma(F[t & 1], hp, h6);
-            if (t >= 1) hn[t - 1] = bf_epi<ACT>(bias, t - 1, lg, prev, orsrc, ooff);
-            prev = a;
-        }
-        const float v = act_t<ACT>(prev[0] + bias[96 + lg]);
-#if FWD_ABL & 1
-        asm volatile("" :: "v"(v));
-#else
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), orsrc, ooff + 4u * lg, 4 * 96, 0);
-#endif
-        hn[6].x = v;
-        return;
-    }
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
         const f32x4 a0 = tf_tile(wb, wtail, 2 * p, lr, lg, hp, h6);
@@ -666,10 +602,9 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
             FW_ST(j, 1)
             const float* wtail = reinterpret_cast<const float*>(bbuf + FWD_WTAIL);
             const float h6f = h[6].x;
-            constexpr bool PIPE = FWD_PIPE && NW <= 8;      // 2 waves per SIMD: room for the prefetch
-            if (act == ACT_TANH) tf_layer<ACT_TANH, PIPE>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
-            else if (act == ACT_RELU) tf_layer<ACT_RELU, PIPE>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
-            else tf_layer<ACT_ID, PIPE>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
+            if (act == ACT_TANH) tf_layer<ACT_TANH>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
+            else if (act == ACT_RELU) tf_layer<ACT_RELU>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
+            else tf_layer<ACT_ID>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
 #if FWD_STAMP
             __builtin_amdgcn_sched_barrier(0);
 #endif
