@@ -412,12 +412,14 @@ int image_maps(vihmc_plan* p, const vihmc_deeponet_desc* d, const int64_t* idx) 
     }
     if (int rc = p->upload(&p->smap_img, sw.data(), p->K)) return rc;
     if (int rc = p->upload(&p->smap_imgf, sf.data(), p->K)) return rc;
-    if (int rc = p->upload(&p->smap_timg, stw.data(), p->K)) return rc;
-    if (int rc = p->upload(&p->smap_timgf, stf.data(), p->K)) return rc;
+    if (p->wtimg) {                                     // (null: no k_bwd_chain for this plan, no W^T images)
+        if (int rc = p->upload(&p->smap_timg, stw.data(), p->K)) return rc;
+        if (int rc = p->upload(&p->smap_timgf, stf.data(), p->K)) return rc;
+    }
     FusedArgs a{};
     fused_args(p, p->maxC, a);
     HIPCHK(launch_split_wimg(a, nullptr));
-    HIPCHK(launch_split_wtimg(a, p->wtimg, p->wtimg_cs, nullptr));
+    if (p->wtimg) HIPCHK(launch_split_wtimg(a, p->wtimg, p->wtimg_cs, nullptr));
     HIPCHK(hipDeviceSynchronize());
     p->img_by_scatter = true;
     return 0;
@@ -721,8 +723,6 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         // pre-split weight images of the bf16x6 fused forward (layers 1.. of both nets)
         p->wimg_cs = (int64_t)(p->nets[0].L.size() - 1 + p->nets[1].L.size() - 1) * FWD_WIMG;
         if (int rc = p->alloc(&p->wimg, p->wimg_cs * C)) return rc;
-        p->wtimg_cs = (int64_t)(p->nets[0].L.size() - 1 + p->nets[1].L.size() - 1) * BWD_WTIMG;
-        if (int rc = p->alloc(&p->wtimg, p->wtimg_cs * C)) return rc;
         p->qsplitA_cs = (int64_t)cdiv(p->N, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
         if (int rc = p->alloc(&p->qsplitA, p->qsplitA_cs * C)) return rc;
         p->qsplitB_cs = (int64_t)cdiv(p->P, CONTRACT_SPLIT_ROWS) * CONTRACT_SPLIT_BLOCK;
@@ -779,6 +779,18 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         }
         n.dwpart_cs = r64(po);
         if (int rc = p->alloc(&n.dwpart, n.dwpart_cs * C)) return rc;
+    }
+    // the whole-network backward's W^T images (k_bwd_chain), only for plans whose backward chunks can be its 64 rows:
+    // at larger chain counts nothing reads them, and the scatter would keep them current for nothing (four of its
+    // ~ten scattered stores per sampled weight)
+    if (p->W == 100) {
+        bool chain_rows = true;
+        for (int net = 0; net < 2; ++net)
+            for (const LayerPk& L : p->nets[net].L) chain_rows &= L.rows_per_chunk == bwd_chain_rows();
+        if (chain_rows) {
+            p->wtimg_cs = (int64_t)(p->nets[0].L.size() - 1 + p->nets[1].L.size() - 1) * BWD_WTIMG;
+            if (int rc = p->alloc(&p->wtimg, p->wtimg_cs * C)) return rc;
+        }
     }
     // contraction side B (branch-owner) partials over trunk chunks
     {
@@ -1000,8 +1012,10 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
             a.net[0].wimg_cs = a.net[1].wimg_cs = p->wimg_cs;
             if (!p->img_by_scatter) {
                 HIPCHK(launch_split_wimg(a, s));
-                HIPCHK(launch_split_wtimg(a, p->wtimg, p->wtimg_cs, s));
-                p->timg_live = true;
+                if (p->wtimg) {
+                    HIPCHK(launch_split_wtimg(a, p->wtimg, p->wtimg_cs, s));
+                    p->timg_live = true;
+                }
             }
         }
         HIPCHK(launch_fwd_fused_bf(a, nwb, s));
