@@ -189,26 +189,29 @@ __global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
 //   Gram-b (c, s): the same over the branch blocks [s SLb, (s+1) SLb) into gb_part; k_gram_sum writes -Gb pre-split
 //     as 4 blocks (rows v, k of the extension).
 // ---------------------------------------------------------------------------------------------------------------
+template <int GT>
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     int list, u;
-    unit_of(blockIdx.x, A.upx_a, A.NG * A.S * A.C, A.C * (A.St + A.Sb), list, u);
+    constexpr int NGT = GT > 0 ? 0 : 1;  // Gram-t units of their own (GT = 0: the T_b units take no Gram-t tiles)
+    unit_of(blockIdx.x, A.upx_a, A.NG * A.S * A.C, A.C * (NGT * A.St + A.Sb), list, u);
     if (list < 0) return;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     // decode the unit
-    int c, s = 0, ng = 0, kind;          // kind 0 = T_b, 1 = Gram-t, 2 = Gram-b
+    int c, s = 0, ng = 0, kind;          // kind 0 = T_b (GT > 0: + its share of the slab's Gram-t tiles), 1 = Gram-t,
+                                         // 2 = Gram-b
     if (list == 0) {
         const int g = u / A.C;
         c = u - g * A.C;
         s = g / A.NG;
         ng = g - s * A.NG;
         kind = 0;
-    } else if (u < A.C * A.St) {
+    } else if (u < NGT * A.C * A.St) {
         c = u / A.St;
         s = u - c * A.St;
         kind = 1;
     } else {
-        const int u2 = u - A.C * A.St;
+        const int u2 = u - NGT * A.C * A.St;
         c = u2 / A.Sb;
         s = u2 - c * A.Sb;
         kind = 2;
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         nb = min(A.SLb, A.nblkN - kb0);
         src0 = A.bimg + c * A.bimg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
     } else if (kind == 1) {
-        kb0 = s * A.SLt;                  // Gram-t slab s: its own split (St, SLt) of the trunk blocks
+        kb0 = s * A.SLt;                  // Gram-t slab s: the T_b slab's trunk blocks
         nb = min(A.SLt, A.nblkP - kb0);
         src0 = A.timg + c * A.timg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
     } else {
@@ -264,19 +267,48 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
             for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // this unit's share of the slab's Gram-t tiles: the NG units of (s, c) stream the same trunk blocks, so wave
+        // w of unit ng takes tiles j = 8 ng + w + 8 NG q (q < GT) of the 28 upper tiles -- no Gram-t units of their
+        // own (which re-streamed the blocks: 128 of 656 k_gram_a units at 16 chains). Per block and tile the same
+        // products and fp64 accumulation as a Gram unit: the same slab values bit for bit.
+        constexpr int G1 = GT > 0 ? GT : 1;
+        double accg[G1][4];
+        int gvt[G1], gtt[G1], gj[G1];
+#pragma unroll
+        for (int q = 0; q < G1; ++q) {
+            gj[q] = GT > 0 ? GR_CW * ng + wave + GR_CW * A.NG * q : 28;     // wave-uniform
+            int rem = min(gj[q], 27), vt = 0;
+            while (rem >= 7 - vt) rem -= 7 - vt++;
+            gvt[q] = vt;
+            gtt[q] = vt + rem;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) accg[q][r] = 0.0;
+        }
         auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
             __syncthreads();
             GR_ST(i, 0)
             const int ii = (GR_ABL & 1) ? 0 : min(i + 1, nb - 1);
             GR_ST(i, 1)
+            const unsigned char* buf = lds + (i % GR_NBUF) * GR_BLK;
             // the next block's A loads, one per tile under this block's MFMAs
-            mma_block(lds + (i % GR_NBUF) * GR_BLK, tro, a, acc, [&](int t) __attribute__((always_inline)) {
+            mma_block(buf, tro, a, acc, [&](int t) __attribute__((always_inline)) {
                 if (t < 6) {
                     const int rt = t / 3, pl = t % 3;
                     an[rt][pl] = *reinterpret_cast<const bf16x8*>(ya + pl * A.ya_plane + rt * rt16 + 32 * ii);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             });
+#pragma unroll
+            for (int q = 0; q < G1; ++q) {
+                if (GT > 0 && gj[q] < 28) {
+                    bf16x8 ga[3], gb[3];
+                    load_b(buf, tro, gvt[q], ga);
+                    load_b(buf, tro, gtt[q], gb);
+                    const f32x4 blk = six(ga, gb, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) accg[q][r] += (double)blk[r];
+                }
+            }
 #if GR_STAMP
             __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -294,6 +326,13 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
             for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(dst + (rt * 7 + t) * 256) = acc[rt][t];
+        double* gpart = A.gt_part + c * A.gt_cs;
+#pragma unroll
+        for (int q = 0; q < G1; ++q)
+            if (GT > 0 && gj[q] < 28) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gpart[((s * 28) + gj[q]) * 256 + 4 * lane + r] = accg[q][r];
+            }
 #if GR_STAMP
         if (gr_samp && tid == 0) {
             gr_real[gr_sidx][1][0] = __builtin_amdgcn_s_memtime();
@@ -689,17 +728,22 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
         return hipErrorInvalidValue;
     if (a.SB < 1 || a.SLB < 1 || a.SB * a.SLB < a.nblkN || (a.SB - 1) * a.SLB >= a.nblkN || (a.SB > 1 && !a.tt_part))
         return hipErrorInvalidValue;
-    if (a.St < 1 || a.SLt < 1 || a.St * a.SLt < a.nblkP || (a.St - 1) * a.SLt >= a.nblkP) return hipErrorInvalidValue;
+    if (a.St != a.S || a.SLt != a.SL) return hipErrorInvalidValue;   // the Gram-t tiles ride the T_b slabs
     if (a.Sb < 1 || a.SLb < 1 || a.Sb * a.SLb < a.nblkN || (a.Sb - 1) * a.SLb >= a.nblkN || !a.gb_part)
         return hipErrorInvalidValue;
     if (a.S > GRAM_TB_DIRECT ? !a.tb_sum : a.tb_sum != nullptr) return hipErrorInvalidValue;
-    const int n1 = a.NG * a.S * a.C, n2 = a.C * (a.St + a.Sb);
+    // the T_b units take the Gram-t tiles (one per wave) when a slab has >= 4 of them (>= 32 waves for 28 tiles);
+    // fewer n groups keep the Gram-t units (two or four tiles per T_b wave spill registers)
+    const int gt = a.NG >= 4 ? 1 : 0;
+    const int n1 = a.NG * a.S * a.C, n2 = a.C * ((gt ? 0 : a.St) + a.Sb);
     a.upx_a = (n1 + 7) / 8;
     const int gpx = (n2 + 7) / 8;
     a.upx_b = (a.PT * a.SB * a.C + 7) / 8;
     const int cpx = (a.C * ((a.N + 31) / 32) + 7) / 8;
     if (!a.aug_done) hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_gram_a, dim3(8 * (a.upx_a + gpx)), dim3(GR_THREADS), GR_LDS, s, a);
+    const dim3 ga(8 * (a.upx_a + gpx));
+    if (gt) hipLaunchKernelGGL(k_gram_a<1>, ga, dim3(GR_THREADS), GR_LDS, s, a);
+    else hipLaunchKernelGGL(k_gram_a<0>, ga, dim3(GR_THREADS), GR_LDS, s, a);
     hipLaunchKernelGGL(k_gram_sum, dim3(56 + (a.tb_sum ? a.NG * 28 : 0), a.C), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gram_b, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GR_LDS, s, a);
     if (a.SB > 1) hipLaunchKernelGGL(k_gram_tt, dim3(a.PT * GR_CW, a.C), dim3(64), 0, s, a);
