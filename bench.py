@@ -139,7 +139,8 @@ def cpu_throughput(procs, seconds, L, step_size):
 KCLASS = {0: ("contract_a", "k_contract_bf", "side-A contraction: S = Z_b Z_t^T + b, Gaussian NLL, G, dZ_trunk"),
           1: ("contract_b", "k_contract_bf_b", "side-B contraction: dZ_branch = G Z_trunk"),
           2: ("bwd", "k_bwd_bf2", "layer backward (dX and dW of both MLPs), one launch per layer"),
-          3: ("fwd", "k_fwd_fused_bf", "fused hidden-layer forward of both MLPs (layers 1..8)"),
+          3: ("fwd", "k_fwd_fused_bf", "fused forward of both MLPs (layers 1..8; with plan option fwd_in0 also the "
+                                       "input layers, on the f32 MFMA)"),
           6: ("gram", "k_gram_a + k_gram_b",
               "Gram-form gradient-only contraction of the inner leapfrog steps: y Zt^, y^T Zb^, Gram terms, dZ "
               "epilogues (one HIP-event pair around both launches)")}
@@ -153,10 +154,19 @@ def mfma_peak(bf16x6: int) -> float:
     return BF16_PEAK_TFLOPS / BF16X6_PRODUCTS if bf16x6 else FP32_PEAK_TFLOPS
 
 
-def class_table(eng, spec, prob, C, evals):
-    """Per-class HIP-event times recorded over `evals` evaluations -> per-launch roofline numbers."""
+def class_flops(eng, spec, prob):
+    """Algorithmic FLOP per chain of each timing class (the input layers count with the forward when its launch runs
+    them: plan option fwd_in0)."""
     fl = spec.flops_by_kernel(prob.N, prob.P)
     fl["gram"] = spec.flops_gram(prob.N, prob.P)
+    if eng.get_option("fwd_in0"):
+        fl["fwd"] += fl["input"]
+    return fl
+
+
+def class_table(eng, spec, prob, C, evals):
+    """Per-class HIP-event times recorded over `evals` evaluations -> per-launch roofline numbers."""
+    fl = class_flops(eng, spec, prob)
     forms = {"contract_a": eng.get_option("contract_bf16x6"), "contract_b": eng.get_option("contract_bf16x6"),
              "bwd": eng.get_option("bwd_bf16x6"), "fwd": eng.get_option("fwd_bf16x6"), "gram": 1}
     ev_ms, ev_n = eng.timing_class(T_EVAL)
@@ -441,8 +451,7 @@ def main():
     leapfrog = world * C * args.L * args.steps
     value = leapfrog / T
     key, kname, what = KCLASS[dom_cls]
-    fl = spec.flops_by_kernel(prob.N, prob.P)
-    fl["gram"] = spec.flops_gram(prob.N, prob.P)
+    fl = class_flops(eng, spec, prob)
     per_eval = cal[key]["launches_per_eval"]
     flops_launch = C * fl[key] / max(per_eval, 1.0)
     avg_s = (k_ms / max(k_n, 1)) / 1e3

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Two builds A/B on the one-chain legs (round 4): bitwise dumps (dump_eval.py), the bench's one-chain legs
+# (probe_legs.py) and the 16-chain class timings, alternating A, B, A, B. A = diagbuild/$A.so, B = diagbuild/$B.so.
+TAG=${TAG:-r04legs}; A=${A:-base}; B=${B:-lat}
+O=gpurun_out/${TAG}.txt
+D=${GRAFT_REPO_ROOT:-$(pwd)}/diagbuild
+: > $O
+for L in $A $B; do
+  VIHMC_LIB=$D/$L.so timeout -k 10 100 python -u profiles/scripts/diag/dump_eval.py gpurun_out/dump_$L.npz >> $O 2>&1 || exit 1
+done
+python profiles/scripts/diag/dump_eval.py --compare gpurun_out/dump_$A.npz gpurun_out/dump_$B.npz >> $O 2>&1
+for rep in 1 2; do
+  for L in $A $B; do
+    echo "== $L rep $rep" >> $O
+    VIHMC_LIB=$D/$L.so timeout -k 10 150 python -u profiles/scripts/probes/probe_legs.py --reps 1 >> $O 2>&1 || exit 1
+    VIHMC_LIB=$D/$L.so timeout -k 10 100 python -u profiles/scripts/probes/probe_classes.py --chains 16 --iters 30 --grad >> $O 2>&1 || exit 1
+  done
+done
+grep -v amdgpu.ids $O

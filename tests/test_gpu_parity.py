@@ -167,6 +167,33 @@ def test_forward_without_weight_images_matches(cuda_device):
     parity.check("grad_relnorm", dg.max(), "fwd_wimg 0 vs 1")
 
 
+@pytest.mark.parametrize("C", [1, 16])
+def test_input_layer_in_forward_launch_bitwise(C, cuda_device):
+    """Plan option fwd_in0 (default 1): the input layers of both nets run inside the bf16x6 forward's launch
+    (FusedNet::x) == the separate row-dot launch (fwd_in0 = 0), bit for bit: log-prob, gradient (both contraction
+    forms: a gradient-only call runs the Gram form from 4 chains) and the activations the backward reads."""
+    c = deeponet_case("deeponet_burgers")
+    rng = np.random.default_rng(12)
+    base = c.thetas[0]
+    seq = [torch.tensor(np.stack([base + 0.01 * rng.standard_normal(base.size).astype(np.float32) for _ in range(C)]),
+                        device=cuda_device) for _ in range(2)]
+    res = []
+    for on in (1, 0):
+        eng = engine_for(c, max_chains=C)
+        eng.option("fwd_in0", on)
+        assert eng.get_option("fwd_in0") == on
+        out = []
+        for th in seq:
+            lp, g = eng.logp_grad(th)
+            out += [lp.cpu(), g.cpu(), torch.from_numpy(eng.debug_buffer("act_b").copy()),
+                    torch.from_numpy(eng.debug_buffer("act_t").copy())]
+            out.append(eng.grad(th).cpu())
+        res.append(out)
+        eng.close()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_weight_images_kept_by_scatter_bitwise(cuda_device):
     """Weight images split once per plan and kept current by the scatter (default) == split from the packed weights
     every evaluation (plan option img_scatter = 0), bit for bit, over a sequence of different thetas per chain and across a

@@ -137,20 +137,39 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
         const float* H = L.H + c * L.h_cs + (int64_t)r0 * L.ldh;
         const __amdgpu_buffer_rsrc_t drs = bf6::make_rsrc(D, (uint32_t)((M - r0) * N.ldd * 4));
         const __amdgpu_buffer_rsrc_t hrs = bf6::make_rsrc(H, (uint32_t)((M - r0) * L.ldh * 4));
-        for (int e = tid; e < CH_ROWS * 25; e += CH_THREADS) {
+        // every piece's load issued before the first store (the strided loops waited out one load per piece: 6
+        // serial round trips before the first layer)
+        constexpr int NP = (CH_ROWS * 25 + CH_THREADS - 1) / CH_THREADS;
+        static_assert(NP == 3, "prologue pieces per thread");
+        f32x4 xd[NP], xh[NP];
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int e = tid + CH_THREADS * u;
             uint32_t voff, loff;
             int c4, row;
-            item_offsets(e, 25, N.ldd, -1, voff, loff, c4, row);
-            const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(drs, voff, 0, 0));
-            store_planes(sm + CH_DP + loff, x);
-            if (c4 == 24) *reinterpret_cast<f32x4*>(sm + (row >> 5) * CH_BUF + CH_DT + (row & 31) * 16) = x;
+            if (e < CH_ROWS * 25) {
+                item_offsets(e, 25, N.ldd, -1, voff, loff, c4, row);
+                xd[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(drs, voff, 0, 0));
+            }
+            if (e < CH_ROWS * hq) {
+                item_offsets(e, hq, L.ldh, 0, voff, loff, c4, row);
+                xh[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hrs, voff, 0, 0));
+            }
         }
-        for (int e = tid; e < CH_ROWS * hq; e += CH_THREADS) {
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int e = tid + CH_THREADS * u;
             uint32_t voff, loff;
             int c4, row;
-            item_offsets(e, hq, L.ldh, 0, voff, loff, c4, row);
-            const f32x4 x = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hrs, voff, 0, 0));
-            store_planes(sm + loff, x);
+            if (e < CH_ROWS * 25) {
+                item_offsets(e, 25, N.ldd, -1, voff, loff, c4, row);
+                store_planes(sm + CH_DP + loff, xd[u]);
+                if (c4 == 24) *reinterpret_cast<f32x4*>(sm + (row >> 5) * CH_BUF + CH_DT + (row & 31) * 16) = xd[u];
+            }
+            if (e < CH_ROWS * hq) {
+                item_offsets(e, hq, L.ldh, 0, voff, loff, c4, row);
+                store_planes(sm + loff, xh[u]);
+            }
         }
         db_column(0, 4 * hq, tid);
     }

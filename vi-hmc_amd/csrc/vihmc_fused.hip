@@ -434,6 +434,78 @@ __device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, co
 #ifndef FWD_STAMP
 #define FWD_STAMP 0   // timing-only instrumentation (variant builds): per-layer phase stamps of k_fwd_fused_bf
 #endif
+// ---- input layer in the forward launch (FusedNet::x): network layer 0 of the wave's 16 rows on the f32 MFMA, every
+// tile's products in k_rowdot_in's order (16-long k blocks .x .y .z .w, then the 4-wide tail steps) and its epilogue
+// (tanh_f = the row-dot epilogue's tanh_cheap; columns >= 100 zero), so h_0 is bitwise the separate launch's. Saves
+// that launch and the re-read of h_0: the lanes' accumulators are the layer walk's operand layout already (tile 6
+// moved into its f32-tail form by four shuffles).
+constexpr int IN0_KMAX = 111;                       // 6 full 16-long k blocks + <= 4 tail steps
+__host__ __device__ constexpr int in0_ldw(int k4) { return k4 + ((24 - (k4 & 15)) & 15); }   // rowdot_ldb
+__device__ __forceinline__ float in0_act(int act, float z) {
+    if (act == ACT_TANH) return tanh_f(z);
+    if (act == ACT_RELU) return fmaxf(z, 0.f);
+    return z;
+}
+
+// x operand of the wave's row: a[kb] = x[16 kb + 4 lg .. + 3] (kb < nkb), atl[q] = x[16 nkb + 4 q + lg] (q < ntl)
+__device__ __forceinline__ void in0_load_x(const FusedNet& N, int rowc, int lg, float4 (&a)[6], float (&atl)[4]) {
+    const float* xr = N.x + (int64_t)rowc * N.ldx;
+    const int nkb = N.k0 >> 4, ntl = (((N.k0 + 3) & ~3) - 16 * nkb) >> 2;
+#pragma unroll
+    for (int kb = 0; kb < 6; ++kb)
+        if (kb < nkb) a[kb] = *reinterpret_cast<const float4*>(xr + 16 * kb + 4 * lg);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (q < ntl) atl[q] = xr[16 * nkb + 4 * q + lg];
+}
+
+__device__ __forceinline__ void in0_layer(const FusedNet& N, const float* w0s, const float* bias, const float4 (&a)[6],
+                                          const float (&atl)[4], int lr, int lg, __amdgpu_buffer_rsrc_t hrs,
+                                          uint32_t hoff, float4 (&h)[7]) {
+    const int nkb = N.k0 >> 4, ntl = (((N.k0 + 3) & ~3) - 16 * nkb) >> 2;
+    const int ldw = in0_ldw((N.k0 + 3) & ~3);
+    float4 o6;
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        const float* wr = w0s + min(16 * t + lr, FW - 1) * ldw;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < 6; ++kb) {
+            if (kb < nkb) {
+                const float4 w = *reinterpret_cast<const float4*>(wr + 16 * kb + 4 * lg);
+                acc = mfma_f(w.x, a[kb].x, acc);
+                acc = mfma_f(w.y, a[kb].y, acc);
+                acc = mfma_f(w.z, a[kb].z, acc);
+                acc = mfma_f(w.w, a[kb].w, acc);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (q < ntl) acc = mfma_f(wr[16 * nkb + 4 * q + lg], atl[q], acc);
+        const int n = 16 * t + 4 * lg;
+        const float4 bv = n < FW ? *reinterpret_cast<const float4*>(bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+        float4 o;
+        o.x = n + 0 < FW ? in0_act(N.act0, acc[0] + bv.x) : 0.f;
+        o.y = n + 1 < FW ? in0_act(N.act0, acc[1] + bv.y) : 0.f;
+        o.z = n + 2 < FW ? in0_act(N.act0, acc[2] + bv.z) : 0.f;
+        o.w = n + 3 < FW ? in0_act(N.act0, acc[3] + bv.w) : 0.f;
+        // columns past the row stride and rows >= M (hoff already out of range) are dropped
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), hrs, n < N.ldin ? hoff + 4u * n : OOB, 0,
+                                               0);
+        if (t < 6) h[t] = o;
+        else o6 = o;
+    }
+    // tile 6: lane (lr, 0) holds h[96..99]; the layer walk wants h[96 + lg] in register 0 of lane (lr, lg)
+    // (FWD_TAILF32), or the accumulator form itself (zeros beyond column 99)
+    if (FWD_TAILF32) {
+        const float v0 = __shfl(o6.x, lr, 64), v1 = __shfl(o6.y, lr, 64), v2 = __shfl(o6.z, lr, 64),
+                    v3 = __shfl(o6.w, lr, 64);
+        h[6] = float4{lg == 0 ? v0 : (lg == 1 ? v1 : (lg == 2 ? v2 : v3)), 0.f, 0.f, 0.f};
+    } else {
+        h[6] = o6;
+    }
+}
+
 #if FWD_STAMP
 // every 8th workgroup (the first 16): per wave (compute, then DMA) and layer s_memtime after the layer's barrier [0],
 // after the operand split (compute) / the DMA issue (DMA waves) [1], after the layer's MFMAs + epilogue + h stores
@@ -562,18 +634,47 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
         VIHMC_FB_LOAD(0)
     }
     float4 h[7];
-    {
+    float4 xa[6];
+    float xt[4];
+    if (N.x != nullptr) {
+        // input layer in this launch: W0 into buffer 1 (layer 1's image goes there only after the first loop barrier),
+        // every piece's load issued before the stores; the row's x operand prefetched
+        const int q4 = ((N.k0 + 3) & ~3) >> 2, n4 = FW * q4, ldw = in0_ldw(4 * q4);
+        const float* W0 = Wc + N.w0_off;
+        float* w0s = reinterpret_cast<float*>(fsmb + FWD_WIMG);
+        constexpr int SP = (FW * ((IN0_KMAX + 3) / 4) + FTHREADS - 1) / FTHREADS;
+        f32x4 wv[SP];
+#pragma unroll
+        for (int u = 0; u < SP; ++u) {
+            const int i = min(tid + FTHREADS * u, n4 - 1);        // clamped slots rewrite the last piece (same value)
+            const int r = i / q4, c4 = i - r * q4;
+            wv[u] = *reinterpret_cast<const f32x4*>(W0 + (int64_t)r * N.ldw0 + 4 * c4);
+        }
+        in0_load_x(N, rowc, lg, xa, xt);
+#pragma unroll
+        for (int u = 0; u < SP; ++u) {
+            const int i = min(tid + FTHREADS * u, n4 - 1);
+            const int r = i / q4, c4 = i - r * q4;
+            *reinterpret_cast<f32x4*>(w0s + r * ldw + 4 * c4) = wv[u];
+        }
+    } else {
         const float* ar = N.in + c * N.in_cs + (int64_t)rowc * N.ldin;
 #pragma unroll
         for (int t = 0; t < 6; ++t) h[t] = *reinterpret_cast<const float4*>(ar + 16 * t + 4 * lg);
         if (FWD_TAILF32) h[6] = float4{ar[96 + lg], 0.f, 0.f, 0.f};
         else h[6] = lg == 0 ? *reinterpret_cast<const float4*>(ar + 96) : float4{0.f, 0.f, 0.f, 0.f};
     }
-    __syncthreads();                            // zero fill done before the staging writes
+    __syncthreads();                            // zero fill done before the staging writes (and W0 staged)
     if (!dma) {
         VIHMC_FB_STORE(0)
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);         // see k_fwd_fused: no vmcnt waits inside the layer loop
+    if (N.x != nullptr) {
+        float* h0 = const_cast<float*>(N.in) + c * N.in_cs;
+        const __amdgpu_buffer_rsrc_t hrs = make_rsrc(h0, (uint32_t)N.rows * (uint32_t)N.ldin * 4u);
+        in0_layer(N, reinterpret_cast<const float*>(fsmb + FWD_WIMG), Wc + N.b0_off, xa, xt, lr, lg, hrs,
+                  rok ? (uint32_t)row * (uint32_t)N.ldin * 4u : OOB, h);
+    }
     const float* outc = N.out + c * N.out_cs;
     const uint32_t ooff = rok ? (uint32_t)row * (uint32_t)N.ldo * 4u : OOB;
     const uint32_t obytes = (uint32_t)N.rows * (uint32_t)N.ldo * 4u;
@@ -779,6 +880,15 @@ size_t fwd_fused_bf_lds_bytes() { return 2 * (size_t)FWD_WIMG; }
 static_assert(BBUF <= FWD_WIMG && FWD_WTAIL + FW * 16 <= FWD_WIMG && FWD_WIMG % 1024 == 0 &&
               2 * FWD_WIMG <= 160 * 1024, "weight image");
 bool fwd_fused_bf_needs_wimg() { return FWD_TAILF32 != 0; }
+
+// an input layer [100][n_in] (x row stride ldx, W0 row stride ldw) the bf16x6 forward can run in its launch (the
+// pre-split-image form: FWD_TAILF32; W0 staged in one image buffer; its tanh the row-dot epilogue's)
+bool fwd_fused_in0_ok(int n_in, int ldx, int ldw) {
+    const int k4 = (n_in + 3) & ~3;
+    return FWD_TAILF32 && FWD_TANH_CHEAP && FWD_ABL == 0 && n_in >= 1 && n_in <= IN0_KMAX && ldx >= k4 &&
+           (n_in < 16 || (ldx & 3) == 0) && ldw >= k4 && (ldw & 3) == 0 &&
+           (size_t)FW * in0_ldw(k4) * sizeof(float) <= (size_t)FWD_WIMG;
+}
 
 #if FWD_STAMP
 extern "C" int vihmc_debug_fwd_stamps(void* stamps, size_t stamp_bytes, void* real, size_t real_bytes) {

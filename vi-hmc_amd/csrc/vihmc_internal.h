@@ -310,6 +310,11 @@ struct FusedNet {
     int32_t aug;                                    // feature 100 of that image: 0 = zero, 1 = one (branch),
                                                     // 2 = the chain's output bias b0 (trunk): the Gram form's
                                                     // augmented outputs (vihmc_gram.hip; unused by the other paths)
+    // the input layer (network layer 0) in the same launch (x != null; the pre-split-image form only): h_0 = act0(x
+    // W0^T + b0) on the f32 MFMA in k_rowdot_in's product order, stored at `in` (row stride ldin) and carried on in
+    // registers instead of re-read; W0 [n0 = 100][k0] (packed, row stride ldw0) staged in LDS buffer 1
+    const float* x; int32_t ldx, k0, ldw0, act0;
+    int64_t w0_off, b0_off;
 };
 struct FusedArgs {
     FusedNet net[2];
@@ -326,6 +331,7 @@ int fwd_img_plane_stride();
 int fwd_img_bias_off(int n);
 int fwd_img_tail_off(int n, int col);
 bool fwd_fused_bf_needs_wimg();                     // the bf16x6 forward reads the fp32 k tail of the image
+bool fwd_fused_in0_ok(int n_in, int ldx, int ldw);  // an input layer of this shape fits the fused forward
 int fwd_fused_bf_waves();                           // its waves per workgroup (16 rows each)
 // Nonzero when a translation unit was built with a timing-only ablation (FWD_ABL, CB_ABL, BB_ABL, RD_ONLY_FIRST: wrong
 // results) or phase-stamp instrumentation (CB_STAMP, BB_STAMP). vihmc_version() reports them and plan

@@ -62,43 +62,60 @@ __global__ void k_init_packed(float* packed, int64_t dp, const float* frozen, co
     }
 }
 
-// sampled value k of chain c -> packed W, W^T and (when kept by the scatter) the forward's weight images
-__device__ __forceinline__ void scatter_one(float* packed, int64_t dp, const int32_t* smap_w, const int32_t* smap_wt,
-                                            const ScatterImg& si, int c, int k, float v) {
-    packed[c * dp + smap_w[k]] = v;
-    const int32_t t = smap_wt[k];
-    if (t >= 0) packed[c * dp + t] = v;
-    if (si.img_w != nullptr) {
+// sampled value k of chain c -> packed W, W^T and (when kept by the scatter) the forward's weight images. The
+// destination offsets are read first (scatter_idx) so a caller can issue them beside its other loads: float
+// stores may alias the float loads that follow them, so a load placed after a store waits for it
+struct ScatterIdx {
+    int32_t w, wt, iw, ifl, tw, tfl;
+};
+__device__ __forceinline__ ScatterIdx scatter_idx(const int32_t* smap_w, const int32_t* smap_wt, const ScatterImg& si,
+                                                  int k) {
+    ScatterIdx x;
+    x.w = smap_w[k];
+    x.wt = smap_wt[k];
+    x.iw = si.img_w != nullptr ? si.img_w[k] : -1;
+    x.ifl = si.img_w != nullptr ? si.img_f[k] : -1;
+    x.tw = si.timg_w != nullptr ? si.timg_w[k] : -1;
+    x.tfl = si.timg_w != nullptr ? si.timg_f[k] : -1;
+    return x;
+}
+
+__device__ __forceinline__ void scatter_store(float* packed, int64_t dp, const ScatterImg& si, int c,
+                                              const ScatterIdx& x, float v) {
+    packed[c * dp + x.w] = v;
+    if (x.wt >= 0) packed[c * dp + x.wt] = v;
+    if (x.iw >= 0 || x.ifl >= 0) {
         unsigned char* img = si.img + c * si.img_cs;
-        const int32_t o = si.img_w[k];
-        if (o >= 0) {
+        if (x.iw >= 0) {
             // the three planes exactly as k_split_wimg splits them
             const __bf16 a = (__bf16)v;
             const float r = v - (float)a;
             const __bf16 b = (__bf16)r;
             const __bf16 cc = (__bf16)(r - (float)b);
-            *reinterpret_cast<__bf16*>(img + o) = a;
-            *reinterpret_cast<__bf16*>(img + o + si.plane) = b;
-            *reinterpret_cast<__bf16*>(img + o + 2 * si.plane) = cc;
+            *reinterpret_cast<__bf16*>(img + x.iw) = a;
+            *reinterpret_cast<__bf16*>(img + x.iw + si.plane) = b;
+            *reinterpret_cast<__bf16*>(img + x.iw + 2 * si.plane) = cc;
         }
-        const int32_t f = si.img_f[k];
-        if (f >= 0) *reinterpret_cast<float*>(img + f) = v;
+        if (x.ifl >= 0) *reinterpret_cast<float*>(img + x.ifl) = v;
     }
-    if (si.timg_w != nullptr) {
+    if (x.tw >= 0 || x.tfl >= 0) {
         unsigned char* img = si.timg + c * si.timg_cs;
-        const int32_t o = si.timg_w[k];
-        if (o >= 0) {
+        if (x.tw >= 0) {
             const __bf16 a = (__bf16)v;
             const float r = v - (float)a;
             const __bf16 b = (__bf16)r;
             const __bf16 cc = (__bf16)(r - (float)b);
-            *reinterpret_cast<__bf16*>(img + o) = a;
-            *reinterpret_cast<__bf16*>(img + o + si.tplane) = b;
-            *reinterpret_cast<__bf16*>(img + o + 2 * si.tplane) = cc;
+            *reinterpret_cast<__bf16*>(img + x.tw) = a;
+            *reinterpret_cast<__bf16*>(img + x.tw + si.tplane) = b;
+            *reinterpret_cast<__bf16*>(img + x.tw + 2 * si.tplane) = cc;
         }
-        const int32_t f = si.timg_f[k];
-        if (f >= 0) *reinterpret_cast<float*>(img + f) = v;
+        if (x.tfl >= 0) *reinterpret_cast<float*>(img + x.tfl) = v;
     }
+}
+
+__device__ __forceinline__ void scatter_one(float* packed, int64_t dp, const int32_t* smap_w, const int32_t* smap_wt,
+                                            const ScatterImg& si, int c, int k, float v) {
+    scatter_store(packed, dp, si, c, scatter_idx(smap_w, smap_wt, si, k), v);
 }
 
 // one element per thread (a grid-stride loop left each thread's scattered stores' index loads serial: 10 us for
@@ -377,8 +394,13 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp
     const float inv_scale = 1.f / prior_scale;
     const float* gpc = gp + c * gp_cs;
     double lp = 0.0;
+    // leapfrog step: its operands (momentum, inverse mass, the scatter's offsets) are loaded with the gather's
+    float e = 0.f;
+    if (LEAP) e = lf.eps[c];
+    const bool scat = LEAP && !lf.last && lf.sc.packed != nullptr;
     for (int kb = k0 + threadIdx.x; kb < k1; kb += GATHER_U * GATHER_THREADS) {
-        float thv[GATHER_U], muv[GATHER_U], ivv[GATHER_U], gpv[GATHER_U];
+        float thv[GATHER_U], muv[GATHER_U], ivv[GATHER_U], gpv[GATHER_U], pv[GATHER_U], imv[GATHER_U];
+        ScatterIdx sx[GATHER_U];
 #pragma unroll
         for (int u = 0; u < GATHER_U; ++u) {
             const int k = min(kb + u * GATHER_THREADS, k1 - 1);
@@ -386,6 +408,11 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp
             muv[u] = prior_mu[k];
             ivv[u] = prior_inv_var[k];
             gpv[u] = gpc[smap[k]];
+            if (LEAP) {
+                pv[u] = lf.p[(int64_t)c * K + k];
+                imv[u] = lf.inv_mass ? lf.inv_mass[k] : 1.f;
+                if (scat) sx[u] = scatter_idx(lf.sc.smap_w, lf.sc.smap_wt, lf.sc.si, k);
+            }
         }
 #pragma unroll
         for (int u = 0; u < GATHER_U; ++u) {
@@ -402,15 +429,14 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp
             if (grad) grad[o] = g;
             if (LEAP) {
 #pragma clang fp contract(off)
-                const float e = lf.eps[c];
-                float pn = lf.p[o] + e * g;
+                float pn = pv[u] + e * g;
                 if (lf.last) {
                     pn = pn - (0.5f * e) * g;
                 } else {
-                    const float step = lf.inv_mass ? (e * lf.inv_mass[k]) * pn : e * pn;
+                    const float step = lf.inv_mass ? (e * imv[u]) * pn : e * pn;
                     const float tn = th + step;
                     lf.th[o] = tn;
-                    if (lf.sc.packed) scatter_one(lf.sc.packed, lf.sc.dp, lf.sc.smap_w, lf.sc.smap_wt, lf.sc.si, c, k, tn);
+                    if (scat) scatter_store(lf.sc.packed, lf.sc.dp, lf.sc.si, c, sx[u], tn);
                 }
                 lf.p[o] = pn;
             }
@@ -450,12 +476,17 @@ __global__ __launch_bounds__(256) void k_leap_open(const float* th_in, float* th
     const float e = eps[c], he = 0.5f * e;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
         const int64_t o = (int64_t)c * K + k;
-        const float pn = p_in[o] + he * g_in[o];
-        const float step = inv_mass ? (e * inv_mass[k]) * pn : e * pn;
+        // every load before the first store (a load after a float store may alias it and waits for it)
+        const float pi = p_in[o], gi = g_in[o], ti = th_in[o];
+        const float im = inv_mass ? inv_mass[k] : 1.f;
+        ScatterIdx sx{};
+        if (sc.packed) sx = scatter_idx(sc.smap_w, sc.smap_wt, sc.si, k);
+        const float pn = pi + he * gi;
+        const float step = inv_mass ? (e * im) * pn : e * pn;
         p_out[o] = pn;
-        const float tn = th_in[o] + step;
+        const float tn = ti + step;
         th_out[o] = tn;
-        if (sc.packed) scatter_one(sc.packed, sc.dp, sc.smap_w, sc.smap_wt, sc.si, c, k, tn);
+        if (sc.packed) scatter_store(sc.packed, sc.dp, sc.si, c, sx, tn);
     }
 }
 

@@ -129,14 +129,27 @@ __device__ __forceinline__ void rowdot_body(const RowdotProb& P, int b, float* b
     const int K4 = (KK + 3) & ~3;
     const int LDB = rowdot_ldb(K4);
 
-    // stage B (rows n < Nn, K4 floats each; global row stride ldb >= K4, zero padded)
+    // stage B (rows n < Nn, K4 floats each; global row stride ldb >= K4, zero padded). The loads of a thread's
+    // pieces go out together (a plain strided loop waited out one load per piece: ~10 serial round trips for the
+    // branch input layer's 100 x 104 block, which set the launch at one chain)
     {
         const int q4 = K4 >> 2;
         const int n4 = P.Nn * q4;
-        for (int i = tid; i < n4; i += 256) {
-            const int r = i / q4, c4 = i - r * q4;
-            *reinterpret_cast<float4*>(bs + r * LDB + 4 * c4) =
-                *reinterpret_cast<const float4*>(B + (int64_t)r * P.ldb + 4 * c4);
+        constexpr int SP = 11;                          // pieces in flight per thread: 100 x 104 in one round
+        for (int i0 = tid; i0 < n4; i0 += 256 * SP) {
+            float4 v[SP];
+#pragma unroll
+            for (int u = 0; u < SP; ++u) {
+                const int i = min(i0 + 256 * u, n4 - 1);   // clamped: every slot loads (stored only if in range)
+                const int r = i / q4, c4 = i - r * q4;
+                v[u] = *reinterpret_cast<const float4*>(B + (int64_t)r * P.ldb + 4 * c4);
+            }
+#pragma unroll
+            for (int u = 0; u < SP; ++u) {                 // (clamped slots rewrite the last piece, same value)
+                const int i = min(i0 + 256 * u, n4 - 1);
+                const int r = i / q4, c4 = i - r * q4;
+                *reinterpret_cast<float4*>(bs + r * LDB + 4 * c4) = v[u];
+            }
         }
     }
     const float* br[NT];

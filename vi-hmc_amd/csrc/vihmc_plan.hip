@@ -201,6 +201,7 @@ struct vihmc_plan {
     int32_t* smap_timg = nullptr;     // per sampled index: byte offset of its W^T-image plane element, or -1
     int32_t* smap_timgf = nullptr;    // ... of its fp32 n-tail copy, or -1
     int fwd_wimg = 1;
+    int fwd_in0 = 1;              // plan option: the input layers inside the bf16x6 forward's launch (FusedNet::x)
     int fuse_scatter = 1;       // plan option: trajectory evaluations take theta already scattered by the leapfrog
     int mlp_fast = 1;             // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
     int bwd_chain = 1;            // plan option: whole-network backward in one launch when the chunks are 64 rows
@@ -981,9 +982,36 @@ void fused_args(vihmc_plan* p, int C, FusedArgs& a) {
     a.net[0].wimg_cs = a.net[1].wimg_cs = p->wimg_cs;
 }
 
-int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
+// the input layers of both nets can run inside the bf16x6 forward's launch (FusedNet::x): the pre-split-image form
+// and an input layer of a shape it stages
+bool fused_input_ok(const vihmc_plan* p) {
+    if (!p->fwd_bf16x6 || !p->fwd_wimg || !p->wimg || !fwd_fused_bf_needs_wimg() || !p->fwd_in0) return false;
+    if ((p->dp & 3) != 0) return false;
+    for (int net = 0; net < 2; ++net) {
+        const Net& n = p->nets[net];
+        const LayerPk& L = n.L[0];
+        if (L.n_out != 100 || (L.wp & 3) != 0 || L.ldo < 100 || !fwd_fused_in0_ok(L.n_in, n.ld_in, L.ldi)) return false;
+    }
+    return true;
+}
+
+int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img, bool in0) {
     FusedArgs a{};
     fused_args(p, C, a);
+    if (in0) {
+        for (int net = 0; net < 2; ++net) {
+            const Net& n = p->nets[net];
+            const LayerPk& L = n.L[0];
+            FusedNet& f = a.net[net];
+            f.x = n.input;
+            f.ldx = n.ld_in;
+            f.k0 = L.n_in;
+            f.ldw0 = L.ldi;
+            f.act0 = L.act;
+            f.w0_off = L.wp;
+            f.b0_off = L.bias;
+        }
+    }
     a.net[0].wimg = a.net[1].wimg = nullptr;           // set below when the bf16x6 kernel stages them
     // 12-wave workgroups (one per CU, 84 KB LDS) unless that grid would leave most of the 256 CUs idle
     const int64_t blocks12 = (int64_t)C * (cdiv(p->nets[0].rows, 192) + cdiv(p->nets[1].rows, 192));
@@ -1031,11 +1059,12 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img) {
 int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img) {
     const int maxl = (int)std::max(p->nets[0].L.size(), p->nets[1].L.size());
     const bool fused = fused_forward_ok(p);
+    const bool in0 = fused && fused_input_ok(p);     // the input layers inside the forward's launch
     for (int j = 0; j < maxl; ++j) {
-        if (j == 1 && fused) {
+        if ((j == 1 && fused) || in0) {
             hipEvent_t stop = nullptr;
             if (int rc = p->timing_begin(VIHMC_T_FWD, s, &stop)) return rc;
-            if (int rc = launch_forward_fused(p, C, s, img)) return rc;
+            if (int rc = launch_forward_fused(p, C, s, img, in0)) return rc;
             if (stop) HIPCHK(hipEventRecord(stop, s));
             return 0;
         }
@@ -1880,7 +1909,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fwd_in0, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1890,6 +1919,7 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "bwd_bf16x6") p->bwd_bf16x6 = value ? 1 : 0;
     else if (k == "graph") p->graph_on = value ? 1 : 0;
     else if (k == "fwd_wimg") p->fwd_wimg = value ? 1 : 0;
+    else if (k == "fwd_in0") p->fwd_in0 = value ? 1 : 0;
     else if (k == "fuse_scatter") p->fuse_scatter = value ? 1 : 0;
     else if (k == "img_scatter") p->img_by_scatter = value && p->smap_img;   // 0: split the images per evaluation
     else if (k == "mlp_fast") p->mlp_fast = value ? 1 : 0;
@@ -1925,6 +1955,7 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "bwd_bf16x6") *value = p->bwd_bf16x6;
     else if (k == "graph") *value = p->graph_on;
     else if (k == "fwd_wimg") *value = p->fwd_wimg;
+    else if (k == "fwd_in0") *value = p->kind == 0 && fused_forward_ok(p) && fused_input_ok(p);
     else if (k == "fuse_scatter") *value = p->fuse_scatter;
     else if (k == "img_scatter") *value = p->img_by_scatter ? 1 : 0;
     else if (k == "mlp_fast") *value = p->mlp_fast && p->kind == 1 && mlp_bnn_fast_ok(p->mlp);

@@ -273,7 +273,8 @@ class _Engine:
 
     def option(self, key: str, value: int):
         """vihmc_plan_option: "fwd_bf16x6" / "contract_bf16x6" / "bwd_bf16x6" (the bf16x6 forms, exact 3-way
-        splits), "graph", "fwd_wimg" (0: the fp32-MFMA fused forward), "img_scatter" (0: the forward's weight images
+        splits), "graph", "fwd_wimg" (0: the fp32-MFMA fused forward), "fwd_in0" (0: the input layers in a launch of
+        their own instead of the bf16x6 forward's), "img_scatter" (0: the forward's weight images
         split every evaluation instead of kept by the scatter), "fuse_scatter" (0: trajectory evaluations run their
         own scatter)."""
         _lib.check(self.L.vihmc_plan_option(self._plan, key.encode(), int(value)), f"vihmc_plan_option({key})")
