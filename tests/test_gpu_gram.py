@@ -151,6 +151,35 @@ def test_gram_deterministic(C, cuda_device):
             assert torch.equal(eng.grad(th), a), (bwd_chain, k)
 
 
+@pytest.mark.parametrize("C", [1, 4])
+def test_gram_without_trunk_fp32_outputs_bitwise(C, cuda_device):
+    """Plan option skip_zt (default 1): an all-Gram evaluation stores no fp32 copy of the trunk's outputs (nothing in
+    it reads one) == storing it (skip_zt = 0), bit for bit, over gradient-only calls interleaved with log-prob
+    evaluations (which store and read it)."""
+    c = deeponet_case("deeponet_burgers")
+    base = np.stack([c.thetas[i % len(c.thetas)] for i in range(C)]).astype(np.float32)
+    rng = np.random.default_rng(23)
+    seq = [torch.tensor(base + 0.01 * rng.standard_normal(base.shape, dtype=np.float32), device=cuda_device)
+           for _ in range(3)]
+    res = []
+    for on in (1, 0):
+        eng = engine_for(c, C, cuda_device)
+        eng.option("skip_zt", on)
+        assert eng.get_option("skip_zt") == on
+        out = []
+        for i, th in enumerate(seq):
+            out.append(eng.grad(th).cpu())
+            assert eng.get_option("gram") & 2
+            if i == 1:
+                lp, g = eng.logp_grad(th)
+                out += [lp.cpu(), g.cpu()]
+            out.append(eng.grad(th).cpu())
+        res.append(out)
+        eng.close()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_gram_deterministic_teacher_shape(cuda_device):
     """The shape that exposed the diagonal-tile race of Gt (64 functions x 21 x 21 points, 4 distinct chains, the
     layer-wise backward; profiles/r04j_nondet3.txt: one element of chain 2's Gt written by two threads with values one

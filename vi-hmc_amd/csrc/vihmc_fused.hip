@@ -692,6 +692,7 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
         const __bf16* wb = reinterpret_cast<const __bf16*>(bbuf);
         const float* bias = reinterpret_cast<const float*>(bbuf + 3 * BPLANE * 2);
         const __amdgpu_buffer_rsrc_t orsrc = make_rsrc(outc + N.h_off[j], obytes);
+        const uint32_t hoffj = (N.skip_last && j == N.nl - 1) ? OOB : ooff;   // stores issued, dropped (vmcnt count)
         bf16x8 hp[3][3];
         const int act = N.act[j];
         if (FWD_TAILF32) {
@@ -703,9 +704,9 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
             FW_ST(j, 1)
             const float* wtail = reinterpret_cast<const float*>(bbuf + FWD_WTAIL);
             const float h6f = h[6].x;
-            if (act == ACT_TANH) tf_layer<ACT_TANH>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
-            else if (act == ACT_RELU) tf_layer<ACT_RELU>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
-            else tf_layer<ACT_ID>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, ooff, h);
+            if (act == ACT_TANH) tf_layer<ACT_TANH>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, hoffj, h);
+            else if (act == ACT_RELU) tf_layer<ACT_RELU>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, hoffj, h);
+            else tf_layer<ACT_ID>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, hoffj, h);
 #if FWD_STAMP
             __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -713,9 +714,9 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
         } else {
             bf16x4 h6[3];
             bf_split_operand(h, hp, h6);
-            if (act == ACT_TANH) bf_layer<ACT_TANH>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
-            else if (act == ACT_RELU) bf_layer<ACT_RELU>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
-            else bf_layer<ACT_ID>(wb, bias, hp, h6, lr, lg, orsrc, ooff, h);
+            if (act == ACT_TANH) bf_layer<ACT_TANH>(wb, bias, hp, h6, lr, lg, orsrc, hoffj, h);
+            else if (act == ACT_RELU) bf_layer<ACT_RELU>(wb, bias, hp, h6, lr, lg, orsrc, hoffj, h);
+            else bf_layer<ACT_ID>(wb, bias, hp, h6, lr, lg, orsrc, hoffj, h);
         }
         if (!dma) {
             VIHMC_FB_STORE((j + 1) & 1)

@@ -315,6 +315,8 @@ struct FusedNet {
     // registers instead of re-read; W0 [n0 = 100][k0] (packed, row stride ldw0) staged in LDS buffer 1
     const float* x; int32_t ldx, k0, ldw0, act0;
     int64_t w0_off, b0_off;
+    int32_t skip_last;                              // the last layer's fp32 rows not stored (its image carries them;
+                                                    // a Gram-form evaluation reads no other copy of the trunk's)
 };
 struct FusedArgs {
     FusedNet net[2];

@@ -202,6 +202,7 @@ struct vihmc_plan {
     int32_t* smap_timgf = nullptr;    // ... of its fp32 n-tail copy, or -1
     int fwd_wimg = 1;
     int fwd_in0 = 1;              // plan option: the input layers inside the bf16x6 forward's launch (FusedNet::x)
+    int skip_zt = 1;              // plan option: all-Gram evaluations store no fp32 copy of the trunk's outputs
     int fuse_scatter = 1;       // plan option: trajectory evaluations take theta already scattered by the leapfrog
     int mlp_fast = 1;             // plan option: the reference BNN shape on the register-resident kernels (vihmc_bnn.hip)
     int bwd_chain = 1;            // plan option: whole-network backward in one launch when the chunks are 64 rows
@@ -995,7 +996,7 @@ bool fused_input_ok(const vihmc_plan* p) {
     return true;
 }
 
-int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img, bool in0) {
+int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img, bool in0, bool gram_only) {
     FusedArgs a{};
     fused_args(p, C, a);
     if (in0) {
@@ -1030,6 +1031,9 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img, bool in0
                 a.net[0].aug = 1;
                 a.net[1].aug = 2;
             }
+            // an all-Gram evaluation reads the trunk's outputs only through this image (the branch's fp32 rows feed
+            // its dZ_b epilogue): their fp32 copy is not stored
+            a.net[1].skip_last = gram_only && p->skip_zt ? 1 : 0;
             p->img_by_fwd = true;
         }
         if (p->fwd_wimg && p->wimg) {
@@ -1056,7 +1060,7 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img, bool in0
 
 // Forward through both MLPs (grouped launches: branch + trunk layer j together); the hidden 100 -> 100
 // stack goes through the fused kernel when its shape allows.
-int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img) {
+int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img, bool gram_only) {
     const int maxl = (int)std::max(p->nets[0].L.size(), p->nets[1].L.size());
     const bool fused = fused_forward_ok(p);
     const bool in0 = fused && fused_input_ok(p);     // the input layers inside the forward's launch
@@ -1064,7 +1068,7 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img) {
         if ((j == 1 && fused) || in0) {
             hipEvent_t stop = nullptr;
             if (int rc = p->timing_begin(VIHMC_T_FWD, s, &stop)) return rc;
-            if (int rc = launch_forward_fused(p, C, s, img, in0)) return rc;
+            if (int rc = launch_forward_fused(p, C, s, img, in0, gram_only)) return rc;
             if (stop) HIPCHK(hipEventRecord(stop, s));
             return 0;
         }
@@ -1226,7 +1230,6 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     // when it runs; otherwise k_split_blocks makes them below
     p->img_by_fwd = false;
     p->timg_live = p->img_by_scatter && p->wtimg;      // the scatter above kept the W^T images current
-    if (int rc = deeponet_forward_layers(p, C, s, want_grad && p->contract_bf16x6 && p->W == 100)) return rc;
     // gradient-only evaluations (no log-prob returned): the Gram-form contraction, which forms no residual; the fit
     // guard sends the chains whose fit is too good for its cancellation to the residual form (both forms in one
     // evaluation, each launch skipping the other form's chains)
@@ -1238,6 +1241,8 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     const bool gram = gram_elig && n_resid < C;          // some chain runs the Gram form
     const bool resid_any = !gram;                        // ... or every chain the residual form
     const bool mixed = gram && n_resid > 0;
+    if (int rc = deeponet_forward_layers(p, C, s, want_grad && p->contract_bf16x6 && p->W == 100, gram && !mixed))
+        return rc;
     p->last_gram = gram;
     p->last_gram_chains = gram ? C - n_resid : 0;
     if (want_grad) {
@@ -1796,7 +1801,7 @@ int deeponet_sensitivity(vihmc_plan* p, const float* theta, const int32_t* pts, 
     a.count = (float)((double)N * npts);
     const ScatterImg si = scatter_img(p);
     e = launch_scatter(p->packed, p->dp, 1, theta, p->K, p->smap_w, p->smap_wt, s, p->img_by_scatter ? &si : nullptr);
-    int rc = e == hipSuccess ? deeponet_forward_layers(p, 1, s, false) : 0;
+    int rc = e == hipSuccess ? deeponet_forward_layers(p, 1, s, false, false) : 0;
     SensArgs* dev_a = nullptr;
     if (e == hipSuccess && rc == 0) e = talloc((void**)&dev_a, sizeof(SensArgs));
     if (e == hipSuccess && rc == 0) e = hipMemcpyAsync(dev_a, &a, sizeof(SensArgs), hipMemcpyHostToDevice, s);
@@ -1909,7 +1914,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fwd_in0, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fwd_in0, skip_zt, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1920,6 +1925,7 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "graph") p->graph_on = value ? 1 : 0;
     else if (k == "fwd_wimg") p->fwd_wimg = value ? 1 : 0;
     else if (k == "fwd_in0") p->fwd_in0 = value ? 1 : 0;
+    else if (k == "skip_zt") p->skip_zt = value ? 1 : 0;
     else if (k == "fuse_scatter") p->fuse_scatter = value ? 1 : 0;
     else if (k == "img_scatter") p->img_by_scatter = value && p->smap_img;   // 0: split the images per evaluation
     else if (k == "mlp_fast") p->mlp_fast = value ? 1 : 0;
@@ -1956,6 +1962,7 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "graph") *value = p->graph_on;
     else if (k == "fwd_wimg") *value = p->fwd_wimg;
     else if (k == "fwd_in0") *value = p->kind == 0 && fused_forward_ok(p) && fused_input_ok(p);
+    else if (k == "skip_zt") *value = p->skip_zt;
     else if (k == "fuse_scatter") *value = p->fuse_scatter;
     else if (k == "img_scatter") *value = p->img_by_scatter ? 1 : 0;
     else if (k == "mlp_fast") *value = p->mlp_fast && p->kind == 1 && mlp_bnn_fast_ok(p->mlp);
