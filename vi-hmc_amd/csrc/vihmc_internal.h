@@ -344,6 +344,7 @@ int diag_switches_bwd_bf();
 int diag_switches_layers();
 int diag_switches_bwd_chain();
 int diag_switches_gram();
+int diag_switches_kernels();
 int diag_switches();
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, int nw, hipStream_t s);     // bf16x6, 12 (or 4) waves

@@ -371,6 +371,12 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
 
 // Gradient gather + prior: grid (GATHER_SPLIT slices, C); each block writes its partial log-prior
 // and the last kernel of the pair adds them in a fixed order.
+#ifndef GATHER_ABL
+#define GATHER_ABL 0   // timing-only ablation (wrong results): 1 = the leapfrog gather scatters nothing into the packed
+                       // weights / images, 2 = nor stores theta / p
+#endif
+int diag_switches_kernels() { return GATHER_ABL; }
+
 #ifndef GATHER_SPLIT_N
 #define GATHER_SPLIT_N 64      // K slices per chain (16: 256 blocks at C = 16, 8.8 us)
 #endif
@@ -435,10 +441,10 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp
                 } else {
                     const float step = lf.inv_mass ? (e * imv[u]) * pn : e * pn;
                     const float tn = th + step;
-                    lf.th[o] = tn;
-                    if (scat) scatter_store(lf.sc.packed, lf.sc.dp, lf.sc.si, c, sx[u], tn);
+                    if (!(GATHER_ABL & 2)) lf.th[o] = tn;
+                    if (scat && !GATHER_ABL) scatter_store(lf.sc.packed, lf.sc.dp, lf.sc.si, c, sx[u], tn);
                 }
-                lf.p[o] = pn;
+                if (!(GATHER_ABL & 2)) lf.p[o] = pn;
             }
         }
     }

@@ -324,8 +324,10 @@ struct vihmc_plan {
         *stop = nullptr;
         if (!((timing_on >> which) & 1)) return 0;
         while (ev_pool.size() < ev_used + 2) {
+            // timing only (read after a stream sync): no system-scope release per record -- with it every event
+            // left a ~6 us gap (cache write-back) before the next launch, inside the bench's timed region
             hipEvent_t e;
-            HIPCHK(hipEventCreate(&e));
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
             ev_pool.push_back(e);
         }
         HIPCHK(hipEventRecord(ev_pool[ev_used], s));
@@ -342,7 +344,7 @@ struct vihmc_plan {
 namespace vihmc {
 int diag_switches() {
     return diag_switches_fused() | diag_switches_contract_bf() | diag_switches_bwd_bf() | diag_switches_layers() |
-           diag_switches_bwd_chain() | diag_switches_gram();
+           diag_switches_bwd_chain() | diag_switches_gram() | diag_switches_kernels();
 }
 }  // namespace vihmc
 
