@@ -212,6 +212,10 @@ def load_traffic(kname, C):
     return total, tj.get("source")
 
 
+EV_STEPS = 3            # one-chain legs: HMC iterations with HIP-event timing after the timed ones
+DOM_EVERY = 4           # the main timed region: the dominant class's HIP events on every 4th evaluation
+
+
 def _timed_steps(runner, warm, steps):
     for _ in range(warm):
         runner.step()
@@ -231,9 +235,12 @@ def leg_deeponet_c1(prob, spec, dev, L, eps, steps=20):
                          0.1, "NLL", 1.0, max_chains=1, device=dev)
     ev = EngineEvaluator(eng)
     th0 = torch.tensor(prob.mu[prob.grad_ind], device=dev)[None]
-    r = HMCRunner(ev, th0, steps + 3, L, eps, rng=ChainRNG(1, eng.K, dev, seeds=[1000]))
-    eng.timing(T_EVAL, True)
+    r = HMCRunner(ev, th0, steps + 3 + EV_STEPS, L, eps, rng=ChainRNG(1, eng.K, dev, seeds=[1000]))
     dt = _timed_steps(r, 3, steps)
+    # the evaluation time from HIP events over a few further steps: at one chain the event records' idle gaps (~12 us
+    # per evaluation) are a measurable share, so they stay out of the throughput's timed steps
+    eng.timing(T_EVAL, True)
+    _timed_steps(r, 0, EV_STEPS)
     ms, n = eng.timing_class(T_EVAL)
     ev_ms = ms / max(n, 1)
     fl = spec.flops_per_grad_eval(prob.N, prob.P)
@@ -258,16 +265,19 @@ def leg_split_c1(spec, dev, L, eps, steps=10):
             for m in range(2)]
     evs = [EngineEvaluator(e) for e in engs]
     th0 = torch.tensor(prob.mu, device=dev)[None]
-    r = HMCRunner(evs, th0, steps + 2, L, eps, integrator=Integrator.SPLITTING,
+    r = HMCRunner(evs, th0, steps + 2 + EV_STEPS, L, eps, integrator=Integrator.SPLITTING,
                   rng=ChainRNG(1, spec.n_params, dev, seeds=[1000]))
-    for e in engs:
-        e.timing(T_EVAL, True)
+    for _ in range(2):
+        r.step()
     for e in evs:
         e.n_grad = e.n_value = 0
-    dt = _timed_steps(r, 2, steps)
+    dt = _timed_steps(r, 0, steps)
+    n_grad = sum(e.n_grad for e in evs)
+    for e in engs:                                   # evaluation times over further steps (see leg_deeponet_c1)
+        e.timing(T_EVAL, True)
+    _timed_steps(r, 0, EV_STEPS)
     ms = sum(e.timing_class(T_EVAL)[0] for e in engs)
     n = sum(e.timing_class(T_EVAL)[1] for e in engs)
-    n_grad = sum(e.n_grad for e in evs)
     out = {"workload": "config 4: full-parameter DeepONet HMC (D = 172,401), Burgers, 2 shards of N/2 = 500, "
                        "Integrator.SPLITTING, 1 chain", "chains": 1, "leapfrog_steps_per_s": steps * L / dt,
            "half_shard_grad_evals_per_s": n_grad / dt, "ms_per_half_shard_eval": ms / max(n, 1),
@@ -404,6 +414,9 @@ def main():
     ev.n_grad = 0
     eng.option("gram_evals", 0)                     # reset the plan's evaluation counters (both forms)
     clock = ShaderClock(dev)
+    # the dominant class under HIP events on every DOM_EVERY-th evaluation of the timed region (each event record
+    # leaves a few-us idle gap before the next launch: instrumentation, not workload)
+    eng.option("timing_every", DOM_EVERY)
     eng.timing(dom_cls, True)
     if world > 1:
         dist.barrier()
@@ -419,6 +432,7 @@ def main():
     t1 = time.perf_counter()
     k_ms, k_n = eng.timing_class(dom_cls)
     eng.timing(-1, False)
+    eng.option("timing_every", 1)
     grad_evals = ev.n_grad
     n_calls, n_gram = eng.get_option("grad_evals"), eng.get_option("gram_evals")
     sclk = clock.mhz()

@@ -181,6 +181,8 @@ struct vihmc_plan {
     // timing hook: HIP events bracket every launch of the enabled kernel classes (vihmc.h VIHMC_T_*) on the
     // evaluation's stream; ev_cls[i] is the class of the event pair (2i, 2i+1)
     int timing_on = 0;              // bit mask of enabled classes
+    int timing_every = 1;           // plan option: events on every n-th DeepONet evaluation only (bench sampling)
+    int64_t n_evals = 0;            // DeepONet evaluations so far (timing_every's phase)
     std::vector<hipEvent_t> ev_pool;
     std::vector<int> ev_cls;       // class of pair i
     std::vector<int> ev_nl;        // launches the pair brackets (the layer backward: one pair around all layers)
@@ -323,6 +325,7 @@ struct vihmc_plan {
     int timing_begin(int which, hipStream_t s, hipEvent_t* stop, int nlaunch = 1) {
         *stop = nullptr;
         if (!((timing_on >> which) & 1)) return 0;
+        if (timing_every > 1 && (n_evals - 1) % timing_every != 0) return 0;
         while (ev_pool.size() < ev_used + 2) {
             // timing only (read after a stream sync): no system-scope release per record -- with it every event
             // left a ~6 us gap (cache write-back) before the next launch, inside the bench's timed region
@@ -1179,6 +1182,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
 int deeponet_eval(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out, hipStream_t s,
                   const LeapArgs* leap = nullptr) {
     if (C < 1 || C > p->maxC) return fail("C must be in [1, max_chains]");
+    ++p->n_evals;
     hipEvent_t stop = nullptr;
     if (int rc = p->timing_begin(VIHMC_T_EVAL, s, &stop)) return rc;
     if (int rc = deeponet_eval_body(p, theta, C, logp, grad, out, s, leap)) return rc;
@@ -1916,7 +1920,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, fwd_wimg, fwd_in0, skip_zt, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, timing_every, fwd_wimg, fwd_in0, skip_zt, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -1928,6 +1932,10 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "fwd_wimg") p->fwd_wimg = value ? 1 : 0;
     else if (k == "fwd_in0") p->fwd_in0 = value ? 1 : 0;
     else if (k == "skip_zt") p->skip_zt = value ? 1 : 0;
+    else if (k == "timing_every") {
+        p->timing_every = std::max(1, value);
+        return 0;                                               // not a kernel choice: graphs stay
+    }
     else if (k == "fuse_scatter") p->fuse_scatter = value ? 1 : 0;
     else if (k == "img_scatter") p->img_by_scatter = value && p->smap_img;   // 0: split the images per evaluation
     else if (k == "mlp_fast") p->mlp_fast = value ? 1 : 0;
@@ -1965,6 +1973,7 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "fwd_wimg") *value = p->fwd_wimg;
     else if (k == "fwd_in0") *value = p->kind == 0 && fused_forward_ok(p) && fused_input_ok(p);
     else if (k == "skip_zt") *value = p->skip_zt;
+    else if (k == "timing_every") *value = p->timing_every;
     else if (k == "fuse_scatter") *value = p->fuse_scatter;
     else if (k == "img_scatter") *value = p->img_by_scatter ? 1 : 0;
     else if (k == "mlp_fast") *value = p->mlp_fast && p->kind == 1 && mlp_bnn_fast_ok(p->mlp);
