@@ -119,6 +119,23 @@ int vihmc_logp_grad(vihmc_plan* p, const float* theta, int C, float* logp, float
  * residual, plan option "gram"); vihmc_trajectory uses the same path for its inner steps. */
 int vihmc_grad(vihmc_plan* p, const float* theta, int C, float* grad, void* stream);
 
+/* One HMC iteration's Metropolis step for C chains of K parameters, all device pointers, one launch. Replaces the
+ * accept block of hamiltorch's sample loop (samplers.py: H0 = -lp0 + ke0, H1 = -lp1 + ke1 from the caller's kinetic
+ * energies [C] of the opening / closing momenta, rho = min(H0 - H1, 0) with NaN -> 0, a chain whose log-prob is not
+ * finite fails (hamiltorch's LogProbError: no accept), accept = rho >= logu[c]), batched as
+ * vihmc.samplers.HMCRunner.step does it: after burn-in (burn = 0) an accepted proposal (th1, lp1, g1) overwrites
+ * the last returned state in place and, when samples != NULL, the state is written to row counts[c] of
+ * samples [C][s_cap][K] (a failed chain's row to row s_cap - 1, uncounted) and counts[c] advances; during burn-in
+ * (burn = 1) th_cur / lp_cur / g_cur receive the proposal, else (failed) the last returned state, else the
+ * fallback th_bp / lp_bp / g_bp, which an accepted proposal replaces. accepted[c * acc_ld + n], trace[c * tr_ld + n]
+ * (the state's log-prob), rho [C] (NaN where failed) and err [C] are written. */
+int vihmc_hmc_accept(int C, int K, int n, int burn, const float* lp0, const float* lp1, const float* ke0,
+                     const float* ke1, const float* logu, const float* th1, const float* g1,
+                     float* th_last, float* lp_last, float* g_last, float* th_bp, float* lp_bp, float* g_bp,
+                     float* th_cur, float* lp_cur, float* g_cur, float* samples, int64_t s_cap, int64_t* counts,
+                     uint8_t* accepted, int64_t acc_ld, float* trace, int64_t tr_ld, float* rho, uint8_t* err,
+                     void* stream);
+
 /* Forward only: logp [C] and the network output out [C, N, P] (DeepONet) or [C, N, out_dim] (BNN).
  * Replaces log_prob_func(..., predict=True) -> (logp, output) (main_VI_HMC_burgers.py:175-176). */
 int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* out, void* stream);

@@ -237,3 +237,117 @@ def test_bnn_register_kernels_match_generic_kernels(cuda_device):
     n = int(res[1].counts.min())
     parity.check("pos_maxabs", float((res[1].samples[:, :n] - res[0].samples[:, :n]).abs().max()),
                  "register vs generic BNN trajectories, 4 x 30 steps")
+
+
+def _accept_reference(lp, lp_new, ke0, ke1, logu):
+    """HMCRunner.step's torch accept block."""
+    d = (-lp + ke0) - (-lp_new + ke1)
+    rho = torch.where(torch.isnan(d), torch.zeros_like(d), torch.clamp(d, max=0.0))
+    ok = torch.isfinite(lp) & torch.isfinite(lp_new)
+    return rho, ok, ok & (rho >= logu)
+
+
+@pytest.mark.parametrize("burn", [0, 1])
+@pytest.mark.parametrize("mass", [False, True])
+def test_hmc_accept_kernel_matches_torch_block(burn, mass, cuda_device):
+    """vihmc_hmc_accept (one launch per HMC iteration) == the torch accept block it replaces, bit for bit: rho
+    (NaN for failed chains), the state selection after burn-in (in place + the sample row, a failed chain's row to
+    the spare last row) and during burn-in (proposal / last returned / fallback), counts, accepted and trace."""
+    import ctypes
+    from vihmc import _lib
+    torch.manual_seed(3)
+    C, K, S, n = 7, 1000, 6, 2
+    dev = cuda_device
+    lp = -torch.rand(C, device=dev) * 10
+    lp_new = lp + 0.05 * torch.randn(C, device=dev)
+    lp_new[2] = float("nan")                            # a failed chain
+    lp[5] = float("-inf")                               # another
+    p0, p1 = torch.randn(C, K, device=dev), torch.randn(C, K, device=dev) * 1.001
+    inv_mass = torch.rand(K, device=dev) + 0.5 if mass else None
+    from vihmc.samplers import _kinetic
+    ke0, ke1 = _kinetic(p0, inv_mass), _kinetic(p1, inv_mass)
+    logu = torch.where(torch.arange(C, device=dev) % 2 == 0, torch.full((C,), -1e-3, device=dev),
+                       torch.full((C,), -50.0, device=dev))
+    rho_ref, ok, acc_ref = _accept_reference(lp, lp_new, ke0, ke1, logu)
+    th1, g1 = torch.randn(C, K, device=dev), torch.randn(C, K, device=dev)
+    last = [torch.randn(C, K, device=dev), lp.clone(), torch.randn(C, K, device=dev)]
+    bp = [torch.randn(C, K, device=dev), torch.randn(C, device=dev), torch.randn(C, K, device=dev)]
+    cur = [torch.empty(C, K, device=dev), torch.empty(C, device=dev), torch.empty(C, K, device=dev)]
+    samples = torch.zeros(C, S, K, device=dev)
+    counts = torch.ones(C, dtype=torch.long, device=dev)
+    accepted = torch.zeros(C, 5, dtype=torch.bool, device=dev)
+    trace = torch.zeros(C, 5, device=dev)
+    rho, err = torch.empty(C, device=dev), torch.empty(C, dtype=torch.uint8, device=dev)
+    exp_last = [t.clone() for t in last]
+    exp_bp = [t.clone() for t in bp]
+
+    def P(t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    L = _lib.lib()
+    _lib.check(L.vihmc_hmc_accept(C, K, n, burn, P(lp), P(lp_new), P(ke0), P(ke1), P(logu), P(th1), P(g1),
+                                  P(last[0]), P(last[1]), P(last[2]), P(bp[0]), P(bp[1]), P(bp[2]), P(cur[0]),
+                                  P(cur[1]), P(cur[2]), P(samples), S, P(counts), P(accepted), accepted.stride(0),
+                                  P(trace), trace.stride(0), P(rho), P(err),
+                                  ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "vihmc_hmc_accept")
+    torch.cuda.synchronize()
+    assert 0 < int(acc_ref.sum()) < C                    # both outcomes exercised
+    assert torch.equal(accepted[:, n], acc_ref)
+    assert torch.equal(err.bool(), ~ok)
+    assert torch.equal(torch.isnan(rho), ~ok)
+    assert torch.equal(rho[ok], rho_ref[ok])
+    new = [th1, lp_new, g1]
+
+    def sel(mask, a, b):
+        return torch.where(mask[:, None] if a.dim() == 2 else mask, a, b)
+    if not burn:
+        nxt = [sel(acc_ref, nw, lr) for nw, lr in zip(new, exp_last)]
+        for a, b in zip(last, nxt):
+            assert torch.equal(a, b) or torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
+        row = torch.where(ok, torch.ones_like(counts), torch.full_like(counts, S - 1))
+        for c in range(C):
+            assert torch.equal(samples[c, int(row[c])], nxt[0][c])
+        assert torch.equal(counts, 1 + ok.long())
+        assert torch.equal(torch.nan_to_num(trace[:, n]), torch.nan_to_num(nxt[1]))
+    else:
+        fb = [sel(~ok, lr, b) for lr, b in zip(exp_last, exp_bp)]
+        nxt = [sel(acc_ref, nw, f) for nw, f in zip(new, fb)]
+        for a, b in zip(cur, nxt):
+            assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
+        for a, b in zip(bp, [sel(acc_ref, nw, b) for nw, b in zip(new, exp_bp)]):
+            assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
+        assert torch.equal(samples, torch.zeros_like(samples)) and torch.equal(counts, torch.ones_like(counts))
+        assert torch.equal(torch.nan_to_num(trace[:, n]), torch.nan_to_num(nxt[1]))
+
+
+@pytest.mark.parametrize("variant", ["hmc", "inv_mass", "nuts"])
+def test_native_accept_equals_torch_accept(variant, cuda_device):
+    """HMCRunner with the Metropolis step in one vihmc_hmc_accept launch == its torch form, on the engine: accept
+    sequences, counts, samples, log-prob traces and (NUTS) adapted step sizes (burn-in and after)."""
+    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.samplers import ChainRNG, EngineEvaluator, HMCRunner, Sampler
+    c = deeponet_case("deeponet_refshape")
+    p = c.prob
+    th0 = torch.tensor(c.thetas[0])
+    C, S, L, eps = 3, 7, 3, 5e-3
+    kw = dict(burn=2)
+    if variant == "inv_mass":
+        kw["inv_mass"] = torch.linspace(0.5, 1.5, th0.numel())
+    if variant == "nuts":
+        kw.update(sampler=Sampler.HMC_NUTS, burn=3)
+    res = []
+    for native in (True, False):
+        eng = DeepONetEngine(c.spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, c.prior_mu,
+                             c.prior_sd, c.loss, c.tau_out, max_chains=C, device=cuda_device)
+        r = HMCRunner(EngineEvaluator(eng), th0[None].repeat(C, 1), S, L, eps,
+                      rng=ChainRNG(C, th0.numel(), cuda_device, seeds=[40 + i for i in range(C)]), **kw)
+        r._accept_native = native
+        for _ in range(S):
+            r.step()
+        res.append(r.result())
+        eng.close()
+    a, b = res
+    assert torch.equal(a.accepted, b.accepted)
+    assert torch.equal(a.counts, b.counts)
+    assert torch.equal(a.samples[:, :int(a.counts.max())], b.samples[:, :int(b.counts.max())])
+    assert torch.equal(a.logp_trace, b.logp_trace)
+    assert a.step_size == b.step_size

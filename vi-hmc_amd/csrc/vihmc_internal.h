@@ -295,6 +295,20 @@ hipError_t launch_gather_trunk(const float* feat_all, int in_t, const float* y_a
 // are prefetched into registers and written to the second of two LDS buffers. h_j of every layer is
 // stored (the backward needs it). Layer j's W block and bias are contiguous in the packed layout.
 constexpr int FUSED_MAXL = 16;
+// vihmc_hmc_accept (k_hmc_accept): one HMC iteration's Metropolis step for C chains of K parameters
+struct AcceptArgs {
+    int32_t K, n, burn;
+    const float *lp0, *lp1, *ke0, *ke1, *logu, *th1, *g1;
+    float *th_last, *lp_last, *g_last;          // the last returned state (updated in place after burn-in)
+    float *th_bp, *lp_bp, *g_bp;                // burn-in fallback (updated in place during burn-in)
+    float *th_cur, *lp_cur, *g_cur;             // burn-in: the current state (output)
+    float* samples; int64_t s_cap; int64_t* counts;   // after burn-in, or null: the sample rows [C][s_cap][K]
+    uint8_t* accepted; int64_t acc_ld;          // accepted[c * acc_ld + n]
+    float* trace; int64_t tr_ld;                // trace[c * tr_ld + n] = the current state's log-prob
+    float* rho; uint8_t* err;                   // [C]: rho (NaN where the chain failed), 1 = failed
+};
+hipError_t launch_hmc_accept(const AcceptArgs& a, int C, hipStream_t s);
+
 struct FusedNet {
     const float* in; int64_t in_cs; int32_t ldin;   // activations feeding the first fused layer
     float* out; int64_t out_cs; int32_t ldo;        // per-chain activation buffer, row stride of h_j

@@ -497,6 +497,80 @@ __global__ __launch_bounds__(256) void k_leap_open(const float* th_in, float* th
 }
 
 // =============================================================================================
+// Metropolis step of one HMC iteration for every chain (hamiltorch sample loop body, SURVEY.md App. A.1;
+// vihmc.samplers.HMCRunner.step): H0 = -lp0 + ke0, H1 = -lp1 + ke1 (the caller's kinetic energies, so the
+// decisions keep the sampler's own summation), rho = min(H0 - H1, 0) (NaN -> 0), ok = both log-probs finite,
+// accept = ok && rho >= log u, and the state selection -- after burn-in the accepted proposal overwrites the last
+// returned state in place and (store) is written as the chain's next sample row (a failed chain's row goes to the
+// spare last row, not counted); during burn-in the current state is the proposal, else (failed) the last returned
+// state, else the burn-in fallback, which an accepted proposal replaces. One block per chain; replaces ~25 small
+// elementwise launches.
+// =============================================================================================
+__global__ __launch_bounds__(256) void k_hmc_accept(AcceptArgs a) {
+    const int c = blockIdx.x;
+    const int64_t o = (int64_t)c * a.K;
+    __shared__ int flags[2];
+    __shared__ int64_t row_s;
+    if (threadIdx.x == 0) {
+#pragma clang fp contract(off)
+        const float lp0 = a.lp0[c], lp1 = a.lp1[c];
+        const float h0 = -lp0 + a.ke0[c], h1 = -lp1 + a.ke1[c];
+        const float d = h0 - h1;
+        const float rho = d != d ? 0.f : fminf(d, 0.f);
+        const bool ok = isfinite(lp0) && isfinite(lp1);
+        const bool acc = ok && rho >= a.logu[c];
+        flags[0] = acc ? 1 : 0;
+        flags[1] = ok ? 0 : 1;
+        a.rho[c] = ok ? rho : __builtin_nanf("");
+        a.err[c] = ok ? 0 : 1;
+        a.accepted[(int64_t)c * a.acc_ld + a.n] = acc ? 1 : 0;
+        float lp_next;
+        if (!a.burn) {
+            if (acc) a.lp_last[c] = lp1;
+            lp_next = acc ? lp1 : a.lp_last[c];
+            if (a.samples) {
+                row_s = ok ? a.counts[c] : a.s_cap - 1;
+                a.counts[c] += ok ? 1 : 0;
+            }
+        } else {
+            lp_next = acc ? lp1 : (ok ? a.lp_bp[c] : a.lp_last[c]);
+            a.lp_cur[c] = lp_next;
+            if (acc) a.lp_bp[c] = lp1;
+        }
+        a.trace[(int64_t)c * a.tr_ld + a.n] = lp_next;
+    }
+    __syncthreads();
+    const bool acc = flags[0] != 0, err = flags[1] != 0;
+    if (!a.burn) {
+        float* srow = a.samples ? a.samples + ((int64_t)c * a.s_cap + row_s) * a.K : nullptr;
+        for (int k = threadIdx.x; k < a.K; k += blockDim.x) {
+            float th = a.th_last[o + k];
+            if (acc) {
+                th = a.th1[o + k];
+                a.th_last[o + k] = th;
+                a.g_last[o + k] = a.g1[o + k];
+            }
+            if (srow) srow[k] = th;
+        }
+    } else {
+        for (int k = threadIdx.x; k < a.K; k += blockDim.x) {
+            const float tn = a.th1[o + k], gn = a.g1[o + k];
+            a.th_cur[o + k] = acc ? tn : (err ? a.th_last[o + k] : a.th_bp[o + k]);
+            a.g_cur[o + k] = acc ? gn : (err ? a.g_last[o + k] : a.g_bp[o + k]);
+            if (acc) {
+                a.th_bp[o + k] = tn;
+                a.g_bp[o + k] = gn;
+            }
+        }
+    }
+}
+
+hipError_t launch_hmc_accept(const AcceptArgs& a, int C, hipStream_t s) {
+    hipLaunchKernelGGL(k_hmc_accept, dim3(C), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// =============================================================================================
 // BNN: one wave per chain. Lanes are data rows; the flat weights live in LDS (broadcast reads);
 // parameter gradients are wave-reduced into LDS and gathered at the sampled indices.
 // =============================================================================================

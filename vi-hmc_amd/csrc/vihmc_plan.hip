@@ -1697,6 +1697,55 @@ int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, con
     });
 }
 
+int vihmc_hmc_accept(int C, int K, int n, int burn, const float* lp0, const float* lp1, const float* ke0,
+                     const float* ke1, const float* logu, const float* th1, const float* g1,
+                     float* th_last, float* lp_last, float* g_last, float* th_bp, float* lp_bp, float* g_bp,
+                     float* th_cur, float* lp_cur, float* g_cur, float* samples, int64_t s_cap, int64_t* counts,
+                     uint8_t* accepted, int64_t acc_ld, float* trace, int64_t tr_ld, float* rho, uint8_t* err,
+                     void* stream) {
+    return guarded([&]() -> int {
+        if (C < 1 || K < 1 || n < 0) return fail("vihmc_hmc_accept: C, K >= 1, n >= 0");
+        if (!lp0 || !lp1 || !ke0 || !ke1 || !logu || !th1 || !g1 || !th_last || !lp_last || !g_last || !accepted ||
+            !trace || !rho || !err)
+            return fail("null argument");
+        if (burn && (!th_bp || !lp_bp || !g_bp || !th_cur || !lp_cur || !g_cur))
+            return fail("vihmc_hmc_accept: burn-in needs the fallback and current-state buffers");
+        if (!burn && samples && (!counts || s_cap < 2)) return fail("vihmc_hmc_accept: samples need counts, s_cap >= 2");
+        if (n >= acc_ld || n >= tr_ld) return fail("vihmc_hmc_accept: n outside the accepted / trace rows");
+        AcceptArgs a{};
+        a.K = K;
+        a.n = n;
+        a.burn = burn ? 1 : 0;
+        a.lp0 = lp0;
+        a.lp1 = lp1;
+        a.ke0 = ke0;
+        a.ke1 = ke1;
+        a.logu = logu;
+        a.th1 = th1;
+        a.g1 = g1;
+        a.th_last = th_last;
+        a.lp_last = lp_last;
+        a.g_last = g_last;
+        a.th_bp = th_bp;
+        a.lp_bp = lp_bp;
+        a.g_bp = g_bp;
+        a.th_cur = th_cur;
+        a.lp_cur = lp_cur;
+        a.g_cur = g_cur;
+        a.samples = burn ? nullptr : samples;
+        a.s_cap = s_cap;
+        a.counts = counts;
+        a.accepted = accepted;
+        a.acc_ld = acc_ld;
+        a.trace = trace;
+        a.tr_ld = tr_ld;
+        a.rho = rho;
+        a.err = err;
+        HIPCHK(launch_hmc_accept(a, C, static_cast<hipStream_t>(stream)));
+        return 0;
+    });
+}
+
 int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* out, void* stream) {
     return guarded([&]() -> int {
         if (!p || !theta || !logp || !out) return fail("null argument");
@@ -2063,7 +2112,9 @@ const char* vihmc_version(void) {
                            std::to_string(vihmc::diag_switches_contract_bf()) + "," +
                            std::to_string(vihmc::diag_switches_bwd_bf()) + "," +
                            std::to_string(vihmc::diag_switches_layers()) + "," +
-                           std::to_string(vihmc::diag_switches_bwd_chain());
+                           std::to_string(vihmc::diag_switches_bwd_chain()) + "," +
+                           std::to_string(vihmc::diag_switches_gram()) + "," +
+                           std::to_string(vihmc::diag_switches_kernels());
     return v.c_str();
 }
 

@@ -298,6 +298,9 @@ class HMCRunner:
         self.counts = torch.ones(C, dtype=torch.long, device=device)
         self.accepted = torch.zeros(C, num_samples, dtype=torch.bool, device=device)
         self.trace = torch.empty(C, num_samples, device=device)
+        # the Metropolis step on the GPU in one launch (vihmc_hmc_accept) instead of ~30 small torch ops per
+        # iteration; the torch form below stays for CPU chains and strict_rng (whose accept draw needs ok first)
+        self._accept_native = device.type == "cuda" and not self.strict
         self._rows = torch.arange(C, device=device) * S_cap
         self.n = 0
 
@@ -370,6 +373,13 @@ class HMCRunner:
         logu = None if self.strict else rng.draw_logu()
         p = z if self.mass_sqrt is None else z * self.mass_sqrt
         th, lp, g = self.cur
+        if self._accept_native:
+            ke0 = _kinetic(p, self.inv_mass)
+            th_new, p, lp_new, g_new = self._trajectory(th, g, p, self._eps())
+            rho, err = self._accept_fused(n, lp, ke0, th_new, _kinetic(p, self.inv_mass), lp_new, g_new, logu)
+            self._adapt(n, rho, err)
+            self.n += 1
+            return
         H0 = -lp + _kinetic(p, self.inv_mass)
         th_new, p, lp_new, g_new = self._trajectory(th, g, p, self._eps())
         H1 = -lp_new + _kinetic(p, self.inv_mass)
@@ -400,8 +410,49 @@ class HMCRunner:
         self.cur = nxt
         self.accepted[:, n] = acc
         self.trace[:, n] = nxt[1]
+        self._adapt(n, torch.where(err, torch.full_like(rho, float("nan")), rho), err)
+        self.n += 1
+
+    def _accept_fused(self, n, lp, ke0, th_new, ke1, lp_new, g_new, logu):
+        """The accept block above for CUDA chains in one vihmc_hmc_accept launch (the same kinetic energies and
+        selection, bit for bit). After burn-in the last returned state is updated in place and is the current
+        state."""
+        import ctypes
+        from . import _lib
+        L = _lib.lib()
+        C, K = self.C, self.K
+        burn = n <= self.burn
+
+        def ptr(t):
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+        f32 = [lp, ke0, th_new, ke1, lp_new, g_new, logu]
+        lp, ke0, th_new, ke1, lp_new, g_new, logu = [t.to(torch.float32).contiguous() for t in f32]
+        rho = torch.empty(C, device=self.device)
+        err = torch.empty(C, dtype=torch.uint8, device=self.device)
+        last = self.last_ret
+        if burn:
+            cur = [torch.empty_like(t) for t in last]
+            bp = self.burn_prev
+        else:
+            cur = last
+            bp = [None, None, None]
+        samples = self.samples if (self.store and not burn) else None
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        _lib.check(L.vihmc_hmc_accept(C, K, n, 1 if burn else 0, ptr(lp), ptr(lp_new), ptr(ke0), ptr(ke1),
+                                      ptr(logu), ptr(th_new), ptr(g_new),
+                                      ptr(last[0]), ptr(last[1]), ptr(last[2]), ptr(bp[0]), ptr(bp[1]), ptr(bp[2]),
+                                      ptr(cur[0]) if burn else None, ptr(cur[1]) if burn else None,
+                                      ptr(cur[2]) if burn else None, ptr(samples), self.samples.shape[1],
+                                      ptr(self.counts), ptr(self.accepted), self.accepted.stride(0), ptr(self.trace),
+                                      self.trace.stride(0), ptr(rho), ptr(err), stream), "vihmc_hmc_accept")
+        self.cur = cur
+        return rho, err.bool()
+
+    def _adapt(self, n, rho, err):
+        """NUTS dual averaging of every chain's step size during burn-in (rho: NaN where the chain failed)."""
         if self.nuts and n <= self.burn:
-            rho_h = torch.where(err, torch.full_like(rho, float("nan")), rho).tolist()   # host sync (burn only)
+            rho_h = rho.tolist()                                   # host sync (burn only)
             err_h = err.tolist()
             for c in range(self.C):
                 if n < self.burn or err_h[c]:
@@ -409,7 +460,6 @@ class HMCRunner:
                         rho_h[c], n, self.step_size_init, self.H_t[c], self.eps_bar[c], self.desired_accept_rate)
                 if n == self.burn:
                     self.eps_host[c] = self.eps_bar[c]
-        self.n += 1
 
     def result(self) -> ChainResult:
         return ChainResult(self.samples, self.counts, self.accepted[:, :self.n], self.trace[:, :self.n],
