@@ -503,70 +503,112 @@ __global__ __launch_bounds__(256) void k_leap_open(const float* th_in, float* th
 // accept = ok && rho >= log u, and the state selection -- after burn-in the accepted proposal overwrites the last
 // returned state in place and (store) is written as the chain's next sample row (a failed chain's row goes to the
 // spare last row, not counted); during burn-in the current state is the proposal, else (failed) the last returned
-// state, else the burn-in fallback, which an accepted proposal replaces. One block per chain; replaces ~25 small
+// state, else the burn-in fallback, which an accepted proposal replaces. A [C, K] launch and a [C] launch replace ~25 small
 // elementwise launches.
 // =============================================================================================
+// the per-chain decision (every block of the chain recomputes it from the [C] inputs)
+struct AcceptDecision {
+    float rho;
+    bool ok, acc;
+};
+__device__ __forceinline__ AcceptDecision accept_decision(const AcceptArgs& a, int c) {
+#pragma clang fp contract(off)
+    const float lp0 = a.lp0[c], lp1 = a.lp1[c];
+    const float h0 = -lp0 + a.ke0[c], h1 = -lp1 + a.ke1[c];
+    const float d = h0 - h1;
+    AcceptDecision r;
+    r.rho = d != d ? 0.f : fminf(d, 0.f);
+    r.ok = isfinite(lp0) && isfinite(lp1);
+    r.acc = r.ok && r.rho >= a.logu[c];
+    return r;
+}
+
+// [C, K] part: grid (ceil(K / 1024), C), 4 elements per thread with every load issued before the first store (a
+// one-element loop waited out one load per trip: 116 us at 16 chains); reads counts[c] before k_hmc_accept_chain
+// advances it (stream order)
+constexpr int ACC_U = 4;
 __global__ __launch_bounds__(256) void k_hmc_accept(AcceptArgs a) {
-    const int c = blockIdx.x;
+    const int c = blockIdx.y;
     const int64_t o = (int64_t)c * a.K;
     __shared__ int flags[2];
     __shared__ int64_t row_s;
     if (threadIdx.x == 0) {
-#pragma clang fp contract(off)
-        const float lp0 = a.lp0[c], lp1 = a.lp1[c];
-        const float h0 = -lp0 + a.ke0[c], h1 = -lp1 + a.ke1[c];
-        const float d = h0 - h1;
-        const float rho = d != d ? 0.f : fminf(d, 0.f);
-        const bool ok = isfinite(lp0) && isfinite(lp1);
-        const bool acc = ok && rho >= a.logu[c];
-        flags[0] = acc ? 1 : 0;
-        flags[1] = ok ? 0 : 1;
-        a.rho[c] = ok ? rho : __builtin_nanf("");
-        a.err[c] = ok ? 0 : 1;
-        a.accepted[(int64_t)c * a.acc_ld + a.n] = acc ? 1 : 0;
-        float lp_next;
-        if (!a.burn) {
-            if (acc) a.lp_last[c] = lp1;
-            lp_next = acc ? lp1 : a.lp_last[c];
-            if (a.samples) {
-                row_s = ok ? a.counts[c] : a.s_cap - 1;
-                a.counts[c] += ok ? 1 : 0;
-            }
-        } else {
-            lp_next = acc ? lp1 : (ok ? a.lp_bp[c] : a.lp_last[c]);
-            a.lp_cur[c] = lp_next;
-            if (acc) a.lp_bp[c] = lp1;
-        }
-        a.trace[(int64_t)c * a.tr_ld + a.n] = lp_next;
+        const AcceptDecision r = accept_decision(a, c);
+        flags[0] = r.acc ? 1 : 0;
+        flags[1] = r.ok ? 0 : 1;
+        if (!a.burn && a.samples) row_s = r.ok ? a.counts[c] : a.s_cap - 1;
     }
     __syncthreads();
     const bool acc = flags[0] != 0, err = flags[1] != 0;
+    const int k0 = blockIdx.x * (ACC_U * 256) + threadIdx.x;
     if (!a.burn) {
         float* srow = a.samples ? a.samples + ((int64_t)c * a.s_cap + row_s) * a.K : nullptr;
-        for (int k = threadIdx.x; k < a.K; k += blockDim.x) {
-            float th = a.th_last[o + k];
+        float th[ACC_U], gn[ACC_U];
+#pragma unroll
+        for (int u = 0; u < ACC_U; ++u) {
+            const int k = min(k0 + 256 * u, a.K - 1);
+            th[u] = acc ? a.th1[o + k] : a.th_last[o + k];
+            gn[u] = acc ? a.g1[o + k] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < ACC_U; ++u) {
+            const int k = k0 + 256 * u;
+            if (k >= a.K) break;
             if (acc) {
-                th = a.th1[o + k];
-                a.th_last[o + k] = th;
-                a.g_last[o + k] = a.g1[o + k];
+                a.th_last[o + k] = th[u];
+                a.g_last[o + k] = gn[u];
             }
-            if (srow) srow[k] = th;
+            if (srow) srow[k] = th[u];
         }
     } else {
-        for (int k = threadIdx.x; k < a.K; k += blockDim.x) {
-            const float tn = a.th1[o + k], gn = a.g1[o + k];
-            a.th_cur[o + k] = acc ? tn : (err ? a.th_last[o + k] : a.th_bp[o + k]);
-            a.g_cur[o + k] = acc ? gn : (err ? a.g_last[o + k] : a.g_bp[o + k]);
+        float tn[ACC_U], gn[ACC_U], tf[ACC_U], gf[ACC_U];
+#pragma unroll
+        for (int u = 0; u < ACC_U; ++u) {
+            const int k = min(k0 + 256 * u, a.K - 1);
+            tn[u] = a.th1[o + k];
+            gn[u] = a.g1[o + k];
+            tf[u] = err ? a.th_last[o + k] : a.th_bp[o + k];
+            gf[u] = err ? a.g_last[o + k] : a.g_bp[o + k];
+        }
+#pragma unroll
+        for (int u = 0; u < ACC_U; ++u) {
+            const int k = k0 + 256 * u;
+            if (k >= a.K) break;
+            a.th_cur[o + k] = acc ? tn[u] : tf[u];
+            a.g_cur[o + k] = acc ? gn[u] : gf[u];
             if (acc) {
-                a.th_bp[o + k] = tn;
-                a.g_bp[o + k] = gn;
+                a.th_bp[o + k] = tn[u];
+                a.g_bp[o + k] = gn[u];
             }
         }
     }
 }
 
+// [C] part, after the [C, K] part: log-probs, counts, accepted, trace, rho, err
+__global__ __launch_bounds__(256) void k_hmc_accept_chain(AcceptArgs a, int C) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const AcceptDecision r = accept_decision(a, c);
+    const float lp1 = a.lp1[c];
+    a.rho[c] = r.ok ? r.rho : __builtin_nanf("");
+    a.err[c] = r.ok ? 0 : 1;
+    a.accepted[(int64_t)c * a.acc_ld + a.n] = r.acc ? 1 : 0;
+    float lp_next;
+    if (!a.burn) {
+        if (r.acc) a.lp_last[c] = lp1;
+        lp_next = r.acc ? lp1 : a.lp_last[c];
+        if (a.samples) a.counts[c] += r.ok ? 1 : 0;
+    } else {
+        lp_next = r.acc ? lp1 : (r.ok ? a.lp_bp[c] : a.lp_last[c]);
+        a.lp_cur[c] = lp_next;
+        if (r.acc) a.lp_bp[c] = lp1;
+    }
+    a.trace[(int64_t)c * a.tr_ld + a.n] = lp_next;
+}
+
 hipError_t launch_hmc_accept(const AcceptArgs& a, int C, hipStream_t s) {
-    hipLaunchKernelGGL(k_hmc_accept, dim3(C), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hmc_accept, dim3((a.K + ACC_U * 256 - 1) / (ACC_U * 256), C), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hmc_accept_chain, dim3((C + 255) / 256), dim3(256), 0, s, a, C);
     return hipGetLastError();
 }
 
