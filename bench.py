@@ -35,7 +35,9 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 240 HMC iterations at ~9 ms: a timed region of >= 2 s (MI355X_MICROARCH.md DVFS item 6: the clock under load
+    # settles over seconds; a 0.18-s region was shorter than the box spread it was meant to resolve)
+    ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--chains-per-gpu", type=int, default=16)
     ap.add_argument("--L", type=int, default=7)
@@ -435,7 +437,8 @@ def main():
     eng.option("timing_every", 1)
     grad_evals = ev.n_grad
     n_calls, n_gram = eng.get_option("grad_evals"), eng.get_option("gram_evals")
-    sclk = clock.mhz()
+    clk = clock.summary()
+    sclk = clk["mhz_by_xcd"]
     T = max_over_ranks(t1 - t0, dev)
 
     extra = {}
@@ -508,12 +511,22 @@ def main():
         "gram_eval_fraction": gram_frac,
         "gram_eval_fraction_basis": f"{n_gram} of {n_calls} gradient-evaluation calls in the timed region ran the "
                                     "Gram form (plan counters grad_evals / gram_evals)",
-        "sclk_mhz": float(np.mean(list(sclk.values()))) if sclk else None,
+        "timed_region_s": T,
+        "sclk_mhz": clk["mean_mhz"],
         "sclk_mhz_by_xcd": {str(k): round(v, 1) for k, v in sclk.items()},
-        "sclk_basis": "average shader clock over the timed region: d s_memtime / d s_memrealtime x 100 MHz per XCD "
-                      "(vihmc_clock_stamp before and after the region, MI355X_MICROARCH.md DVFS item 6); nominal 2400",
-        "roofline_frac_at_sclk": ((achieved / (peak * float(np.mean(list(sclk.values()))) / 2400.0))
-                                  if (achieved and sclk) else None),
+        "sclk_spread": clk["spread"],
+        "sclk_cus_per_xcd": {str(k): v for k, v in clk["cus_per_xcd"].items()},
+        "sclk_rejected_above_2400": clk["rejected_above_max"],
+        "sclk_basis": "average shader clock over the timed region per CU from that CU's own two stamps: d s_memtime / "
+                      "d s_memrealtime x 100 MHz (vihmc_clock_stamp before and after the region, 256 one-wave "
+                      "workgroups paired by XCD / CU; MI355X_MICROARCH.md DVFS item 6); per XCD the median over its "
+                      "CUs; readings above the 2,400-MHz maximum rejected and listed; spread = (max - min) / mean "
+                      "over the XCD medians",
+        "roofline_frac_at_sclk": ((achieved / (peak * clk["mean_mhz"] / 2400.0))
+                                  if (achieved and clk["mean_mhz"] and clk["spread"] is not None
+                                      and clk["spread"] <= 0.10) else None),
+        "roofline_frac_at_sclk_basis": "the roofline fraction against the peak scaled to the measured clock; reported "
+                                       "only when the per-XCD spread is <= 10 %",
         "accept_rate": acc_rate,
         "roofline": {"kernel": f"{kname}: {what}", "selected_as": "largest share of the evaluation's GPU time "
                      f"({cal[key]['share_of_eval']:.3f}, HIP-event calibration before the timed region)",

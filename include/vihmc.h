@@ -125,7 +125,8 @@ int vihmc_grad(vihmc_plan* p, const float* theta, int C, float* grad, void* stre
  * finite fails (hamiltorch's LogProbError: no accept), accept = rho >= logu[c]), batched as
  * vihmc.samplers.HMCRunner.step does it: after burn-in (burn = 0) an accepted proposal (th1, lp1, g1) overwrites
  * the last returned state in place and, when samples != NULL, the state is written to row counts[c] of
- * samples [C][s_cap][K] (a failed chain's row to row s_cap - 1, uncounted) and counts[c] advances; during burn-in
+ * samples [C][s_cap][K] (a failed chain's row to row s_cap - 1, uncounted) and counts[c] advances; rows 0 .. s_cap - 2
+ * hold samples: once counts[c] reaches s_cap - 1 further states go to the spare row uncounted; during burn-in
  * (burn = 1) th_cur / lp_cur / g_cur receive the proposal, else (failed) the last returned state, else the
  * fallback th_bp / lp_bp / g_bp, which an accepted proposal replaces. accepted[c * acc_ld + n], trace[c * tr_ld + n]
  * (the state's log-prob), rho [C] (NaN where failed) and err [C] are written. */
@@ -251,16 +252,17 @@ int vihmc_plan_check_canaries(vihmc_plan* p, int64_t* corrupted);
 int vihmc_plan_debug_copy(vihmc_plan* p, const char* name, void* dst, int64_t* bytes);
 
 /* Measurement (new; no reference counterpart): enqueue on `stream` one stamp of the shader clock. out is DEVICE
- * memory [64][3] uint64: per one-wave workgroup (8 per XCD) its XCD id, s_memtime (shader-clock ticks) and
- * s_memrealtime (100 MHz ticks). Two stamps around a timed region give each XCD's average shader clock over it:
- * (d memtime / d memrealtime) x 100 MHz (bench.py: "sclk_mhz"). */
+ * memory [256][4] uint64: per one-wave workgroup its XCD id, HW_ID register (CU / shader array / engine),
+ * s_memtime (shader-clock ticks) and s_memrealtime (100 MHz ticks). Two stamps around a timed region give each CU's
+ * average shader clock over it from that CU's own two readings: (d memtime / d memrealtime) x 100 MHz (bench.py:
+ * "sclk_mhz", medians per XCD). */
 int vihmc_clock_stamp(uint64_t* out, void* stream);
 
 void        vihmc_plan_destroy(vihmc_plan* p);
 const char* vihmc_last_error(void);
-/* "vihmc <ver> gfx950 diag=<fwd>,<contract_bf>,<bwd_bf>,<layers>,<bwd_chain>": the timing-only ablation / stamp switches the
- * library was built with (all 0 in a product build). Plan creation fails in a build with any of them on
- * unless VIHMC_ALLOW_DIAG=1 (A/B timing of variant builds only: results are wrong by design). */
+/* "vihmc <ver> gfx950 diag=<n>": the VIHMC_DIAG value (csrc/vihmc_diag.h: timing-only ablations and phase stamps) the
+ * library was built with (0 in a product build). Plan creation fails in a build with VIHMC_DIAG != 0 unless
+ * VIHMC_ALLOW_DIAG=1 (A/B timing of variant builds only: results are wrong by design). */
 const char* vihmc_version(void);
 
 #ifdef __cplusplus

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Two builds A/B on the bench's timed region (no side legs, no CPU baseline, no ESS phase) and its one-chain legs,
-# alternating A, B, A, B. A = diagbuild/$A.so, B = diagbuild/$B.so. Output: gpurun_out/${TAG}.txt
+# alternating A, B, A, B. A = _ab/$A.so, B = _ab/$B.so. Output: gpurun_out/${TAG}.txt
 TAG=${TAG:-r04bab}; A=${A:-base}; B=${B:-new}
 O=gpurun_out/${TAG}.txt
-D=${GRAFT_REPO_ROOT:-$(pwd)}/diagbuild
+D=${GRAFT_REPO_ROOT:-$(pwd)}/_ab
 : > $O
 for rep in 1 2; do
   for L in $A $B; do

@@ -1,7 +1,7 @@
-"""Phase stamps of the bf16x6 layer backward (k_bwd_bf) from a -DBB_STAMP=1 variant build.
+"""Phase stamps of the bf16x6 layer backward (k_bwd_bf) from a -DVIHMC_DIAG=0x20 variant build.
 
-    make -C vi-hmc_amd OUT=$PWD/_var/bbstamp.so BUILD=$PWD/build/bbstamp EXTRA=-DBB_STAMP=1
-    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/bbstamp.so python profiles/scripts/diag/stamps_bwd.py
+    make -C vi-hmc_amd OUT=$PWD/_ab/bbstamp.so BUILD=$PWD/build/bbstamp EXTRA=-DVIHMC_DIAG=0x20
+    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_ab/bbstamp.so python profiles/scripts/diag/stamps_bwd.py
 
 Every 16th trunk workgroup of the last launch with a dX part (layer 1) records per wave and 32-row sub-tile:
 s_memtime at the barrier exit, after staging the next sub-tile (split + LDS stores + the loads two ahead), and

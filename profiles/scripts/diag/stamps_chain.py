@@ -1,7 +1,7 @@
-"""Phase stamps of the whole-network backward (k_bwd_chain) from a -DCH_STAMP=1 variant build.
+"""Phase stamps of the whole-network backward (k_bwd_chain) from a -DVIHMC_DIAG=0x40 variant build.
 
-    make -C vi-hmc_amd OUT=$PWD/_var/chstamp.so BUILD=$PWD/build/chstamp EXTRA=-DCH_STAMP=1
-    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/chstamp.so python profiles/scripts/diag/stamps_chain.py
+    make -C vi-hmc_amd OUT=$PWD/_ab/chstamp.so BUILD=$PWD/build/chstamp EXTRA=-DVIHMC_DIAG=0x40
+    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_ab/chstamp.so python profiles/scripts/diag/stamps_chain.py
 
 Every 8th workgroup of a single-chain Burgers evaluation records per wave and layer s_memtime after barrier A,
 after A2, when its compute phase is done, after barrier B and when its write phase is done; printed per layer as

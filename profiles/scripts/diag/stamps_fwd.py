@@ -1,7 +1,7 @@
-"""Phase stamps of the bf16x6 fused forward (k_fwd_fused_bf) from a -DFWD_STAMP=1 variant build.
+"""Phase stamps of the bf16x6 fused forward (k_fwd_fused_bf) from a -DVIHMC_DIAG=0x10 variant build.
 
-    make -C vi-hmc_amd OUT=$PWD/diagbuild/fwstamp.so BUILD=$PWD/build/fwstamp EXTRA=-DFWD_STAMP=1
-    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/diagbuild/fwstamp.so python profiles/scripts/diag/stamps_fwd.py --chains 1
+    make -C vi-hmc_amd OUT=$PWD/_ab/fwstamp.so BUILD=$PWD/build/fwstamp EXTRA=-DVIHMC_DIAG=0x10
+    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_ab/fwstamp.so python profiles/scripts/diag/stamps_fwd.py --chains 1
 
 Every 8th workgroup (the first 16) of the last forward records per wave and layer: s_memtime after the layer's
 barrier [0], after the operand split (compute waves) / the next image's DMA issue (DMA waves) [1], after the layer's

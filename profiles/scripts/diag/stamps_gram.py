@@ -1,7 +1,7 @@
-"""Phase stamps of k_gram_a's T_b units from a -DGR_STAMP=1 variant build.
+"""Phase stamps of k_gram_a's T_b units from a -DVIHMC_DIAG=0x200 variant build.
 
-    make -C vi-hmc_amd OUT=$PWD/diagbuild/grstamp.so BUILD=$PWD/build/grstamp EXTRA=-DGR_STAMP=1
-    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/diagbuild/grstamp.so python profiles/scripts/diag/stamps_gram.py --chains 16
+    make -C vi-hmc_amd OUT=$PWD/_ab/grstamp.so BUILD=$PWD/build/grstamp EXTRA=-DVIHMC_DIAG=0x200
+    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_ab/grstamp.so python profiles/scripts/diag/stamps_gram.py --chains 16
 
 Every 16th T_b unit of the last k_gram_a launch records per wave (0-7 compute, 8 the DMA wave) and k block:
 s_memtime at the barrier exit [0], after issuing the next block's loads (compute: A rows; DMA wave: the block two

@@ -1,7 +1,7 @@
-"""Phase stamps of the side-A contraction (k_contract_bf) from a -DCB_STAMP=1 variant build.
+"""Phase stamps of the side-A contraction (k_contract_bf) from a -DVIHMC_DIAG=0x80 variant build.
 
-    make -C vi-hmc_amd OUT=$PWD/_var/stamp.so BUILD=$PWD/build/stamp EXTRA=-DCB_STAMP=1
-    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_var/stamp.so python profiles/scripts/diag/stamps_side_a.py
+    make -C vi-hmc_amd OUT=$PWD/_ab/stamp.so BUILD=$PWD/build/stamp EXTRA=-DVIHMC_DIAG=0x80
+    VIHMC_ALLOW_DIAG=1 VIHMC_LIB=$PWD/_ab/stamp.so python profiles/scripts/diag/stamps_side_a.py
 
 Every 64th workgroup records, per wave and chunk, s_memtime at the barrier exit and when the chunk's
 results exist (S role: G and the likelihood partial; D role: the dZ_t accumulators), plus s_memtime /

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Forward W-fragment prefetch A/B (round 4): bitwise dumps of the product build vs FWD_PIPE=0 (diagbuild/base.so)
-# and the 8-wave variant (diagbuild/fw8.so), forward stamps at one chain, gradient-only class timings at 16 chains,
+# Forward W-fragment prefetch A/B (round 4): bitwise dumps of the product build vs FWD_PIPE=0 (_ab/base.so)
+# and the 8-wave variant (_ab/fw8.so), forward stamps at one chain, gradient-only class timings at 16 chains,
 # and the one-chain crossover. Output: gpurun_out/${TAG}.txt
 TAG=${TAG:-r04zf}
 O=gpurun_out/${TAG}.txt
-D=${GRAFT_REPO_ROOT:-$(pwd)}/diagbuild
+D=${GRAFT_REPO_ROOT:-$(pwd)}/_ab
 VIHMC_LIB=$D/base.so timeout -k 10 100 python -u profiles/scripts/diag/dump_eval.py gpurun_out/dump_base.npz > $O 2>&1 || exit 1
 timeout -k 10 100 python -u profiles/scripts/diag/dump_eval.py gpurun_out/dump_new.npz >> $O 2>&1 || exit 1
 python profiles/scripts/diag/dump_eval.py --compare gpurun_out/dump_base.npz gpurun_out/dump_new.npz >> $O 2>&1

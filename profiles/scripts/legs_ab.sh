@@ -1,9 +1,9 @@
 #!/bin/bash
 # Two builds A/B on the one-chain legs (round 4): bitwise dumps (dump_eval.py), the bench's one-chain legs
-# (probe_legs.py) and the 16-chain class timings, alternating A, B, A, B. A = diagbuild/$A.so, B = diagbuild/$B.so.
+# (probe_legs.py) and the 16-chain class timings, alternating A, B, A, B. A = _ab/$A.so, B = _ab/$B.so.
 TAG=${TAG:-r04legs}; A=${A:-base}; B=${B:-lat}
 O=gpurun_out/${TAG}.txt
-D=${GRAFT_REPO_ROOT:-$(pwd)}/diagbuild
+D=${GRAFT_REPO_ROOT:-$(pwd)}/_ab
 : > $O
 for L in $A $B; do
   VIHMC_LIB=$D/$L.so timeout -k 10 100 python -u profiles/scripts/diag/dump_eval.py gpurun_out/dump_$L.npz >> $O 2>&1 || exit 1

@@ -1,10 +1,10 @@
 #!/bin/bash
 # Two builds A/B (round 4): bitwise dumps (dump_eval.py), gradient-only and full-evaluation class timings at 16
-# chains, the one-chain crossover, alternating A, B, A, B. A = diagbuild/$A.so, B = diagbuild/$B.so.
+# chains, the one-chain crossover, alternating A, B, A, B. A = _ab/$A.so, B = _ab/$B.so.
 # Output: gpurun_out/${TAG}.txt
 TAG=${TAG:-r04ab}; A=${A:-base}; B=${B:-noslp}
 O=gpurun_out/${TAG}.txt
-D=${GRAFT_REPO_ROOT:-$(pwd)}/diagbuild
+D=${GRAFT_REPO_ROOT:-$(pwd)}/_ab
 : > $O
 for L in $A $B; do
   VIHMC_LIB=$D/$L.so timeout -k 10 100 python -u profiles/scripts/diag/dump_eval.py gpurun_out/dump_$L.npz >> $O 2>&1 || exit 1

@@ -59,4 +59,4 @@ def test_shipped_library_has_no_diagnostic_switches():
     """Timing-only ablations (FWD_ABL, CB_ABL, BB_ABL) and stamp instrumentation are never in the product
     build: the version string reports them and vihmc._lib refuses such a library."""
     from vihmc import _lib
-    assert re.search(r"diag=0(,0)*(\s|$)", _lib.lib().vihmc_version().decode())
+    assert re.search(r"diag=0(\s|$)", _lib.lib().vihmc_version().decode())

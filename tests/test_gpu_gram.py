@@ -250,51 +250,73 @@ def test_gram_loss_forms_vs_fp64_oracle(loss, tau, cuda_device):
 FIT_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gpurun_out", "gram_fit_table.json")
 
 
+FIT_REALIZATIONS = 3
+
+
 @pytest.mark.parametrize("noise", [1e-2, 1e-3, 1e-4, 1e-5, 1e-6])
 def test_gram_precision_vs_fit(noise, cuda_device):
     """The Gram form's cancellation (Zb^ Gt vs y Zt^) grows with |y| / |S - y|: full Burgers shape, theta AT the
     teacher with the frozen weights at the teacher too (mu_noise = 0), so the residual is the data noise alone
     (sum r^2 / sum y^2 ~ noise^2 / E y^2). A flat prior (sd 1e3) leaves the likelihood gradient, whose error the
-    cancellation affects. Both forms against the fp64 oracle; the table of error vs fit goes to
-    gpurun_out/gram_fit_table.json (profiles/r04_gram_fit_table.json)."""
+    cancellation affects. Three thetas per fit (the teacher and two copies moved by 1e-6 relative: one fit, three
+    independent rounding realisations -- a single gradient's fp32 error is a random draw, dominated by the mean of S
+    through d/db0), each against the fp64 oracle: the engine's Gram form, its residual form, and the reference's own
+    fp32 closure (TorchDeepONetRef: the reference's torch ops on the CPU, the yardstick of VERDICT r4 item 6). Table
+    -> gpurun_out/gram_fit_table.json (profiles/r05_gram_fit_table.json)."""
+    from oracle.deeponet_ref import TorchDeepONetRef
     from vihmc.data import deeponet_problem
     from vihmc.engine import DeepONetEngine, trunk_features
     from vihmc.layout import DeepONetSpec
     spec = DeepONetSpec()
     sd = 1e3
     p = deeponet_problem(seed=3, noise=noise, mu_noise=0.0)
-    th = p.teacher[p.grad_ind].astype(np.float32)
+    t0 = p.teacher[p.grad_ind].astype(np.float32)
+    rng = np.random.default_rng(31)
+    ths = [t0] + [(t0 * (1 + 1e-6 * rng.standard_normal(t0.size))).astype(np.float32)
+                  for _ in range(FIT_REALIZATIONS - 1)]
+    R = len(ths)
     eng = DeepONetEngine(spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, sd, "NLL", 1.0,
-                         max_chains=2, device=cuda_device)
-    eng.option("gram_min_chains", 2)
+                         max_chains=R, device=cuda_device)
+    eng.option("gram_min_chains", 1)
     k_default = eng.get_option("gram_guard")
     eng.option("gram_guard", 0)                      # measure the Gram form itself at every fit
-    tt = torch.tensor(np.stack([th, th]), device=cuda_device)
-    gg = eng.grad(tt)[0].cpu().numpy()
+    tt = torch.tensor(np.stack(ths), device=cuda_device)
+    gg = eng.grad(tt).cpu().numpy()
     assert eng.get_option("gram") & 2
     lp, gres = eng.logp_grad(tt)
-    gres = gres[0].cpu().numpy()
+    gres = gres.cpu().numpy()
     lay = deeponet_layout(spec.in_branch, spec.width_branch, spec.depth_branch, spec.in_trunk, spec.width_trunk,
                           spec.depth_trunk, spec.out)
-    rl, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, 0.0, sd, "NLL", 1.0)
-    # fit ratio from the log-likelihood: ll = -0.5 sum r^2 (v = 1: the log v term is 0); prior part removed
-    prior = float(np.sum(-0.5 * (th.astype(np.float64) / sd) ** 2 - np.log(sd) - 0.5 * np.log(2 * np.pi)))
-    ssr = -2.0 * (rl - prior)
-    fit = ssr / float(np.sum(p.y.astype(np.float64) ** 2))
-    e_gram, e_res = rel_norm(gg, rg), rel_norm(gres, rg)
-    row = {"noise": noise, "fit_ratio": fit, "grad_norm": float(np.linalg.norm(rg)), "gram_relnorm": e_gram,
-           "residual_relnorm": e_res, "gram_elem": float(np.abs(gg - rg).max() / np.abs(rg).max()),
-           "residual_elem": float(np.abs(gres - rg).max() / np.abs(rg).max())}
+    ref32 = TorchDeepONetRef(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, 0.0, sd, "NLL", 1.0)
+    # a second fp32 yardstick: the same closure with a correctly rounded tanh (fp64 tanh rounded to fp32) -- what an
+    # ideal fp32 implementation of the reference's ops gives; one rounding realisation differs from another by ~3x
+    ref32cr = TorchDeepONetRef(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, 0.0, sd, "NLL", 1.0)
+    ref32cr.act = lambda z: torch.tanh(z.double()).float()
+    cols = {"gram": [], "residual": [], "ref_fp32": [], "ref_fp32_cr_tanh": []}
+    fit = None
+    for i, th in enumerate(ths):
+        rl, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, 0.0, sd, "NLL", 1.0)
+        _, g32 = ref32.logp_grad(th)
+        cols["gram"].append(rel_norm(gg[i], rg))
+        cols["residual"].append(rel_norm(gres[i], rg))
+        cols["ref_fp32"].append(rel_norm(g32, rg))
+        cols["ref_fp32_cr_tanh"].append(rel_norm(ref32cr.logp_grad(th)[1], rg))
+        if i == 0:
+            # fit ratio from the log-likelihood: ll = -0.5 sum r^2 (v = 1: the log v term is 0); prior part removed
+            prior = float(np.sum(-0.5 * (th.astype(np.float64) / sd) ** 2 - np.log(sd) - 0.5 * np.log(2 * np.pi)))
+            fit = -2.0 * (rl - prior) / float(np.sum(p.y.astype(np.float64) ** 2))
+    med = {k: float(np.median(v)) for k, v in cols.items()}
+    row = {"noise": noise, "fit_ratio": fit, "realizations": R,
+           **{f"{k}_relnorm": v for k, v in cols.items()}, **{f"{k}_median": v for k, v in med.items()},
+           "gram_over_ref_fp32": med["gram"] / med["ref_fp32"],
+           "residual_over_ref_fp32": med["residual"] / med["ref_fp32"]}
     print(json.dumps(row))
     os.makedirs(os.path.dirname(FIT_TABLE), exist_ok=True)
     rows = json.load(open(FIT_TABLE)) if os.path.exists(FIT_TABLE) else []
     rows = [r for r in rows if r["noise"] != noise] + [row]
     json.dump(sorted(rows, key=lambda r: -r["noise"]), open(FIT_TABLE, "w"), indent=1)
-    # Both forms lose precision on the likelihood gradient at the same rate as the fit improves (the fp32 rounding of
-    # S - y or of the Gram terms, relative to a gradient that shrinks with the residual): measured gram / residual
-    # 1.65-1.7 from fit 0.13 down to 1.5e-9 (profiles/r04_gram_fit_table.json), so the Gram form is never more than
-    # ~2x the reference's own fp32 arithmetic. Bound: 2.5x at every fit, above and below the guard threshold.
-    assert e_gram <= 2.5 * e_res + 1e-7, row
+    # the Gram form within 2.5x the residual form's error at every fit (the cancellation alone)
+    assert med["gram"] <= 2.5 * med["residual"] + 1e-7, row
     assert k_default > 0
 
 

@@ -46,13 +46,16 @@ def _engine(c, C, dev):
                           c.prior_sd, c.loss, c.tau_out, max_chains=C, device=dev)
 
 
-def _trajectory_parity(res, ref_fn, th0, seeds, S, L, eps, burn=0):
-    """Compare chain c of the batched GPU run with the scalar reference sampler on seed[c]. Returns the
+def _trajectory_parity(res, ref_fn, th0, seeds, S, L, eps, burn=0, chains=None):
+    """Compare chain chains[i] (default i) of the batched GPU run with the scalar reference sampler on seeds[i],
+    started from th0 (one [K] start for every chain, or [C, K] with a start per chain of the run). Returns the
     aligned (gpu, ref) sample lists up to the first permitted divergence, and the smallest margin."""
     aligned = []
     min_margin = np.inf
-    for c, s in enumerate(seeds):
-        out, st = HR.sample(ref_fn, th0, S, L, eps, burn=burn, generator=torch.Generator().manual_seed(s),
+    chains = list(range(len(seeds))) if chains is None else list(chains)
+    for c, s in zip(chains, seeds):
+        start = th0 if th0.dim() == 1 else th0[c]
+        out, st = HR.sample(ref_fn, start.cpu(), S, L, eps, burn=burn, generator=torch.Generator().manual_seed(s),
                             return_stats=True)
         acc = res.accepted[c].cpu().tolist()
         margins = np.abs(np.asarray(st["rhos"]) - np.asarray(st["logus"]))

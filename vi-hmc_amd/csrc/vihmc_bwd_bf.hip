@@ -69,9 +69,6 @@ __device__ __forceinline__ float tanh_grad(float h) {
 }
 }  // namespace
 
-#ifndef BB_STAMP
-#define BB_STAMP 0        // timing-only instrumentation (variant builds): in-kernel phase stamps
-#endif
 #if BB_STAMP
 // every 16th trunk workgroup of the launches with a dX part (the last one written wins: layer 1): per wave and
 // sub-tile s_memtime at the barrier exit [0], after the staging of the next sub-tile [1], when the MFMA results
@@ -245,13 +242,25 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         // offset instead of a branch around the store
         const __amdgpu_buffer_rsrc_t drs =
             bf6::make_rsrc(P.Dout + c * P.o_cs, (uint32_t)((int64_t)P.M * P.ldh * 4));
-        // h-row staging (the staging waves move the deltas): item e = tid + 512 v of the sub-tile's 32 x hq4 float4,
-        // wrapped like the staging role's; sub-tile s is loaded into set s & 1 two sub-tiles before its store
+        // h-row staging (the staging waves move the deltas); sub-tile s is loaded into set s & 1 two sub-tiles before
+        // its store. Layers with a dX part (n_in = 100): lane (lr, lg) stages exactly the float4 its own epilogue
+        // multiplies -- row 16 h + lr, columns 16 (t0 + v) + 4 lg, clamped to float4 24 (columns 96..99: a duplicate of
+        // lane lg = 0's item, never the constant-1 db column 100) -- so act'(h) comes from the fp32 rows at staging
+        // time and waits in registers for the epilogue instead of being rebuilt from the three LDS planes per element
+        // (5 VALU and 3 LDS reads per element less; the same h, so bitwise the same deltas). Other layers: item
+        // e = tid + 512 v of the sub-tile's 32 x hq4 float4, wrapped like the staging role's.
         uint32_t hvoff[B2_HSLOTS], hloff[B2_HSLOTS];
 #pragma unroll
         for (int v = 0; v < B2_HSLOTS; ++v) {
-            const int e = (tid + 512 * v) % (BB_SUB * hq4);
-            const int r = e / hq4, c4 = e - r * hq4;
+            int r, c4;
+            if (P.has_dx) {
+                r = 16 * h + lr;
+                c4 = min(4 * (t0 + v) + lg, 24);
+            } else {
+                const int e = (tid + 512 * v) % (BB_SUB * hq4);
+                r = e / hq4;
+                c4 = e - r * hq4;
+            }
             hvoff[v] = (uint32_t)(r * P.ldh + 4 * c4) * 4u;
             hloff[v] = (uint32_t)(BB_HP + r * BB_PITCH + 8 * c4);
         }
@@ -279,10 +288,20 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             constexpr bool TANH = decltype(tanh_c)::value;
             constexpr int NU = TWO ? 2 : 1;
             f32x4 hsa[B2_HSLOTS], hsb[B2_HSLOTS];       // per instantiation: no register set live across the dispatch
+            f32x4 ag[NU];                              // act'(h) of the staged sub-tile (dX layers), epilogue operand
+            auto hstage = [&](int buf, const f32x4 (&hs)[B2_HSLOTS]) __attribute__((always_inline)) {
+                hstore(buf, hs);
+                if (P.has_dx) {
+#pragma unroll
+                    for (int u = 0; u < NU; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) ag[u][r] = TANH ? tanh_grad(hs[u][r]) : act_grad_bf(P.act, hs[u][r]);
+                }
+            };
             if (nsub > 0) {
                 hload(hsub_at(0), hsa);
                 hload(hsub_at(1), hsb);
-                hstore(0, hsa);
+                hstage(0, hsa);
                 hload(hsub_at(2), hsa);
             }
             bf16x8 wra[3][3];                          // [kb][plane] W^T fragments of the first i-tile (registers)
@@ -325,20 +344,13 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 VIHMC_BB_STAMP(i, 1)
 #endif
                 const int m = sub + 16 * h + lr;
-                const unsigned char* hrow = buf + BB_HP + (16 * h + lr) * BB_PITCH;
 #pragma unroll
                 for (int u = 0; u < NU; ++u) {
                     const int col = 16 * (t0 + u) + 4 * lg;
-                    bf16x4 hq[3];
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) hq[p] = *reinterpret_cast<const bf16x4*>(hrow + p * BB_PLANE + 2 * col);
                     const uint32_t off = (m < r1 && col < NI4) ? (uint32_t)(m * P.ldh + col) * 4u : bf6::OOB;
                     f32x4 o;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float hv = ((float)hq[2][r] + (float)hq[1][r]) + (float)hq[0][r];
-                        o[r] = acc[u][r] * (TANH ? tanh_grad(hv) : act_grad_bf(P.act, hv));
-                    }
+                    for (int r = 0; r < 4; ++r) o[r] = acc[u][r] * ag[u][r];
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bf6::u32x4, o), drs, off, 0, 0);
                 }
             };
@@ -348,13 +360,13 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 __syncthreads();                       // buffer 0 holds sub-tile i
                 VIHMC_BB_STAMP(i, 0)
                 dx_sub(i);
-                hstore(1, hsb);                        // h of sub-tile i + 1 into the free buffer
+                hstage(1, hsb);                        // h of sub-tile i + 1 into the free buffer (+ its act')
                 hload(hsub_at(i + 3), hsb);
                 VIHMC_BB_STAMP(i, 2)
                 __syncthreads();                       // buffer 1 holds sub-tile i + 1
                 VIHMC_BB_STAMP(i + 1, 0)
                 dx_sub(i + 1);
-                if (i + 2 < nsub) hstore(0, hsa);
+                if (i + 2 < nsub) hstage(0, hsa);
                 hload(hsub_at(i + 4), hsa);
                 VIHMC_BB_STAMP(i + 1, 2)
             }
@@ -474,7 +486,5 @@ hipError_t launch_bwd_bf(const BwdArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// timing-only / instrumentation switches this translation unit was built with (0 = product build)
-int diag_switches_bwd_bf() { return BB_STAMP << 8; }
 
 }  // namespace vihmc

@@ -58,12 +58,6 @@ __device__ __forceinline__ float act_grad(int act, float h) {
 }
 }  // namespace
 
-#ifndef CH_STAMP
-#define CH_STAMP 0        // timing-only instrumentation (variant builds): in-kernel phase stamps
-#endif
-#ifndef CH_ABL
-#define CH_ABL 0          // timing-only ablation (wrong results): 1 = no dW MFMAs, 2 = no dX bf16 MFMAs
-#endif
 #if CH_STAMP
 // every 8th workgroup (the first 16 of them): per wave and layer, s_memtime after barrier A [0], when the compute
 // phase is done [2], after barrier B [3], when the write phase is done [4] ([1] = [0]); per workgroup s_memtime /
@@ -466,7 +460,5 @@ hipError_t launch_bwd_chain(const BwdChainArgs& a, hipStream_t s) {
 
 int bwd_chain_rows() { return CH_ROWS; }
 
-// timing-only / instrumentation switches this translation unit was built with (0 = product build)
-int diag_switches_bwd_chain() { return (CH_STAMP << 8) | CH_ABL; }
 
 }  // namespace vihmc

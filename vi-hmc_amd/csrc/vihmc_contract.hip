@@ -15,9 +15,6 @@
 // 4 apart (lane groups 0/1 and 2/3 of each half-wave) are 16 banks apart.
 #include "vihmc_internal.h"
 
-#ifndef VIHMC_CONTRACT_WS
-#define VIHMC_CONTRACT_WS 1
-#endif
 
 namespace vihmc {
 

@@ -65,9 +65,6 @@ constexpr int CB_GLDS = CB_BLOCK / 1024;           // 22 wave-wide 16-B-per-lane
 
 }  // namespace
 
-#ifndef CB_STAMP
-#define CB_STAMP 0      // timing-only instrumentation (variant builds): in-kernel phase stamps, see below
-#endif
 #if CB_STAMP
 // every 64th workgroup: per wave and chunk, s_memtime at the barrier exit [0] and when the chunk's results
 // exist [1]; per workgroup s_memtime / s_memrealtime (100 MHz) at start and end (scripts/diag/stamps_side_a.py)
@@ -534,7 +531,5 @@ hipError_t launch_contract_bf(const ContractProb& p, int C, hipStream_t s) {
     return hipGetLastError();
 }
 
-// timing-only / instrumentation switches this translation unit was built with (0 = product build)
-int diag_switches_contract_bf() { return CB_STAMP << 8; }
 
 }  // namespace vihmc

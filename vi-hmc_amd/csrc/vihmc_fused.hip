@@ -34,32 +34,8 @@ __device__ __forceinline__ f32x4 mfma_f(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-#ifndef FWD_ABL
-#define FWD_ABL 0     // timing-only ablation (wrong results): 1 = no h stores in the bf16x6 forward, 2 = tanh -> identity,
-                      // 4 = the DMA waves issue no weight-image copies, 8 = no bf16 MFMAs in the layer body
-#endif
-#ifndef FWD_TANH_CHEAP
-#define FWD_TANH_CHEAP 1   // 0: odd Taylor series below 0.25, exp-rcp above (<= 4 ulp, ~17 VALU)
-#endif
 
-__device__ __forceinline__ float tanh_f(float x) {
-    if (FWD_TANH_CHEAP) {
-        // (1 - t) / (1 + t), t = exp(-2|x|): 6 VALU + 2 transcendental, absolute error <= ~1.2e-7 (relative
-        // accuracy is lost only where |tanh x| is itself below ~1e-3)
-        const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(x));
-        return copysignf((1.f - t) * __builtin_amdgcn_rcpf(1.f + t), x);
-    }
-    const float ax = fabsf(x);
-    const float x2 = x * x;
-    float p = fmaf(x2, -0.0088632355f, 0.0218694885f);
-    p = fmaf(x2, p, -0.0539682540f);
-    p = fmaf(x2, p, 0.1333333333f);
-    p = fmaf(x2, p, -0.3333333333f);
-    const float small = fmaf(x * x2, p, x);
-    const float e = __expf(2.f * ax);
-    const float big = copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f), x);
-    return ax < 0.25f ? small : big;
-}
+__device__ __forceinline__ float tanh_f(float x) { return tanh_acc(x); }
 
 template <int ACT>
 __device__ __forceinline__ float act_t(float z) {
@@ -367,15 +343,6 @@ __device__ __forceinline__ void bf_split_operand(const float4 (&h)[7], bf16x8 (&
 // B[k = lg][m = lr] = h[m][96 + lg] must sit in lane (lr, lg): tile 6's A rows are W rows 96 + (lr >> 2)
 // (rows 4g .. 4g+3 all W row 96 + g), so accumulator register 0 of lane (lr, lg) is exactly h[lr][96 + lg] --
 // no cross-lane move. The image carries the fp32 tail W[n][96..99] ([100][4] after the bias).
-#ifndef FWD_TAILF32
-#define FWD_TAILF32 1
-#endif
-#ifndef FWD_BF_NW
-#define FWD_BF_NW 12       // waves per workgroup of the bf16x6 forward (16 rows each): 12 = 3 per SIMD at 168 VGPRs
-#endif
-#ifndef FWD_DMA_ONLY
-#define FWD_DMA_ONLY 0     // timing builds: the register-staging path compiled out with FWD_TAILF32 = 0 too
-#endif
 constexpr int FWD_WTAIL = 3 * BPLANE * 2 + 112 * 4;   // byte offset of the fp32 W tail [100][4] in an image
 constexpr int QI_PITCH = 224;                           // contraction block image (vihmc_contract_bf.hip): plane
 constexpr int QI_PLANE = CONTRACT_SPLIT_ROWS * QI_PITCH;  // rows of 112 bf16, 3 planes, then the fp32 tail [32][4]
@@ -431,12 +398,9 @@ __device__ __forceinline__ void tf_layer(const __bf16* wb, const float* bias, co
     hn[6].x = v;
 }
 
-#ifndef FWD_STAMP
-#define FWD_STAMP 0   // timing-only instrumentation (variant builds): per-layer phase stamps of k_fwd_fused_bf
-#endif
 // ---- input layer in the forward launch (FusedNet::x): network layer 0 of the wave's 16 rows on the f32 MFMA, every
 // tile's products in k_rowdot_in's order (16-long k blocks .x .y .z .w, then the 4-wide tail steps) and its epilogue
-// (tanh_f = the row-dot epilogue's tanh_cheap; columns >= 100 zero), so h_0 is bitwise the separate launch's. Saves
+// (tanh_f = the row-dot epilogue's tanh_acc; columns >= 100 zero), so h_0 is bitwise the separate launch's. Saves
 // that launch and the re-read of h_0: the lanes' accumulators are the layer walk's operand layout already (tile 6
 // moved into its f32-tail form by four shuffles).
 constexpr int IN0_KMAX = 111;                       // 6 full 16-long k blocks + <= 4 tail steps
@@ -886,7 +850,7 @@ bool fwd_fused_bf_needs_wimg() { return FWD_TAILF32 != 0; }
 // pre-split-image form: FWD_TAILF32; W0 staged in one image buffer; its tanh the row-dot epilogue's)
 bool fwd_fused_in0_ok(int n_in, int ldx, int ldw) {
     const int k4 = (n_in + 3) & ~3;
-    return FWD_TAILF32 && FWD_TANH_CHEAP && FWD_ABL == 0 && n_in >= 1 && n_in <= IN0_KMAX && ldx >= k4 &&
+    return FWD_TAILF32 && FWD_ABL == 0 && n_in >= 1 && n_in <= IN0_KMAX && ldx >= k4 &&
            (n_in < 16 || (ldx & 3) == 0) && ldw >= k4 && (ldw & 3) == 0 &&
            (size_t)FW * in0_ldw(k4) * sizeof(float) <= (size_t)FWD_WIMG;
 }
@@ -923,7 +887,5 @@ hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s) {
     return hipGetLastError();
 }
 
-// timing-only / instrumentation switches this translation unit was built with (0 = product build)
-int diag_switches_fused() { return FWD_ABL | (FWD_STAMP << 8); }
 
 }  // namespace vihmc

@@ -5,9 +5,31 @@
 #include <cstdint>
 #include <vector>
 
+#include "vihmc_diag.h"
+
 namespace vihmc {
 
 enum { ACT_ID = 0, ACT_TANH = 1, ACT_RELU = 2, ACT_SINE = 3 };
+
+// tanh of the DeepONet layer epilogues (fused forward, row-dot input layers): <= 0.9 ulp below |x| = 0.625, ~1-2 ulp
+// above (v_exp_f32 / v_rcp_f32), and UNBIASED -- the contraction sums 10^4-10^7 products of these outputs, so a
+// systematic error adds up where a random one averages out. Until round 5 the epilogues used (1 - t) / (1 + t),
+// t = exp(-2|x|): absolute error ~6e-8 near 0 (2e4 ulp at |x| ~ 1e-3) and a -0.08-ulp bias from log2(e) rounded to
+// fp32; at a good fit the likelihood gradient came out ~50x the reference's own fp32 error.
+//   |x| < 0.625: x + x^3 P(x^2), P of degree 4 fitted to tanh with each fp32 coefficient chosen for zero mean error
+//   else:        1 - 2 t / (1 + t), t = 2^(-2 log2(e) |x|) <= 0.287, log2(e) as two fp32 parts in one fma
+__device__ __forceinline__ float tanh_acc(float x) {
+    const float ax = fabsf(x);
+    const float u = x * x;
+    float p = fmaf(u, -0.005816340912133455f, 0.020738132297992706f);
+    p = fmaf(u, p, -0.053769949823617935f);
+    p = fmaf(u, p, 0.13331805169582367f);
+    p = fmaf(u, p, -0.33333295583724976f);
+    const float small = fmaf(x * u, p, x);
+    const float t = __builtin_amdgcn_exp2f(fmaf(ax, -2.885390043258667f, ax * -3.851926067000022e-08f));
+    const float big = copysignf(fmaf(-2.f, t * __builtin_amdgcn_rcpf(1.f + t), 1.f), x);
+    return ax < 0.625f ? small : big;
+}
 enum { MODE_FWD = 0, MODE_BWD = 1 };
 
 // contraction geometry (vihmc_contract.hip): 4 waves x 32 owner rows per workgroup, 16-row Q chunks
@@ -246,7 +268,7 @@ struct StatsJob {
 };
 hipError_t launch_reduce(const ReduceJob* jobs_dev, int n_jobs, int max_len, int C, hipStream_t s,
                          const StatsJob* stats = nullptr, const ChainBits* only = nullptr);
-constexpr int CLOCK_STAMP_WG = 64;     // k_clock_stamp workgroups; 3 uint64 each
+constexpr int CLOCK_STAMP_WG = 256;    // k_clock_stamp workgroups; 4 uint64 each
 hipError_t launch_clock_stamp(unsigned long long* out, hipStream_t s);
 hipError_t launch_contract_stats(const StatsJob& J, int C, hipStream_t s);
 // sum of y^2 over n elements (fixed order, fp64): `parts` partial sums into part[], then *out (the fit guard's scale)
@@ -349,16 +371,8 @@ int fwd_img_tail_off(int n, int col);
 bool fwd_fused_bf_needs_wimg();                     // the bf16x6 forward reads the fp32 k tail of the image
 bool fwd_fused_in0_ok(int n_in, int ldx, int ldw);  // an input layer of this shape fits the fused forward
 int fwd_fused_bf_waves();                           // its waves per workgroup (16 rows each)
-// Nonzero when a translation unit was built with a timing-only ablation (FWD_ABL, CB_ABL, BB_ABL, RD_ONLY_FIRST: wrong
-// results) or phase-stamp instrumentation (CB_STAMP, BB_STAMP). vihmc_version() reports them and plan
-// creation refuses such a library unless VIHMC_ALLOW_DIAG=1 (the A/B scripts' variant builds).
-int diag_switches_fused();
-int diag_switches_contract_bf();
-int diag_switches_bwd_bf();
-int diag_switches_layers();
-int diag_switches_bwd_chain();
-int diag_switches_gram();
-int diag_switches_kernels();
+// VIHMC_DIAG (vihmc_diag.h): nonzero in a build with timing-only ablations (wrong results) or phase stamps.
+// vihmc_version() reports it and plan creation refuses such a library unless VIHMC_ALLOW_DIAG=1.
 int diag_switches();
 hipError_t launch_fwd_fused(const FusedArgs& a, int nwaves, hipStream_t s);   // nwaves: 12 or 4
 hipError_t launch_fwd_fused_bf(const FusedArgs& a, int nw, hipStream_t s);     // bf16x6, 12 (or 4) waves

@@ -168,9 +168,6 @@ __device__ void contract_stats_body(const StatsJob& J, int c) {
 
 __global__ __launch_bounds__(256) void k_contract_stats(StatsJob J) { contract_stats_body(J, blockIdx.x); }
 
-#ifndef REDUCE_GROUP_MIN
-#define REDUCE_GROUP_MIN 32   // slab count from which a block's four waves split the slabs (see k_reduce)
-#endif
 
 // Fixed-order sum of partial slabs (p = 0, 1, ... sequentially -- bitwise reproducible); grid slice y = n_jobs
 // (when present) runs the likelihood statistics instead (saves their launch after side A); 4 consecutive
@@ -371,15 +368,7 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
 
 // Gradient gather + prior: grid (GATHER_SPLIT slices, C); each block writes its partial log-prior
 // and the last kernel of the pair adds them in a fixed order.
-#ifndef GATHER_ABL
-#define GATHER_ABL 0   // timing-only ablation (wrong results): 1 = the leapfrog gather scatters nothing into the packed
-                       // weights / images, 2 = nor stores theta / p
-#endif
-int diag_switches_kernels() { return GATHER_ABL; }
 
-#ifndef GATHER_SPLIT_N
-#define GATHER_SPLIT_N 64      // K slices per chain (16: 256 blocks at C = 16, 8.8 us)
-#endif
 constexpr int GATHER_SPLIT = GATHER_SPLIT_N;
 static_assert(GATHER_SPLIT <= GATHER_SPLIT_MAX, "lp_part slots");
 
@@ -536,7 +525,8 @@ __global__ __launch_bounds__(256) void k_hmc_accept(AcceptArgs a) {
         const AcceptDecision r = accept_decision(a, c);
         flags[0] = r.acc ? 1 : 0;
         flags[1] = r.ok ? 0 : 1;
-        if (!a.burn && a.samples) row_s = r.ok ? a.counts[c] : a.s_cap - 1;
+        // a full sample store (counts[c] reached the spare row s_cap - 1) writes the spare row and stops counting
+        if (!a.burn && a.samples) row_s = (r.ok && a.counts[c] < a.s_cap - 1) ? a.counts[c] : a.s_cap - 1;
     }
     __syncthreads();
     const bool acc = flags[0] != 0, err = flags[1] != 0;
@@ -597,7 +587,7 @@ __global__ __launch_bounds__(256) void k_hmc_accept_chain(AcceptArgs a, int C) {
     if (!a.burn) {
         if (r.acc) a.lp_last[c] = lp1;
         lp_next = r.acc ? lp1 : a.lp_last[c];
-        if (a.samples) a.counts[c] += r.ok ? 1 : 0;
+        if (a.samples) a.counts[c] += (r.ok && a.counts[c] < a.s_cap - 1) ? 1 : 0;
     } else {
         lp_next = r.acc ? lp1 : (r.ok ? a.lp_bp[c] : a.lp_last[c]);
         a.lp_cur[c] = lp_next;
@@ -1004,15 +994,19 @@ hipError_t launch_mlp_traj(const MlpArgs& a, const MlpTrajArgs& t, int C, int ma
     VIHMC_LAUNCH(k_mlp_traj<0>, dim3(C), dim3(64), shm, s, a, maxw, tt);
 }
 
-// Shader-clock stamp (measurement, vihmc_clock_stamp): 64 one-wave workgroups (8 per XCD under the b % 8 dispatch)
-// record their XCD id, s_memtime (shader-clock ticks) and s_memrealtime (100 MHz); two stamps around a timed region
-// give each XCD's average shader clock over it (MI355X_MICROARCH.md "DVFS give-back" item 6). Vector stores only.
+// Shader-clock stamp (measurement, vihmc_clock_stamp): CLOCK_STAMP_WG one-wave workgroups record their XCD id, their
+// HW_ID (CU / shader array / shader engine of the wave), s_memtime (shader-clock ticks) and s_memrealtime (100 MHz); two
+// stamps around a timed region give each CU's average shader clock over it, from the SAME CU's two readings (the
+// s_memtime counters of different CUs are not one clock domain: pairing medians across CUs read 2.58 GHz on one XCD
+// in round 4) -- MI355X_MICROARCH.md "DVFS give-back" item 6. Vector stores only.
 __global__ __launch_bounds__(64) void k_clock_stamp(unsigned long long* out) {
-    unsigned x;
+    unsigned x, hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     const unsigned long long t = __builtin_amdgcn_s_memtime();
     const unsigned long long r = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x < 3) out[blockIdx.x * 3 + threadIdx.x] = threadIdx.x == 0 ? (unsigned long long)x : threadIdx.x == 1 ? t : r;
+    const int i = threadIdx.x;
+    if (i < 4) out[blockIdx.x * 4 + i] = i == 0 ? (unsigned long long)x : i == 1 ? (unsigned long long)hw : i == 2 ? t : r;
 }
 
 hipError_t launch_clock_stamp(unsigned long long* out, hipStream_t s) {

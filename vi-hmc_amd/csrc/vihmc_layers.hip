@@ -15,36 +15,8 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// tanh for the layer epilogues: odd Taylor series through x^11 for |x| < 0.25 (truncation < 1e-8
-// relative), 1 - 2/(exp(2|x|)+1) with v_exp_f32 / v_rcp_f32 above (<= ~4 ulp); ~15 VALU ops
-// instead of the ~40 of the libm-accurate tanhf.
-__device__ __forceinline__ float tanh_fast(float x) {
-    const float ax = fabsf(x);
-    const float x2 = x * x;
-    float p = fmaf(x2, -0.0088632355f, 0.0218694885f);
-    p = fmaf(x2, p, -0.0539682540f);
-    p = fmaf(x2, p, 0.1333333333f);
-    p = fmaf(x2, p, -0.3333333333f);
-    const float small = fmaf(x * x2, p, x);
-    const float e = __expf(2.f * ax);
-    const float big = copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f), x);
-    return ax < 0.25f ? small : big;
-}
-
-#ifndef ROWDOT_TANH_CHEAP
-#define ROWDOT_TANH_CHEAP 1   // 0: tanh_fast above (Taylor / exp-rcp, ~17 VALU + 2 transcendental)
-#endif
-
-// (1 - t) / (1 + t), t = exp(-2|x|): the fused forward's form (vihmc_fused.hip tanh_f), 6 VALU + 2
-// transcendental, absolute error <= ~1.2e-7. The input layers' epilogue is the VALU bound of that launch (the
-// trunk's 16.3 M outputs at C = 16, profiles/r02_input/README.md).
-__device__ __forceinline__ float tanh_cheap(float x) {
-    const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(x));
-    return copysignf((1.f - t) * __builtin_amdgcn_rcpf(1.f + t), x);
-}
-
 __device__ __forceinline__ float act_apply_l(int act, float z) {
-    if (act == ACT_TANH) return ROWDOT_TANH_CHEAP ? tanh_cheap(z) : tanh_fast(z);
+    if (act == ACT_TANH) return tanh_acc(z);
     if (act == ACT_RELU) return fmaxf(z, 0.f);
     return z;
 }
@@ -599,11 +571,6 @@ size_t rowdot_lds_bytes(const RowdotArgs& a) {
     return m;
 }
 
-#ifndef RD_ONLY_FIRST
-#define RD_ONLY_FIRST 0   // timing-only (wrong results): 1 = grouped row-dot launches run the first problem's
-                          // workgroups only (the branch part of the input layers)
-#endif
-int diag_switches_layers() { return RD_ONLY_FIRST; }
 
 // branch + trunk input layers of the Burgers DeepONet (K = 101 -> 104 padded columns, K <= 100 run time): the
 // padded operand columns are zero (packed W rows, the uploaded input rows), so KF0 = 104 is exact

@@ -345,10 +345,7 @@ struct vihmc_plan {
 };
 
 namespace vihmc {
-int diag_switches() {
-    return diag_switches_fused() | diag_switches_contract_bf() | diag_switches_bwd_bf() | diag_switches_layers() |
-           diag_switches_bwd_chain() | diag_switches_gram() | diag_switches_kernels();
-}
+int diag_switches() { return VIHMC_DIAG; }   // vihmc_diag.h: one value for every translation unit
 }  // namespace vihmc
 
 namespace {
@@ -545,8 +542,10 @@ int guard_snapshot(vihmc_plan* p, int C, hipStream_t s) {
 // The form is a property of the plan (its max_chains), not of the call's chain count: a chain's trajectory does not
 // depend on how many chains share its launch (a ragged last rank, a partial batch) -- ADVICE r3.
 bool gram_on(const vihmc_plan* p) {
+    // a guard that cannot run (more chains than the fit ring holds) keeps the plan on the residual form: the guard
+    // exists to keep well-fitting chains off the cancellation-limited Gram gradient
     return p->gram && p->gram_alloc && p->W == 100 && p->contract_bf16x6 && p->maxC >= p->gram_min_chains &&
-           !p->y_masked;
+           !p->y_masked && (p->gram_guard == 0 || p->maxC <= GUARD_MAXC);
 }
 
 GramArgs gram_args(vihmc_plan* p, int C) {
@@ -941,9 +940,6 @@ inline int rowdot_tpw(int64_t total_tiles) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(8, cdiv(total_tiles, (int64_t)768)));
 }
 
-#ifndef VIHMC_FUSED_FWD
-#define VIHMC_FUSED_FWD 1
-#endif
 
 // Layers 1..L-1 of both nets can run in the fused register-resident forward (vihmc_fused.hip) when they
 // are all 100 -> 100 with the packed [W | bias] block contiguous.
@@ -2108,13 +2104,7 @@ int vihmc_graph_enable(vihmc_plan* p, int on) {
 void vihmc_plan_destroy(vihmc_plan* p) { delete p; }
 const char* vihmc_last_error(void) { return g_err.c_str(); }
 const char* vihmc_version(void) {
-    static std::string v = "vihmc 0.2.0 gfx950 diag=" + std::to_string(vihmc::diag_switches_fused()) + "," +
-                           std::to_string(vihmc::diag_switches_contract_bf()) + "," +
-                           std::to_string(vihmc::diag_switches_bwd_bf()) + "," +
-                           std::to_string(vihmc::diag_switches_layers()) + "," +
-                           std::to_string(vihmc::diag_switches_bwd_chain()) + "," +
-                           std::to_string(vihmc::diag_switches_gram()) + "," +
-                           std::to_string(vihmc::diag_switches_kernels());
+    static std::string v = "vihmc 0.3.0 gfx950 diag=" + std::to_string(vihmc::diag_switches());
     return v.c_str();
 }
 

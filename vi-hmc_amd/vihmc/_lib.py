@@ -102,7 +102,7 @@ def lib() -> ctypes.CDLL:
                 f.restype = res
                 f.argtypes = args
             ver = L.vihmc_version().decode()
-            if not re.search(r"diag=0(,0)*(\s|$)", ver) and os.environ.get("VIHMC_ALLOW_DIAG") != "1":
+            if not re.search(r"diag=0(\s|$)", ver) and os.environ.get("VIHMC_ALLOW_DIAG") != "1":
                 raise RuntimeError(f"{LIB_PATH} was built with timing-only diagnostic switches ({ver}); its results "
                                    "are wrong by design. Rebuild without EXTRA=-D*_ABL/-D*_STAMP, or set "
                                    "VIHMC_ALLOW_DIAG=1 for A/B timing only")

@@ -314,12 +314,17 @@ class _Engine:
 
 
 class ShaderClock:
-    """Average shader clock of each XCD over a region of a stream: vihmc_clock_stamp before and after it (64 one-wave
-    workgroups, 8 per XCD: XCD id, s_memtime, s_memrealtime); clock = d memtime / d memrealtime x 100 MHz."""
+    """Average shader clock over a region of a stream: vihmc_clock_stamp before and after it (256 one-wave workgroups:
+    XCD id, HW_ID, s_memtime, s_memrealtime). Each CU's clock is d memtime / d memrealtime x 100 MHz from ITS OWN two
+    readings (workgroups paired by (XCD, CU / shader array / engine)); per XCD the median over its paired CUs.
+    Readings above the 2,400-MHz maximum are physically impossible: they are rejected and counted, never averaged."""
+
+    WG = 256
+    MAX_MHZ = 2400.0
 
     def __init__(self, device):
         self.device = torch.device(device)
-        self.buf = torch.zeros(2, 64, 3, dtype=torch.int64, device=self.device)
+        self.buf = torch.zeros(2, self.WG, 4, dtype=torch.int64, device=self.device)
         self.L = _lib.lib()
 
     def _stamp(self, i):
@@ -334,17 +339,44 @@ class ShaderClock:
     def stop(self):
         self._stamp(1)
 
-    def mhz(self) -> dict:
-        """{xcd: MHz} from the two stamps (syncs); medians over each XCD's workgroups."""
-        b = self.buf.cpu().numpy().view(np.uint64).astype(np.float64)
+    @staticmethod
+    def _cu_key(xcc, hw):
+        # HW_ID: wave [3:0], SIMD [5:4], pipe [7:6], CU [11:8], shader array [12], shader engine [15:13]
+        return int(xcc), (int(hw) >> 8) & 0xFF
+
+    def per_cu(self) -> dict:
+        """{(xcd, cu key): MHz} for every CU stamped in both readings (syncs)."""
+        b = self.buf.cpu().numpy().view(np.uint64)
+        first = [{}, {}]
+        for i in range(2):
+            for row in b[i]:
+                first[i].setdefault(self._cu_key(row[0], row[1]), (float(row[2]), float(row[3])))
         out = {}
-        for x in sorted(set(int(v) for v in b[0, :, 0]) & set(int(v) for v in b[1, :, 0])):
-            a0, a1 = b[0][b[0, :, 0] == x], b[1][b[1, :, 0] == x]
-            dt = np.median(a1[:, 1]) - np.median(a0[:, 1])
-            dr = np.median(a1[:, 2]) - np.median(a0[:, 2])
-            if dr > 0:
-                out[x] = 100.0 * dt / dr
+        for k, (t0, r0) in first[0].items():
+            if k in first[1]:
+                t1, r1 = first[1][k]
+                if r1 > r0:
+                    out[k] = 100.0 * (t1 - t0) / (r1 - r0)
         return out
+
+    def summary(self) -> dict:
+        """Per-XCD medians of the valid per-CU clocks, their spread, and the rejected readings."""
+        cu = self.per_cu()
+        bad = {f"{k[0]}:{k[1]}": round(v, 1) for k, v in cu.items() if not (0.0 < v <= self.MAX_MHZ)}
+        by_xcd = {}
+        for (x, _), v in cu.items():
+            if 0.0 < v <= self.MAX_MHZ:
+                by_xcd.setdefault(x, []).append(v)
+        med = {x: float(np.median(v)) for x, v in sorted(by_xcd.items())}
+        vals = list(med.values())
+        mean = float(np.mean(vals)) if vals else None
+        spread = (max(vals) - min(vals)) / mean if vals else None
+        return {"mhz_by_xcd": med, "mean_mhz": mean, "spread": spread, "cus_paired": len(cu),
+                "cus_per_xcd": {x: len(v) for x, v in sorted(by_xcd.items())}, "rejected_above_max": bad}
+
+    def mhz(self) -> dict:
+        """{xcd: MHz}: the per-XCD medians of summary()."""
+        return self.summary()["mhz_by_xcd"]
 
 
 def expand_prior(K: int, mu, sd) -> (np.ndarray, np.ndarray):

@@ -300,7 +300,9 @@ class HMCRunner:
         self.trace = torch.empty(C, num_samples, device=device)
         # the Metropolis step on the GPU in one launch (vihmc_hmc_accept) instead of ~30 small torch ops per
         # iteration; the torch form below stays for CPU chains and strict_rng (whose accept draw needs ok first)
-        self._accept_native = device.type == "cuda" and not self.strict
+        # (engine evaluators only: a runner over user torch closures never needs libvihmc)
+        self._accept_native = (device.type == "cuda" and not self.strict
+                               and all(isinstance(e, EngineEvaluator) for e in self.evs))
         self._rows = torch.arange(C, device=device) * S_cap
         self.n = 0
 
@@ -438,14 +440,16 @@ class HMCRunner:
             cur = last
             bp = [None, None, None]
         samples = self.samples if (self.store and not burn) else None
-        stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        _lib.check(L.vihmc_hmc_accept(C, K, n, 1 if burn else 0, ptr(lp), ptr(lp_new), ptr(ke0), ptr(ke1),
-                                      ptr(logu), ptr(th_new), ptr(g_new),
-                                      ptr(last[0]), ptr(last[1]), ptr(last[2]), ptr(bp[0]), ptr(bp[1]), ptr(bp[2]),
-                                      ptr(cur[0]) if burn else None, ptr(cur[1]) if burn else None,
-                                      ptr(cur[2]) if burn else None, ptr(samples), self.samples.shape[1],
-                                      ptr(self.counts), ptr(self.accepted), self.accepted.stride(0), ptr(self.trace),
-                                      self.trace.stride(0), ptr(rho), ptr(err), stream), "vihmc_hmc_accept")
+        with torch.cuda.device(self.device):
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+            rc = L.vihmc_hmc_accept(C, K, n, 1 if burn else 0, ptr(lp), ptr(lp_new), ptr(ke0), ptr(ke1),
+                                  ptr(logu), ptr(th_new), ptr(g_new),
+                                  ptr(last[0]), ptr(last[1]), ptr(last[2]), ptr(bp[0]), ptr(bp[1]), ptr(bp[2]),
+                                  ptr(cur[0]) if burn else None, ptr(cur[1]) if burn else None,
+                                  ptr(cur[2]) if burn else None, ptr(samples), self.samples.shape[1],
+                                  ptr(self.counts), ptr(self.accepted), self.accepted.stride(0), ptr(self.trace),
+                                  self.trace.stride(0), ptr(rho), ptr(err), stream)
+        _lib.check(rc, "vihmc_hmc_accept")
         self.cur = cur
         return rho, err.bool()
 

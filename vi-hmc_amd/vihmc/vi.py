@@ -321,8 +321,10 @@ class BatchEngines:
         y, count = self.canonical(batch[1], batch[2])
         eng.set_data(xb, y)
         masked = count < xb.shape[0] * self.P
-        eng.option("y_masked", 1 if masked else 0)
-        eng.option("lik_count", count if masked else 0)
+        # options only on a change: vihmc_plan_option drops the plan's captured graphs (VIHMC_GRAPH=1)
+        for k, v in (("y_masked", 1 if masked else 0), ("lik_count", count if masked else 0)):
+            if eng.get_option(k) != v:
+                eng.option(k, v)
         self.count = count
         return eng
 
@@ -430,7 +432,10 @@ def mse(data_loader, model, noise_type=0, dataset="Burgers", engines: Optional[B
         with torch.no_grad():
             _, out = eng.forward(model.mu_flat().detach()[None].to(eng.device))
         y = engines.canonical(batch_data[1], batch_data[2])[0].to(eng.device)
-        l_total += torch.nanmean((out[0] - y) ** 2).item()   # p < P: over each item's own points
+        # p < P: over each item's own points -- the mask is on the targets only, so a NaN prediction (a diverged
+        # model) still gives NaN, as nn.MSELoss does in the reference
+        m = ~torch.isnan(y)
+        l_total += ((out[0] - y)[m] ** 2).mean().item()
     l_total = l_total / (i + 1)
     return l_total
 
