@@ -9,8 +9,9 @@
 // per evaluation and bitwise equal: every product and every accumulation order is k_bwd_bf2's.
 //
 // One 768-thread workgroup (8 dX + 4 dW waves, 3 per SIMD) per 64-row chunk of one net of one chain -- the
-// plan's chunk when a single chain's rows fill the chip in one round (C = 1: 16 + 160 workgroups). LDS (127 KB):
-//   2 sub-tiles x [delta_j planes [3][32][224 B] | delta_j fp32 tail [32][4]], 2 h sets x 2 sub-tiles x planes
+// plan's chunk when a single chain's rows fill the chip in one round (C = 1: 16 + 160 workgroups). LDS (153 KB):
+//   2 sub-tiles x [delta_j planes [3][32][224 B] | delta_j fp32 tail [32][4]], 2 h sets x 2 sub-tiles x planes,
+//   act'(h) of the epilogue [64][104] fp32
 // W_j^T never touches LDS: each dX wave keeps the fragments of its two input tiles in registers, loaded from the
 // pre-split W^T image (BWD_WTIMG, kept current by the scatter) right after its last MFMA of the layer before, so
 // they land while the workgroup writes the next deltas.
@@ -44,7 +45,11 @@ constexpr int CH_DT = 3 * CH_PLANE;
 constexpr int CH_BUF = CH_DT + CH_SUB * 16;            // 22016 per sub-tile
 constexpr int CH_HSUB = 3 * CH_PLANE;                  // 21504
 constexpr int CH_HOFF = 2 * CH_BUF;                    // 44032
-constexpr int CH_LDS = CH_HOFF + 4 * CH_HSUB;          // 130048
+// act'(h) of the dX epilogue, fp32 [64 rows][104] (stride 8 mod 16 dwords: the k-permuted float4 pattern of the
+// epilogue lanes is conflict free), written when the h rows are staged, read by the same lane one layer later
+constexpr int CH_AG = CH_HOFF + 4 * CH_HSUB;           // 130048
+constexpr int CH_AGLD = 104;
+constexpr int CH_LDS = CH_AG + CH_ROWS * CH_AGLD * 4;  // 156672
 static_assert(CH_LDS <= 160 * 1024, "LDS");
 constexpr int CH_THREADS = 768;
 constexpr int CH_HSLOTS = 4;                           // h float4 per dX lane: 64 rows x <= 32 float4 / 512
@@ -197,6 +202,41 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                     wt[u] = *reinterpret_cast<const float*>(ti + BWD_WTTAIL + 4 * (row * 4 + lg));
                 }
             };
+            // act'(h_{j-1}) of this lane's epilogue elements (rows 32 s + 16 h + lr, columns 16 (t0 + u) + 4 lg),
+            // computed from the fp32 h rows when they are staged (one layer ahead) and kept in the CH_AG array, which
+            // only this lane reads back, instead of rebuilding h from the three LDS planes per element (as k_bwd_bf2
+            // does since round 5; the same h, bitwise the same deltas). Slot v = 2 s + u of the aligned staging
+            // map; columns past 99 clamp to float4 24 (a duplicate item: the same value to the same address).
+            auto aligned_item = [&](int v, int& row, int& c4) {
+                row = 32 * (v >> 1) + 16 * h + lr;
+                c4 = min(4 * (t0 + (v & 1)) + lg, 24);
+            };
+            auto ag_at = [&](int v) {
+                int row, c4;
+                aligned_item(v, row, c4);
+                return reinterpret_cast<f32x4*>(sm + CH_AG + (row * CH_AGLD + 4 * c4) * 4);
+            };
+            auto act_of = [&](int act, const f32x4& x) __attribute__((always_inline)) {
+                f32x4 out;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) out[r] = TANH ? act_grad(ACT_TANH, x[r]) : act_grad(act, x[r]);
+                return out;
+            };
+            if (nl >= 2) {                             // the top layer's epilogue: h_{nl-2}, loaded again (L2)
+                const BwdChainLayer& L = N.L[nl - 1];
+                const float* H = L.H + c * L.h_cs + (int64_t)r0 * L.ldh;
+                const __amdgpu_buffer_rsrc_t hrs = bf6::make_rsrc(H, (uint32_t)((M - r0) * L.ldh * 4));
+                f32x4 x[2 * NU];
+#pragma unroll
+                for (int v = 0; v < 2 * NU; ++v) {
+                    int row, c4;
+                    aligned_item(2 * (v / NU) + v % NU, row, c4);
+                    x[v] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(hrs, (uint32_t)(row * L.ldh + 4 * c4) * 4u, 0, 0));
+                }
+#pragma unroll
+                for (int v = 0; v < 2 * NU; ++v) *ag_at(2 * (v / NU) + v % NU) = act_of(N.L[nl - 1].act, x[v]);
+            }
             load_w(max(nl - 1, 1));
             for (int j = nl - 1; j >= 0; --j) {
                 const int hs = (nl - 1 - j) & 1;       // h set of this layer's h_{j-1}
@@ -209,6 +249,9 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                 uint32_t hl[CH_HSLOTS];
                 const BwdChainLayer& Ln = N.L[max(j - 1, 0)];
                 const int hq_n = (Ln.n_in + 3) >> 2;
+                // the next layer has a dX part (j - 1 >= 1, n_in = 100): the aligned map, whose items are this lane's
+                // epilogue elements of that layer; else (the input layer next) item e = tid + 512 v, wrapped
+                const bool aligned = j >= 2;
                 {
                     const float* H = Ln.H + c * Ln.h_cs + (int64_t)r0 * Ln.ldh;
                     const __amdgpu_buffer_rsrc_t hrs = bf6::make_rsrc(H, (uint32_t)((M - r0) * Ln.ldh * 4));
@@ -216,11 +259,16 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
 #pragma unroll
                     for (int v = 0; v < CH_HSLOTS; ++v) {
                         // wrapped: a lane past the end moves an item another lane moves too (same value and address)
-                        const int e = (tid + 512 * v) % tot;
-                        uint32_t voff, loff;
-                        int c4, row;
-                        item_offsets(e, hq_n, Ln.ldh, hs ^ 1, voff, loff, c4, row);
-                        hl[v] = loff;
+                        int row, c4;
+                        if (aligned) {
+                            aligned_item(v, row, c4);
+                        } else {
+                            const int e = (tid + 512 * v) % tot;
+                            row = e / hq_n;
+                            c4 = e - row * hq_n;
+                        }
+                        const uint32_t voff = (uint32_t)(row * Ln.ldh + 4 * c4) * 4u;
+                        hl[v] = (uint32_t)(CH_HOFF + (2 * (hs ^ 1) + (row >> 5)) * CH_HSUB + (row & 31) * CH_PITCH + 8 * c4);
                         hx[v] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hrs, voff, 0, 0));
                     }
                 }
@@ -247,19 +295,13 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
                                 else ac[u] = six(wf[u][kb], db, ac[u]);
                             }
                         }
-                        // epilogue: act'(h_{j-1}) from the exact h planes
+                        // epilogue: act'(h_{j-1}), staged with h_{j-1} one layer ago (or in the prologue)
+                        (void)act;
 #pragma unroll
                         for (int u = 0; u < NU; ++u) {
-                            const int col = 16 * (t0 + u) + 4 * lg;
-                            const unsigned char* hrow = hset(hs, s) + (16 * h + lr) * CH_PITCH + 2 * col;
-                            bf16x4 hq[3];
+                            const f32x4 ag = *ag_at(2 * s + u);
 #pragma unroll
-                            for (int p = 0; p < 3; ++p) hq[p] = *reinterpret_cast<const bf16x4*>(hrow + p * CH_PLANE);
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) {
-                                const float hv = ((float)hq[2][r] + (float)hq[1][r]) + (float)hq[0][r];
-                                ac[u][r] = ac[u][r] * (TANH ? act_grad(ACT_TANH, hv) : act_grad(act, hv));
-                            }
+                            for (int r = 0; r < 4; ++r) ac[u][r] = ac[u][r] * ag[r];
                             o[s][u] = ac[u];
                         }
                     }
@@ -273,6 +315,12 @@ __global__ __launch_bounds__(CH_THREADS, 1) void k_bwd_chain(BwdChainArgs A) {
 #pragma unroll
                     for (int v = 0; v < CH_HSLOTS; ++v) store_planes(sm + hl[v], hx[v]);
                     db_column(hs ^ 1, 4 * hq_n, tid);
+                    if (aligned) {                     // act'(h_{j-2}) for the next layer's epilogue
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                            for (int u = 0; u < NU; ++u) *ag_at(2 * s2 + u) = act_of(N.L[j - 1].act, hx[2 * s2 + u]);
+                    }
                 }
 #if CH_STAMP
                 asm volatile("" :: "v"(o[0][0]), "v"(o[1][0]));
