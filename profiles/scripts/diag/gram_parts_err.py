@@ -14,14 +14,15 @@ from vihmc.engine import DeepONetEngine, trunk_features  # noqa: E402
 from vihmc.layout import DeepONetSpec  # noqa: E402
 
 noise = float(sys.argv[1]) if len(sys.argv) > 1 else 1e-2
+C = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 s = DeepONetSpec()
 p = deeponet_problem(seed=3, noise=noise, mu_noise=0.0)
 th = p.teacher[p.grad_ind].astype(np.float32)
 eng = DeepONetEngine(s, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, 1e3, "NLL", 1.0,
-                     max_chains=1, device="cuda:0")
+                     max_chains=C, device="cuda:0")
 eng.option("gram_min_chains", 1)
 eng.option("gram_guard", 0)
-eng.grad(torch.tensor(th[None], device="cuda:0"))
+eng.grad(torch.tensor(np.stack([th] * C), device="cuda:0"))
 assert eng.get_option("gram") & 2
 N, P = p.N, p.P
 BLK, PL, PITCH = 22528, 7168, 224
@@ -30,6 +31,7 @@ BLK, PL, PITCH = 22528, 7168, 224
 def image(name, rows):
     raw = eng.debug_buffer(name)
     nb = (rows + 31) // 32
+    raw = raw[:raw.size // C]                            # chain 0
     out = np.zeros((nb * 32, 112))
     for pl in range(3):
         for b in range(nb):
@@ -57,16 +59,24 @@ def tiles(raw, groups, ngroup_rows):
 NG, PT = (N + 255) // 256, (P + 255) // 256
 tbs = eng.debug_buffer("gram_tb_sum")
 if tbs is not None:
+    tbs = tbs[:tbs.size // C]
     tb_eng = tiles(tbs.view(np.float32)[:NG * 8 * 14 * 256].astype(np.float64), NG, N)[:, :101]
 else:
-    tbp = eng.debug_buffer("gram_tb").view(np.float32).astype(np.float64)
+    tbp = eng.debug_buffer("gram_tb")
+    tbp = tbp[:tbp.size // C].view(np.float32).astype(np.float64)
     S = tbp.size // (NG * 8 * 14 * 256)
     tb_eng = sum(tiles(tbp[s_ * NG * 8 * 14 * 256:(s_ + 1) * NG * 8 * 14 * 256], NG, N) for s_ in range(S))[:, :101]
-gt_eng = eng.debug_buffer("gram_gt").view(np.float32).reshape(112, 112)[:101, :101].astype(np.float64)
-tt = eng.debug_buffer("gram_tt").view(np.float32).astype(np.float64)
-SB = tt.size // (PT * 8 * 14 * 256)
-tt = tt.reshape(PT, SB, 8 * 14 * 256)
-acc_eng = sum(tiles(tt[:, sb].reshape(-1), PT, P) for sb in range(SB))[:, :101]
+gt_eng = eng.debug_buffer("gram_gt").view(np.float32)[:112 * 112].reshape(112, 112)[:101, :101].astype(np.float64)
+tt = eng.debug_buffer("gram_tt")
+acc_eng = None
+if tt is not None and tt.size:
+    tt = tt[:tt.size // C].view(np.float32).astype(np.float64)
+    SB = tt.size // (PT * 8 * 14 * 256)
+    tt = tt.reshape(PT, SB, 8 * 14 * 256)
+    acc_eng = sum(tiles(tt[:, sb].reshape(-1), PT, P) for sb in range(SB))[:, :101]
+st = eng.debug_buffer("gram_stats")
+st = st[:st.size // C].view(np.float64)
+db_eng = st[1:2 * PT * 8:2].sum()                       # sum over (pt, wave) slots of d ll / d b0 (= -gscale acc)
 
 
 def rel(a, b):
@@ -78,6 +88,46 @@ print(f"  T_b  = y Zt^        rel err {rel(tb_eng, Tb):.3e}   |T_b| / |dZb| = {n
 print(f"  Gt   = Zt^T Zt^     rel err {rel(gt_eng, Gt):.3e}")
 print(f"  dZb from T_b err    rel err {rel(Zb @ Gt - tb_eng, dzb_ex):.3e}")
 print(f"  dZb from Gt err     rel err {rel(Zb @ gt_eng - Tb, dzb_ex):.3e}")
-print(f"  T_t acc = y^T Zb^ - Zt^ Gb  rel err {rel(acc_eng, acc_ex):.3e}   |y^T Zb^| / |acc| = "
-      f"{np.linalg.norm(Tt) / np.linalg.norm(acc_ex):.1f}")
-print(f"  column 100 (d ll / d b0): engine {acc_eng[:, 100].sum():.6e} exact {acc_ex[:, 100].sum():.6e}")
+if acc_eng is not None:
+    print(f"  T_t acc = y^T Zb^ - Zt^ Gb  rel err {rel(acc_eng, acc_ex):.3e}   |y^T Zb^| / |acc| = "
+          f"{np.linalg.norm(Tt) / np.linalg.norm(acc_ex):.1f}")
+print(f"  d ll / d b0: engine slots {db_eng:.6e} exact {acc_ex[:, 100].sum():.6e} (gscale = -1: d ll / d b0 = sum acc)"
+      f" -> abs err {abs(db_eng - acc_ex[:, 100].sum()):.3e}")
+
+# ---- gradient error of each intermediate's error, through an fp64 backward (the oracle's activations)
+from oracle.deeponet_ref import deeponet_layout, np_forward, trunk_feats_np  # noqa: E402
+lay = deeponet_layout(s.in_branch, s.width_branch, s.depth_branch, s.in_trunk, s.width_trunk, s.depth_trunk, s.out)
+flat = p.mu.astype(np.float64).copy()
+flat[p.grad_ind] = th
+_, hs = np_forward(lay, flat, p.branch_in, trunk_feats_np(p.trunk_in))
+
+
+def backward(dzb, dzt):
+    br, tr, D = lay
+    g = np.zeros(D)
+    for name, layers, dz in (("b", br, dzb[:, :100]), ("t", tr, dzt[:, :100])):
+        h, gg = hs[name], dz
+        for j in range(len(layers) - 1, -1, -1):
+            l = layers[j]
+            d = gg if not l.act else gg * (1 - h[j + 1] ** 2)
+            g[l.w_off:l.w_off + l.n_out * l.n_in] = (d.T @ h[j]).reshape(-1)
+            g[l.b_off:l.b_off + l.n_out] = d.sum(0)
+            if j > 0:
+                gg = d @ flat[l.w_off:l.w_off + l.n_out * l.n_in].reshape(l.n_out, l.n_in)
+    return g[p.grad_ind]
+
+
+dzt_ex = -acc_ex                                          # gscale = -1: dZt = -gscale acc... (sign: dZt = acc * 1)
+dzt_ex = acc_ex
+g_ex = backward(dzb_ex, dzt_ex)
+nrm = np.linalg.norm(g_ex)
+gt32 = Gt.astype(np.float32).astype(np.float64)
+gb32 = Gb.astype(np.float32).astype(np.float64)
+terms = {"T_b (engine slabs)": (Zb @ Gt - tb_eng, dzt_ex),
+         "Gt rounded to fp32 (exact)": (Zb @ gt32 - Tb, dzt_ex),
+         "Gt (engine)": (Zb @ gt_eng - Tb, dzt_ex),
+         "Gb rounded to fp32 (exact)": (dzb_ex, Tt - Zt @ gb32)}
+if acc_eng is not None:
+    terms["T_t acc (engine)"] = (dzb_ex, acc_eng)
+for k, (a, b) in terms.items():
+    print(f"  grad err from {k:28s} {np.linalg.norm(backward(a, b) - g_ex) / nrm:.3e}")

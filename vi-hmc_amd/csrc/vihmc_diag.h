@@ -53,3 +53,5 @@
 // the fp32-MFMA contraction (k_contract_ws + k_contract2) and fused forward forms (0: the round-1 generic kernels)
 #define VIHMC_CONTRACT_WS 1
 #define VIHMC_FUSED_FWD 1
+// Gram form: the dZb epilogue's sums (Zb^ Gt over v, the T_b slabs) in fp64 (0: fp32 fma)
+#define GRAM_DZB_FP64 1

@@ -745,6 +745,9 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
                     split3(av, a0, a1, a2);
                     const __bf16 al = lg == 0 ? a0 : (lg == 1 ? a1 : a2);
                     f100 = (uint64_t)__builtin_bit_cast(uint16_t, al);
+                    // trunk: column 101 = 1 (planes 1, 0, 0), so the Gram-t tiles carry the column sums sum_p Zt^[p][v]
+                    // in fp64 (Gt[v][101]) for the exact d ll / d b0 (vihmc_gram.hip gram_tt_epilogue)
+                    if (N.aug == 2 && lg == 0) f100 |= (uint64_t)0x3F80u << 16;
                 }
                 z[0] = f100;
                 z[1] = 0;

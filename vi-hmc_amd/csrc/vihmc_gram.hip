@@ -30,6 +30,7 @@
 // YA = y[n][p] and YB = y^T[p][n] store each 32-long k block in that order, so a lane's A fragment is one 16-B load.
 #include "vihmc_internal.h"
 #include "vihmc_bf16x6.h"
+#include <type_traits>
 
 namespace vihmc {
 
@@ -45,7 +46,14 @@ constexpr int GR_PIECES = GR_BLK / 1024;                  // 21 one-KB DMA piece
 static_assert(GR_PIECES * 1024 == GR_BLK, "whole DMA pieces");
 constexpr int GR_NBUF = 3;
 constexpr int GR_LDS = GR_NBUF * GR_BLK;                  // 64.5 KB
-static_assert((101 * 112 + 101 * 32) * 4 <= GR_LDS, "dZb epilogue staging fits the ring");
+// k_gram_b: the ring, then the 4th planes of the 4 -Gb extension blocks (DMA'd first); its dZb epilogue units stage
+// Gt in fp64 [101][112] and Zb^T [101][32] fp32 over the same LDS
+constexpr int GRB_P3 = GR_LDS;
+constexpr int GRB_LDS_T = GRB_P3 + 4 * GRAM_P3_BLOCK;     // 92.5 KB
+constexpr int GRB_DZB = 101 * 112 * 8 + 101 * 32 * 4;     // 103,424 B
+constexpr int GRB_LDS = GRB_LDS_T > GRB_DZB ? GRB_LDS_T : GRB_DZB;
+static_assert(GRB_LDS <= 160 * 1024, "k_gram_b LDS");
+static_assert(GRAM_P3_BLOCK % 1024 == 0, "whole DMA pieces");
 constexpr int GR_CW = 8;                                  // compute waves (32 rows each)
 constexpr int GR_THREADS = 64 * (GR_CW + 1);              // + one DMA wave
 
@@ -125,6 +133,27 @@ __device__ __forceinline__ void mma_block(const unsigned char* buf, int tro, con
     }
 }
 
+// the extension blocks' product with a FOUR-plane B (the -Gb image, k_gram_sum): the three order-3 products
+// (a2 b1, a1 b2, a0 b3: ~2^-24 of the product each) first, then bf6::six's six -- the B value carried to ~32 bits
+__device__ __forceinline__ f32x4 nine(const bf16x8 (&a)[3], const bf16x8 (&b)[3], const bf16x8& b3, f32x4 acc) {
+    acc = bf6::mfma_bf(a[2], b[1], acc);
+    acc = bf6::mfma_bf(a[1], b[2], acc);
+    acc = bf6::mfma_bf(a[0], b3, acc);
+    return six(a, b, acc);
+}
+__device__ __forceinline__ void mma_block9(const unsigned char* buf, const unsigned char* p3, int tro,
+                                           const bf16x8 (&a)[2][3], f32x4 (&acc)[2][7]) {
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        bf16x8 b[3];
+        load_b(buf, tro, t, b);
+        const bf16x8 b3 = bf6::tr_frag(p3, tro, 16 * t);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[rt][t] = nine(a[rt], b, b3, acc[rt][t]);
+        __builtin_amdgcn_sched_barrier(0);             // one tile's fragments live at a time (no hoisting: spills)
+    }
+}
+
 // unit of a workgroup with XCD-contiguous unit ranges (workgroup b runs on XCD b % 8, checked by
 // scripts/diag/xcc_probe.hip): `upx` slots of every XCD take units [x upx, (x + 1) upx) of the grouped list, `gpx`
 // slots round-robin units of the second list; -1 = idle slot. second_first: k_gram_a's Gram units are shorter than
@@ -167,6 +196,10 @@ __global__ __launch_bounds__(256) void k_gram_aug(GramArgs A) {
         *reinterpret_cast<__bf16*>(row + f) = a;
         *reinterpret_cast<__bf16*>(row + GR_PL + f) = bb;
         *reinterpret_cast<__bf16*>(row + 2 * GR_PL + f) = (__bf16)(rr - (float)bb);
+        // column 101 = 1: Gt[v][101] = sum_p Zt^[p][v] (the exact d ll / d b0, gram_tt_epilogue)
+        *reinterpret_cast<__bf16*>(row + f + 2) = (__bf16)1.0f;
+        *reinterpret_cast<__bf16*>(row + GR_PL + f + 2) = (__bf16)0.0f;
+        *reinterpret_cast<__bf16*>(row + 2 * GR_PL + f + 2) = (__bf16)0.0f;
     }
 }
 
@@ -414,23 +447,39 @@ __global__ __launch_bounds__(256) void k_gram_sum(GramArgs A) {
     int rem = tile, vt = 0;
     while (rem >= 7 - vt) rem -= 7 - vt++;
     const int t = vt + rem, v = 16 * vt + 4 * (l >> 4) + r, x = 16 * t + (l & 15);
+    // the fp64 column sums of the exact d ll / d b0: sum_n Zb^[n][v] = Gb[v][100], sum_p Zt^[p][v] = Gt[v][101]
+    if (x == (gb ? 100 : 101)) A.gcol[c * A.gcol_cs + (gb ? 0 : 112) + v] = sum;
     if (!gb) {
         float* gt = A.gt + c * A.gt_cs2;
+        double* g64 = A.gt64 + c * A.gt_cs2;
         gt[v * 112 + x] = (float)sum;
-        if (vt != t) gt[x * 112 + v] = (float)sum;
+        g64[v * 112 + x] = sum;
+        if (vt != t) {
+            gt[x * 112 + v] = (float)sum;
+            g64[x * 112 + v] = sum;
+        }
         return;
     }
-    // -Gb pre-split: element (v, x) -> extension block v / 32, row v % 32, feature x
+    // -Gb pre-split from the fp64 sum into FOUR bf16 planes (~32 significant bits): every trunk row's extension product
+    // Zt^ Gb uses the same Gb, so its representation error is coherent over the P rows -- rounded to fp32 it cost
+    // 4.2e-4 of the gradient norm at fit 0.13 (profiles/r05d_gram_parts.txt); k_gram_b adds the order-3 products.
+    // Element (v, x) -> extension block v / 32, row v % 32, feature x; planes 0..2 in the block image, plane 3 in gb3img
     unsigned char* gbi = A.gbimg + c * A.gbimg_cs;
-    const float val = (float)-sum;
+    unsigned char* gb3 = A.gb3img + c * 4 * GRAM_P3_BLOCK;
+    const double val = -sum;
     auto put = [&](int vv, int xx) __attribute__((always_inline)) {
-        const __bf16 p0 = (__bf16)val;
-        const float rr = val - (float)p0;
-        const __bf16 p1 = (__bf16)rr;
+        double rr = val;
+        __bf16 pl[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            pl[k] = (__bf16)(float)rr;         // rr -> fp32 -> bf16: the fp32 step is exact for k >= 1 (|rr| small)
+            rr -= (double)(float)pl[k];
+        }
         unsigned char* q = gbi + (vv / 32) * CONTRACT_SPLIT_BLOCK + (vv % 32) * bf6::PITCH + 2 * xx;
-        *reinterpret_cast<__bf16*>(q) = p0;
-        *reinterpret_cast<__bf16*>(q + GR_PL) = p1;
-        *reinterpret_cast<__bf16*>(q + 2 * GR_PL) = (__bf16)(rr - (float)p1);
+        *reinterpret_cast<__bf16*>(q) = pl[0];
+        *reinterpret_cast<__bf16*>(q + GR_PL) = pl[1];
+        *reinterpret_cast<__bf16*>(q + 2 * GR_PL) = pl[2];
+        *reinterpret_cast<__bf16*>(gb3 + (vv / 32) * GRAM_P3_BLOCK + (vv % 32) * bf6::PITCH + 2 * xx) = pl[3];
     };
     put(v, x);
     if (vt != t) put(x, v);
@@ -473,6 +522,12 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     if (wave == GR_CW) {
         const unsigned char* bsrc = A.bimg + c * A.bimg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
         const unsigned char* gsrc = A.gbimg + c * A.gbimg_cs;
+        if (ext) {
+            // the 4th -Gb planes of the 4 extension blocks, first: dma_role's counted waits retire them with block 0
+            const unsigned char* p3 = A.gb3img + c * 4 * GRAM_P3_BLOCK;
+            for (int k = 0; k < 4 * GRAM_P3_BLOCK / 1024; ++k)
+                bf6::glds16_asm(p3 + k * 1024 + lane * 16, lds + GRB_P3 + k * 1024);
+        }
         dma_role(lds, lane, nb, [&](int i) {
             return i < nbm ? bsrc + (int64_t)i * CONTRACT_SPLIT_BLOCK : gsrc + (int64_t)(i - nbm) * CONTRACT_SPLIT_BLOCK;
         });
@@ -537,7 +592,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
                         if (!pval[rt]) lo = bf16x4{}, hi = bf16x4{};
                         a[rt][pl] = bf6::cat8(lo, hi);
                     }
-                mma_block(lds + ((nbm + e) % GR_NBUF) * GR_BLK, tro, a, acc);
+                mma_block9(lds + ((nbm + e) % GR_NBUF) * GR_BLK, lds + GRB_P3 + e * GRAM_P3_BLOCK, tro, a, acc);
             }
         }
     }
@@ -564,7 +619,6 @@ __device__ __forceinline__ void gram_tt_epilogue(const GramArgs& A, int c, int p
     // dZt = -gscale acc
     const float sc = -A.gscale;
     float* out = A.dzt + c * A.dzt_cs;
-    float db = 0.f;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -573,18 +627,25 @@ __device__ __forceinline__ void gram_tt_epilogue(const GramArgs& A, int c, int p
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int p = p0 + 16 * rt + 4 * lg + r;
-                const float v = sc * acc[rt][t][r];
-                if (x < 100 && p < A.P) out[(int64_t)p * A.ldz + x] = v;
-                if (t == 6 && lr == 4) db += v;     // x == 100: sum_n G[n][p] (rows past P are 0)
+                if (x < 100 && p < A.P) out[(int64_t)p * A.ldz + x] = sc * acc[rt][t][r];
             }
         }
-    // lanes 4, 20, 36, 52 hold the wave's column-100 sums
-    db += __shfl_xor(db, 16, 64);
-    db += __shfl_xor(db, 32, 64);
-    if (lane == 4) {
+    // d ll / d b0 = sum G = gscale (sum_{n,p} (S + b0) - sum y) = gscale (sum_v colsum_b[v] colsum_t[v] - sum y), all in
+    // fp64 from the fp64 Gram slab sums (k_gram_sum) and the plan's sum y: the column-100 sum of acc (sum over p of
+    // sum_n y[n][p] - Zt^ Gb, each ~sqrt(N) |y| / |S - y| larger than sum_n G[n][p]) was the Gram form's largest
+    // error, 8.5e-3 absolute on a 16.6 derivative at fit 0.13 (~1e-3 of the gradient norm: profiles/r05d_gram_parts.txt).
+    // One slot per chain carries it (slot 0; the statistics slice adds the PT * 8 slots).
+    if (lane == 0) {
         double* st = A.stats + c * A.stats_cs + 2 * (int64_t)(pt * GR_CW + wave);
+        double db = 0.0;
+        if (pt == 0 && wave == 0) {
+            const double* col = A.gcol + c * A.gcol_cs;
+            double ss = 0.0;
+            for (int v = 0; v <= 100; ++v) ss = fma(col[v], col[112 + v], ss);
+            db = (double)A.gscale * (ss - *A.ysum);
+        }
         st[0] = 0.0;
-        st[1] = (double)db;
+        st[1] = db;
     }
 }
 
@@ -627,16 +688,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 // 3e-5 with this sum exact: profiles/r05_gram_fit_table.json). The products of fp32 values are exact in fp64.
 // ---------------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char* lds) {
-    float* gts = reinterpret_cast<float*>(lds);                  // Gt [101][112]
-    float* zbt = gts + 101 * 112;                                // Zb^T [101][32]
+    double* gts = reinterpret_cast<double*>(lds);                // Gt [101][112], fp64 (k_gram_sum's gt64)
+    float* zbt = reinterpret_cast<float*>(gts + 101 * 112);      // Zb^T [101][32]
     const int ngroups = (A.N + 31) / 32;
     const int c = u / ngroups, m = u - c * ngroups;
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-    const float* gt = A.gt + c * A.gt_cs2;
-    for (int e = tid; e < 101 * 28; e += GR_THREADS) {
-        const int v = e / 28, q = e - v * 28;
-        *reinterpret_cast<f32x4*>(gts + v * 112 + 4 * q) = *reinterpret_cast<const f32x4*>(gt + v * 112 + 4 * q);
+    const double* gt = A.gt64 + c * A.gt_cs2;
+    for (int e = tid; e < 101 * 56; e += GR_THREADS) {
+        const int v = e / 56, q = e - v * 56;
+        typedef double f64x2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<f64x2*>(gts + v * 112 + 2 * q) = *reinterpret_cast<const f64x2*>(gt + v * 112 + 2 * q);
     }
     const float* zb = A.zb + c * A.zb_cs;
     for (int e = tid; e < 32 * 101; e += GR_THREADS) {
@@ -655,25 +717,26 @@ __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char
     float* out = A.dzb + c * A.dzb_cs;
     for (int tile = wv; tile < 14; tile += GR_THREADS / 64) {
         const int rt = tile / 7, t = tile - rt * 7;
-        double ts[4] = {0.0, 0.0, 0.0, 0.0};
+        using acc_t = std::conditional_t<GRAM_DZB_FP64 != 0, double, float>;
+        acc_t ts[4] = {0, 0, 0, 0};
         for (int ss = 0; ss < nslab; ++ss) {
             const f32x4 v = *reinterpret_cast<const f32x4*>(tb + ss * sstride + tile * 256);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ts[r] += (double)v[r];
+            for (int r = 0; r < 4; ++r) ts[r] += (acc_t)v[r];
         }
-        double gz[4] = {0.0, 0.0, 0.0, 0.0};
+        acc_t gz[4] = {0, 0, 0, 0};
         const int x = 16 * t + lr;
         for (int v = 0; v < 101; ++v) {
             const f32x4 z = *reinterpret_cast<const f32x4*>(zbt + v * 32 + 16 * rt + 4 * lg);
-            const double g = (double)gts[v * 112 + x];
+            const acc_t g = (acc_t)gts[v * 112 + x];     // fp64 Gt (with GRAM_DZB_FP64 = 0 rounded to fp32)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) gz[r] = fma((double)z[r], g, gz[r]);
+            for (int r = 0; r < 4; ++r) gz[r] = fma((acc_t)z[r], g, gz[r]);
         }
         if (x < 100) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int n = n32 + 16 * rt + 4 * lg + r;
-                if (n < A.N) out[(int64_t)n * A.ldz + x] = (float)((double)A.gscale * (gz[r] - ts[r]));
+                if (n < A.N) out[(int64_t)n * A.ldz + x] = (float)((acc_t)A.gscale * (gz[r] - ts[r]));
             }
         }
     }
@@ -746,7 +809,7 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     if (gt) hipLaunchKernelGGL(k_gram_a<1>, ga, dim3(GR_THREADS), GR_LDS, s, a);
     else hipLaunchKernelGGL(k_gram_a<0>, ga, dim3(GR_THREADS), GR_LDS, s, a);
     hipLaunchKernelGGL(k_gram_sum, dim3(56 + (a.tb_sum ? a.NG * 28 : 0), a.C), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_gram_b, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GR_LDS, s, a);
+    hipLaunchKernelGGL(k_gram_b, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GRB_LDS, s, a);
     if (a.SB > 1) hipLaunchKernelGGL(k_gram_tt, dim3(a.PT * GR_CW, a.C), dim3(64), 0, s, a);
     return hipGetLastError();
 }

@@ -183,11 +183,15 @@ struct GramArgs {
     double* gb_part; int64_t gb_cs; int32_t Sb, SLb;       // [C][Sb][28 tiles][256] Gram-b slabs of SLb branch blocks
     float* tb_sum; int64_t tbs_cs;                         // [C][NG][8][14][256] sum of the S T_b slabs (S > 8), else null
     float* gt; int64_t gt_cs2;                             // [C][112][112] Zt^T Zt^
+    double* gt64;                                          // [C][112][112] the same in fp64 (dZb epilogue), gt_cs2
+    unsigned char* gb3img;                                 // [C][4][GRAM_P3_BLOCK]: 4th bf16 plane of -Gb
     unsigned char* gbimg; int64_t gbimg_cs;                // [C][4 blocks] -Zb^T Zb^ pre-split
     const float* zb; int64_t zb_cs;                        // fp32 Z_b rows [N][ldz]
     float* dzb; int64_t dzb_cs;                            // dZ_b [N][ldz]
     float* dzt; int64_t dzt_cs;                            // dZ_t [P][ldz]
-    double* stats; int64_t stats_cs;                       // (0, sum G) pairs, PT * 8 per chain
+    double* stats; int64_t stats_cs;                       // (0, sum G) pairs, PT * 8 per chain (slot 0: d ll / d b0)
+    double* gcol; int64_t gcol_cs;                         // [C][2][112] fp64 column sums of Zb^ (Gb[v][100]), Zt^ (Gt[v][101])
+    const double* ysum;                                    // sum y (fp64, with sum y^2 by k_ysq)
     const float* b0; int64_t b0_cs;
     int32_t N, P, ldz, NG, S, SL, PT, C;
     int32_t St, SLt;                                       // Gram-t split of the trunk blocks (gt_part: St slabs)
@@ -201,6 +205,7 @@ struct GramArgs {
     float gscale;
     int32_t sel; ChainBits bits;                           // sel = 1: chains whose bit is set exit (residual form)
 };
+constexpr int GRAM_P3_BLOCK = 32 * 224;   // bytes of one 32-row plane of a pre-split block (the 4th plane of -Gb)
 constexpr int GRAM_TB_DIRECT = 8;   // up to this many T_b slabs the dZb epilogue units sum them themselves
 hipError_t launch_gram(const GramArgs& a, hipStream_t s);
 hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld, __bf16* yb,

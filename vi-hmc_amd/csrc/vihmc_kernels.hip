@@ -910,23 +910,40 @@ hipError_t launch_contract_stats(const StatsJob& J, int C, hipStream_t s) {
     VIHMC_LAUNCH(k_contract_stats, dim3(C), dim3(256), 0, s, J);
 }
 
-// sum of y^2 in fixed order: YSQ_PARTS contiguous chunks (thread-strided fp64 sums + block tree), then one block
-// over the partials
+// sum of y^2 and sum of y in fixed order: YSQ_PARTS contiguous chunks (thread-strided fp64 sums + block tree), then
+// one block over the partials: out[0] = sum y^2, out[1] = sum y (part holds YSQ_PARTS pairs)
 __global__ __launch_bounds__(256) void k_ysq_part(const float* y, int64_t n, double* part) {
     __shared__ double sh[8];
     const int64_t chunk = (n + YSQ_PARTS - 1) / YSQ_PARTS;
     const int64_t e0 = (int64_t)blockIdx.x * chunk, e1 = e0 + chunk < n ? e0 + chunk : n;
-    double v = 0.0;
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) v += (double)y[e] * (double)y[e];
+    double v = 0.0, w = 0.0;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) {
+        const double x = (double)y[e];
+        v += x * x;
+        w += x;
+    }
     v = block_sum(v, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = v;
+    __syncthreads();
+    w = block_sum(w, sh);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = v;
+        part[YSQ_PARTS + blockIdx.x] = w;
+    }
 }
 __global__ __launch_bounds__(256) void k_ysq_final(const double* part, double* out) {
     __shared__ double sh[8];
-    double v = 0.0;
-    for (int i = threadIdx.x; i < YSQ_PARTS; i += 256) v += part[i];
+    double v = 0.0, w = 0.0;
+    for (int i = threadIdx.x; i < YSQ_PARTS; i += 256) {
+        v += part[i];
+        w += part[YSQ_PARTS + i];
+    }
     v = block_sum(v, sh);
-    if (threadIdx.x == 0) *out = v;
+    __syncthreads();
+    w = block_sum(w, sh);
+    if (threadIdx.x == 0) {
+        out[0] = v;
+        out[1] = w;
+    }
 }
 hipError_t launch_ysq(const float* y, int64_t n, double* part, double* out, hipStream_t s) {
     hipLaunchKernelGGL(k_ysq_part, dim3(YSQ_PARTS), dim3(256), 0, s, y, n, part);
