@@ -63,6 +63,16 @@ def main():
             rows["wm"].append(np.mean(mm[8:, i] - bar[8:, i]))
             rows["xl"].append(np.max(mm[:8, i]) - t0)
             rows["wl"].append(np.max(mm[8:, i]) - t0)
+    pro, tail, ns = [], [], []
+    for g in np.nonzero(ok)[0]:
+        bar = st[g, :, :, 0]
+        nsub = int(np.sum(bar[0] > 0))
+        ns.append(nsub)
+        pro.append(bar[:, 0].min() - rl[g, 0, 0])                      # start -> first barrier exit
+        last = st[g, :, nsub - 1, 2].max() if nsub else rl[g, 0, 0]
+        tail.append(rl[g, 1, 0] - last)                                   # last sub-tile's work -> workgroup end
+    print(f"prologue (start -> first barrier exit) {np.mean(pro):7.0f} cycles; tail (last stamp -> end) "
+          f"{np.mean(tail):7.0f}; sub-tiles per workgroup {np.mean(ns):.1f}; total {np.mean(cyc):.0f} cycles")
     f = lambda a: f"{np.mean(a):7.0f} (p10 {np.percentile(a, 10):6.0f}, p90 {np.percentile(a, 90):6.0f})"  # noqa: E731
     print("cycles per 32-row sub-tile (shader clock), steady state:")
     print(f"  barrier period               {f(rows['per'])}")

@@ -11,14 +11,15 @@
 // 16 waves = 8 dX + 4 dW + 4 staging waves (one dW and one staging wave per SIMD). LDS (151 KB):
 //   2 x [D planes [3][32][224 B], H planes [3][32][224 B], D fp32 tail [32][4] (features 96..99)]
 //   W^T planes [3][100][224 B] + fp32 tail [100][4], split once per workgroup
-//   staging (4 waves): sub-tile i+1 into the free buffer while the others compute sub-tile i, i+2 in flight in
-//                 registers. Branch-free: every wave-slot is all D or all H, its per-lane global and LDS
-//                 offsets are fixed at kernel start, the loads go through buffer resources based at the
-//                 sub-tile (rows past M read 0), so a slot costs its loads, the exact split and three LDS stores.
+//   staging (4 waves): the deltas of sub-tile i+1 into the free buffer while the others compute sub-tile i, i+2 in
+//                 flight in registers (3 slots per lane on layers with a dX part, whose two single-tile dX waves
+//                 carry the last 32 items; 4 otherwise). Branch-free: per-lane global and LDS offsets fixed at kernel
+//                 start, loads through buffer resources based at the sub-tile (rows past M read 0), so a slot costs
+//                 its loads, the exact split and three LDS stores. The h rows are staged by the dX waves.
 //   dX waves (8): i-tiles {2p, 2p+1} x 16-row half h. A = W^T rows, B = D rows (ds_read_b128 of the planes);
 //                 the 4-long k tail is one exact f32 MFMA that seeds the accumulator. Epilogue: act'(h) from
-//                 the H planes (exact reconstruction h = h2 + h1 + h0), buffer stores (rows past the chunk and
-//                 columns past n_in dropped by the range check).
+//                 the fp32 h rows the wave staged itself, buffer stores (rows past the chunk and columns past n_in
+//                 dropped by the range check).
 //   dW waves (4): output row tiles x column tiles by transposed reads (k = the 32 rows of the sub-tile); db[n]
 //                 from the MFMAs through a constant-one column of H at column NI4 (exact products).
 // Deterministic: every partial slab has exactly one writer, reduced in a fixed order by k_reduce.
@@ -53,8 +54,14 @@ constexpr int BB_LDS = BB_WT + 100 * 16;               // 154880
 static_assert(BB_LDS <= 160 * 1024, "LDS");
 static_assert(BB_BUF + 2 * BB_PLANE < 65536, "LDS store offsets fit the ds_write immediate");
 constexpr int BB_THREADS = 1024;                       // 8 dX + 4 dW + 4 staging waves, 4 per SIMD
-constexpr int B2_SLOTS = 4;                            // staged D float4 per staging lane (800 per sub-tile / 256)
 constexpr int B2_HSLOTS = 2;                           // staged H float4 per dX lane (<= 32 x 28 per sub-tile / 512)
+
+// H planes: 8-B slot c4 of sub-tile row r sits at slot c4 ^ ((r >> 2) & 3) (a permutation inside each aligned group of
+// four slots). The dX waves store h in the epilogue's layout -- 16 lanes of a store group on 16 rows, one slot each --
+// and the 224-B pitch puts rows r and r + 4 on one bank (56 r mod 32 dwords): 4-way conflicts on every h store (~670
+// of the sub-tile's LDS-array cycles) without the swizzle. The transposed reads of the dW waves stay conflict free:
+// a read group's rows 4lg .. 4lg + 3 share (r >> 2) & 3 = lg, so it reads each row's 32 bytes in a permuted order.
+__device__ __forceinline__ int hslot(int r, int c4) { return c4 ^ ((r >> 2) & 3); }
 
 __device__ __forceinline__ float act_grad_bf(int act, float h) {
 #pragma clang fp contract(off)
@@ -148,6 +155,22 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         // same LDS address), so no slot is ever skipped; the offsets are constant over the sub-tiles. The h rows are
         // the dX waves' (below): split between the two roles, neither is the period's critical path alone.
         const int g = __builtin_amdgcn_readfirstlane(wave - 12);
+        // db column: H column NI4 of both buffers is the constant 1 (planes 1, 0, 0), never overwritten by the
+        // H stores (columns < NI4), so the dW MFMAs produce part[n][NI4] = sum_m D[m][n] = db[n] exactly
+        // (the products D x 1 are exact; fp32 accumulation) in the column tile that already covers it
+        {
+            const int t = tid - 768;
+            if (t < 2 * BB_SUB) {
+                unsigned char* o = smw + (t >> 5) * BB_BUF + BB_HP + (t & 31) * BB_PITCH + 8 * hslot(t & 31, NI4 >> 2);
+                *reinterpret_cast<unsigned short*>(o) = 0x3F80;
+                *reinterpret_cast<unsigned short*>(o + BB_PLANE) = 0;
+                *reinterpret_cast<unsigned short*>(o + 2 * BB_PLANE) = 0;
+            }
+        }
+        // NS = 3 slots (items 0..767) on layers with a dX part, whose two single-tile dX waves carry the last 32
+        // items (dX role); 4 (items wrapped modulo 800) on the others
+        auto stage_run = [&](auto ns_c) __attribute__((always_inline)) {
+        constexpr int B2_SLOTS = decltype(ns_c)::value;
         uint32_t voff[B2_SLOTS], loff[B2_SLOTS], toff[B2_SLOTS];
         bool tl[B2_SLOTS];
 #pragma unroll
@@ -158,18 +181,6 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             loff[v] = (uint32_t)(BB_DP + r * BB_PITCH + 8 * c4);
             tl[v] = c4 == 24;
             toff[v] = (uint32_t)(BB_DT + r * 16);
-        }
-        // db column: H column NI4 of both buffers is the constant 1 (planes 1, 0, 0), never overwritten by the
-        // H stores (columns < NI4), so the dW MFMAs produce part[n][NI4] = sum_m D[m][n] = db[n] exactly
-        // (the products D x 1 are exact; fp32 accumulation) in the column tile that already covers it
-        {
-            const int t = tid - 768;
-            if (t < 2 * BB_SUB) {
-                unsigned char* o = smw + (t >> 5) * BB_BUF + BB_HP + (t & 31) * BB_PITCH + 2 * NI4;
-                *reinterpret_cast<unsigned short*>(o) = 0x3F80;
-                *reinterpret_cast<unsigned short*>(o + BB_PLANE) = 0;
-                *reinterpret_cast<unsigned short*>(o + 2 * BB_PLANE) = 0;
-            }
         }
         // two register sets: sub-tile s is loaded into set s & 1 two sub-tiles before its store, so a load has
         // a whole sub-tile period plus the store phase to land
@@ -226,6 +237,9 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             VIHMC_BB_STAMP(i, 1)
             VIHMC_BB_STAMP(i, 2)
         }
+        };
+        if (P.has_dx) stage_run(std::integral_constant<int, 3>{});
+        else stage_run(std::integral_constant<int, 4>{});
     } else if (wave < 8) {
         // ---------------- dX role: i-tiles {2p, 2p+1} x row half h ----------------
         // The role body is instantiated per tile count (TWO) and the epilogue per activation (tanh or the rest),
@@ -249,49 +263,76 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         // time and waits in registers for the epilogue instead of being rebuilt from the three LDS planes per element
         // (5 VALU and 3 LDS reads per element less; the same h, so bitwise the same deltas). Other layers: item
         // e = tid + 512 v of the sub-tile's 32 x hq4 float4, wrapped like the staging role's.
-        uint32_t hvoff[B2_HSLOTS], hloff[B2_HSLOTS];
-#pragma unroll
-        for (int v = 0; v < B2_HSLOTS; ++v) {
-            int r, c4;
-            if (P.has_dx) {
-                r = 16 * h + lr;
-                c4 = min(4 * (t0 + v) + lg, 24);
-            } else {
-                const int e = (tid + 512 * v) % (BB_SUB * hq4);
-                r = e / hq4;
-                c4 = e - r * hq4;
-            }
-            hvoff[v] = (uint32_t)(r * P.ldh + 4 * c4) * 4u;
-            hloff[v] = (uint32_t)(BB_HP + r * BB_PITCH + 8 * c4);
-        }
         const int slast = r0 + max(nsub - 1, 0) * BB_SUB;
         auto hsub_at = [&](int k) { return min(r0 + k * BB_SUB, slast); };
-        auto hload = [&](int sub, f32x4 (&hs)[B2_HSLOTS]) __attribute__((always_inline)) {
-            const __amdgpu_buffer_rsrc_t rs = bf6::make_rsrc(H + (int64_t)sub * P.ldh, (uint32_t)((P.M - sub) * P.ldh * 4));
-#pragma unroll
-            for (int v = 0; v < B2_HSLOTS; ++v)
-                hs[v] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, hvoff[v], 0, 0));
-        };
-        auto hstore = [&](int buf, const f32x4 (&hs)[B2_HSLOTS]) __attribute__((always_inline)) {
-#pragma unroll
-            for (int v = 0; v < B2_HSLOTS; ++v) {
-                bf16x4 p0, p1, p2;
-                split4(hs[v], p0, p1, p2);
-                unsigned char* base = smw + buf * BB_BUF + hloff[v];
-                *reinterpret_cast<bf16x4*>(base) = p0;
-                *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;
-                *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;
-            }
-        };
-        auto dx_run = [&](auto two_c, auto tanh_c) __attribute__((always_inline)) {
+        auto dx_run = [&](auto dx_c, auto two_c, auto tanh_c) __attribute__((always_inline)) {
+            constexpr bool DX = decltype(dx_c)::value;
             constexpr bool TWO = decltype(two_c)::value;
             constexpr bool TANH = decltype(tanh_c)::value;
             constexpr int NU = TWO ? 2 : 1;
-            f32x4 hsa[B2_HSLOTS], hsb[B2_HSLOTS];       // per instantiation: no register set live across the dispatch
+            // The single-tile dX waves of a dX layer (i-tile 6: only lanes lg = 0 have an h item, columns 96..99) stage
+            // ONE slot: lanes lg >= 1 carry the staging role's last 32 delta items (768..799, wrapped; the staging
+            // waves then take 3 slots instead of 4 -- 1,024 staged items for 800 before)
+            constexpr bool MIX = DX && !TWO;
+            constexpr int NS = MIX ? 1 : B2_HSLOTS;
+            const bool dlane = MIX && lg != 0;
+            uint32_t hvoff[NS], hloff[NS], dvoff = bf6::OOB;
+            bool dtail = false;
+            uint32_t dtoff = 0;
+#pragma unroll
+            for (int v = 0; v < NS; ++v) {
+                int r, c4;
+                if (DX) {
+                    r = 16 * h + lr;
+                    c4 = min(4 * (t0 + v) + lg, 24);
+                } else {
+                    const int e = (tid + 512 * v) % (BB_SUB * hq4);
+                    r = e / hq4;
+                    c4 = e - r * hq4;
+                }
+                hvoff[v] = (uint32_t)(r * P.ldh + 4 * c4) * 4u;
+                hloff[v] = (uint32_t)(BB_HP + r * BB_PITCH + 8 * hslot(r, c4));
+            }
+            if (MIX) {
+                const int e = 768 + (48 * h + 16 * (lg - 1) + lr) % 32;
+                const int r = e / 25, c4 = e - r * 25;
+                if (dlane) {
+                    dvoff = (uint32_t)(r * P.ldd + 4 * c4) * 4u;
+                    hvoff[0] = bf6::OOB;
+                    hloff[0] = (uint32_t)(BB_DP + r * BB_PITCH + 8 * c4);
+                    dtail = c4 == 24;
+                    dtoff = (uint32_t)(BB_DT + r * 16);
+                }
+            }
+            auto hload = [&](int sub, f32x4 (&hs)[NS]) __attribute__((always_inline)) {
+                const __amdgpu_buffer_rsrc_t rs = bf6::make_rsrc(H + (int64_t)sub * P.ldh, (uint32_t)((P.M - sub) * P.ldh * 4));
+#pragma unroll
+                for (int v = 0; v < NS; ++v)
+                    hs[v] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, hvoff[v], 0, 0));
+                if (MIX) {
+                    // both loads by every lane, one of them out of range (reads 0, no memory traffic)
+                    const __amdgpu_buffer_rsrc_t ds = bf6::make_rsrc(D + (int64_t)sub * P.ldd, (uint32_t)((P.M - sub) * P.ldd * 4));
+                    const f32x4 dv = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ds, dvoff, 0, 0));
+                    if (dlane) hs[0] = dv;
+                }
+            };
+            auto hstore = [&](int buf, const f32x4 (&hs)[NS]) __attribute__((always_inline)) {
+#pragma unroll
+                for (int v = 0; v < NS; ++v) {
+                    bf16x4 p0, p1, p2;
+                    split4(hs[v], p0, p1, p2);
+                    unsigned char* base = smw + buf * BB_BUF + hloff[v];
+                    *reinterpret_cast<bf16x4*>(base) = p0;
+                    *reinterpret_cast<bf16x4*>(base + BB_PLANE) = p1;
+                    *reinterpret_cast<bf16x4*>(base + 2 * BB_PLANE) = p2;
+                }
+                if (MIX && dtail) *reinterpret_cast<f32x4*>(smw + buf * BB_BUF + dtoff) = hs[0];
+            };
+            f32x4 hsa[NS], hsb[NS];                    // per instantiation: no register set live across the dispatch
             f32x4 ag[NU];                              // act'(h) of the staged sub-tile (dX layers), epilogue operand
-            auto hstage = [&](int buf, const f32x4 (&hs)[B2_HSLOTS]) __attribute__((always_inline)) {
+            auto hstage = [&](int buf, const f32x4 (&hs)[NS]) __attribute__((always_inline)) {
                 hstore(buf, hs);
-                if (P.has_dx) {
+                if (DX) {
 #pragma unroll
                     for (int u = 0; u < NU; ++u)
 #pragma unroll
@@ -308,7 +349,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             float wta = 0.f, wtb = 0.f;
             auto dx_sub = [&](int i) __attribute__((always_inline)) {
                 const int sub = r0 + i * BB_SUB;
-                if (!P.has_dx) return;
+                if (!DX) return;
                 if (i == 0) {
 #pragma unroll
                     for (int kb = 0; kb < 3; ++kb)
@@ -377,13 +418,17 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 VIHMC_BB_STAMP(i, 2)
             }
         };
+        // instantiated per dX part too: with a run-time has_dx the Dout stores were conditional, so hipcc's counted
+        // wait before each h split had to assume they might be missing and also waited for the NEXT set's loads,
+        // issued half a period earlier (vmcnt(2) instead of 4: the dX waves' ~1,100-cycle split phase in the stamps)
         const bool tanh_act = P.act == ACT_TANH;
-        if (t0 + 1 < 7) {
-            if (tanh_act) dx_run(std::true_type{}, std::true_type{});
-            else dx_run(std::true_type{}, std::false_type{});
+        if (!P.has_dx) dx_run(std::false_type{}, std::true_type{}, std::true_type{});
+        else if (t0 + 1 < 7) {
+            if (tanh_act) dx_run(std::true_type{}, std::true_type{}, std::true_type{});
+            else dx_run(std::true_type{}, std::true_type{}, std::false_type{});
         } else {
-            if (tanh_act) dx_run(std::false_type{}, std::true_type{});
-            else dx_run(std::false_type{}, std::false_type{});
+            if (tanh_act) dx_run(std::true_type{}, std::false_type{}, std::true_type{});
+            else dx_run(std::true_type{}, std::false_type{}, std::false_type{});
         }
     } else {
         // ---------------- dW role: two row tiles per wave, the second over a column range ----------------
@@ -403,6 +448,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
 #pragma unroll
             for (int t = 0; t < 7; ++t) acc[s2][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         const int tro = bf6::tr_lane_off(lr, lg);
+        const int troh = (4 * lg + (lr >> 2)) * BB_PITCH + 8 * ((lr & 3) ^ lg);   // the H planes' slot swizzle (hslot)
         // instantiated for 7 column tiles (every layer but the trunk input layer) with the tile loop's reads
         // unconditional, so the next tile's H reads stay in flight under this tile's MFMAs (a run-time tile count
         // made them conditional, and hipcc then waited lgkmcnt(0) -- for the prefetch too -- before each tile)
@@ -418,14 +464,14 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 for (int p = 0; p < 3; ++p) {
                     da[0][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * rta);
                     da[1][p] = tr_frag(buf + BB_DP + p * BB_PLANE, tro, 16 * rtb);
-                    hb[0][p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 0);
+                    hb[0][p] = tr_frag(buf + BB_HP + p * BB_PLANE, troh, 0);
                 }
 #pragma unroll
                 for (int t = 0; t < 7; ++t) {
                     if (t >= nt) break;                    // wave-uniform (NT = 0 only)
                     if (t + 1 < nt) {
 #pragma unroll
-                        for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(buf + BB_HP + p * BB_PLANE, tro, 16 * (t + 1));
+                        for (int p = 0; p < 3; ++p) hb[(t + 1) & 1][p] = tr_frag(buf + BB_HP + p * BB_PLANE, troh, 16 * (t + 1));
                     }
                     acc[0][t] = six(da[0], hb[t & 1], acc[0][t]);
                     if (t >= cb0 && t < cb1) acc[1][t] = six(da[1], hb[t & 1], acc[1][t]);
