@@ -145,9 +145,9 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
         }
     }
 
-    // static wave priority: the staging waves at 1 (the youngest waves, and the critical path of the sub-tile
-    // period without it: stamps, profiles/r02p_stamps.log)
-    if (wave >= 12) __builtin_amdgcn_s_setprio(1);
+    // no static wave priority: with 3 staging slots (round 5) the staging waves are no longer the critical path, and
+    // at priority 1 (round 2, profiles/r02p_stamps.log) their split VALU held back the dX waves' epilogues: 52.5 ->
+    // 51.0 us per launch without it, the dX waves at priority 1 or the dW waves at 1 no better (profiles/r05r_ab.txt)
     if (wave >= 12) {
         // ---------------- staging role ----------------
         // wave-slot ws = 4 v + g (g = staging wave, v = slot) carries D items e = 64 ws + lane (800 of them: 32 rows x
