@@ -78,16 +78,20 @@ __device__ __forceinline__ float tanh_grad(float h) {
 
 #if BB_STAMP
 // every 16th trunk workgroup of the launches with a dX part (the last one written wins: layer 1): per wave and
-// sub-tile s_memtime at the barrier exit [0], after the staging of the next sub-tile [1], when the MFMA results
-// exist [2]; per workgroup s_memtime / s_memrealtime at start and end (scripts/diag/stamps_bwd.py)
-constexpr int BBS_WG = 16, BBS_SUB = 32;
-__device__ unsigned long long bb_stamps[BBS_WG][16][BBS_SUB][3];
+// sub-tile s_memtime at the barrier exit [0] and at the role's phase ends [1..5] (staging: stores, loads; dX: MFMAs
+// issued, epilogue stores, h stores, act', h loads; dW: fragment reads, MFMAs issued), each fenced by a scheduling
+// barrier; per workgroup s_memtime / s_memrealtime at start and end (scripts/diag/stamps_bwd.py)
+constexpr int BBS_WG = 16, BBS_SUB = 32, BBS_K = 6;
+__device__ unsigned long long bb_stamps[BBS_WG][16][BBS_SUB][BBS_K];
 __device__ unsigned long long bb_real[BBS_WG][2][2];
 #define VIHMC_BB_STAMP(I, K)                                                                                  \
-    if (samp && lane == 0 && (I) < BBS_SUB) bb_stamps[sidx][wave][(I)][(K)] = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+    if (samp && lane == 0 && (I) < BBS_SUB) bb_stamps[sidx][wave][(I)][(K)] = __builtin_amdgcn_s_memtime();   \
+    __builtin_amdgcn_sched_barrier(0);
 #else
 #define VIHMC_BB_STAMP(I, K)
 #endif
+constexpr int BBS_NONE = 1 << 20;                      // stamp index of the prologue's h stage: never recorded
 
 __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smw[];
@@ -221,14 +225,14 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             __syncthreads();                           // buffer 0 holds sub-tile i, buffer 1 is free
             VIHMC_BB_STAMP(i, 0)
             store(1, pfb);
-            load(sub_at(i + 3), pfb);
             VIHMC_BB_STAMP(i, 1)
+            load(sub_at(i + 3), pfb);
             VIHMC_BB_STAMP(i, 2)
             __syncthreads();                           // buffer 1 holds sub-tile i + 1, buffer 0 is free
             VIHMC_BB_STAMP(i + 1, 0)
             if (i + 2 < nsub) store(0, pfa);
-            load(sub_at(i + 4), pfa);
             VIHMC_BB_STAMP(i + 1, 1)
+            load(sub_at(i + 4), pfa);
             VIHMC_BB_STAMP(i + 1, 2)
         }
         if (i < nsub) {
@@ -330,19 +334,21 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
             };
             f32x4 hsa[NS], hsb[NS];                    // per instantiation: no register set live across the dispatch
             f32x4 ag[NU];                              // act'(h) of the staged sub-tile (dX layers), epilogue operand
-            auto hstage = [&](int buf, const f32x4 (&hs)[NS]) __attribute__((always_inline)) {
+            auto hstage = [&](int buf, const f32x4 (&hs)[NS], int si) __attribute__((always_inline)) {
                 hstore(buf, hs);
+                VIHMC_BB_STAMP(si, 3)
                 if (DX) {
 #pragma unroll
                     for (int u = 0; u < NU; ++u)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) ag[u][r] = TANH ? tanh_grad(hs[u][r]) : act_grad_bf(P.act, hs[u][r]);
                 }
+                VIHMC_BB_STAMP(si, 4)
             };
             if (nsub > 0) {
                 hload(hsub_at(0), hsa);
                 hload(hsub_at(1), hsb);
-                hstage(0, hsa);
+                hstage(0, hsa, BBS_NONE);
                 hload(hsub_at(2), hsa);
             }
             bf16x8 wra[3][3];                          // [kb][plane] W^T fragments of the first i-tile (registers)
@@ -394,6 +400,7 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                     for (int r = 0; r < 4; ++r) o[r] = acc[u][r] * ag[u][r];
                     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(bf6::u32x4, o), drs, off, 0, 0);
                 }
+                VIHMC_BB_STAMP(i, 2)
             };
             // unrolled by two (static register sets, every load unconditional: see the staging role)
             int i = 0;
@@ -401,21 +408,20 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 __syncthreads();                       // buffer 0 holds sub-tile i
                 VIHMC_BB_STAMP(i, 0)
                 dx_sub(i);
-                hstage(1, hsb);                        // h of sub-tile i + 1 into the free buffer (+ its act')
+                hstage(1, hsb, i);                     // h of sub-tile i + 1 into the free buffer (+ its act')
                 hload(hsub_at(i + 3), hsb);
-                VIHMC_BB_STAMP(i, 2)
+                VIHMC_BB_STAMP(i, 5)
                 __syncthreads();                       // buffer 1 holds sub-tile i + 1
                 VIHMC_BB_STAMP(i + 1, 0)
                 dx_sub(i + 1);
-                if (i + 2 < nsub) hstage(0, hsa);
+                if (i + 2 < nsub) hstage(0, hsa, i + 1);
                 hload(hsub_at(i + 4), hsa);
-                VIHMC_BB_STAMP(i + 1, 2)
+                VIHMC_BB_STAMP(i + 1, 5)
             }
             if (i < nsub) {
                 __syncthreads();
                 VIHMC_BB_STAMP(i, 0)
                 dx_sub(i);
-                VIHMC_BB_STAMP(i, 2)
             }
         };
         // instantiated per dX part too: with a run-time has_dx the Dout stores were conditional, so hipcc's counted
@@ -478,7 +484,6 @@ __global__ __launch_bounds__(BB_THREADS, 1) void k_bwd_bf2(BwdArgs args) {
                 }
 #if BB_STAMP
                 asm volatile("" :: "v"(acc[0][0]), "v"(acc[1][6]));
-                VIHMC_BB_STAMP(i, 1)
                 VIHMC_BB_STAMP(i, 2)
 #endif
             }

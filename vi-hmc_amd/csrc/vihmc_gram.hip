@@ -579,9 +579,9 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
                 const int pc = min(p, A.P - 1);
                 trow[rt] = A.timg + c * A.timg_cs + (int64_t)(pc / 32) * CONTRACT_SPLIT_BLOCK + (pc % 32) * bf6::PITCH;
             }
-            for (int e = 0; e < 4; ++e) {
-                __syncthreads();
-                bf16x8 a[2][3];
+            // the A operand of extension block e + 1 loaded under block e's products (two register sets; loaded at
+            // use, each of the four blocks waited out an L2 / HBM latency)
+            auto load_ext = [&](int e, bf16x8 (&a)[2][3]) __attribute__((always_inline)) {
 #pragma unroll
                 for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
@@ -592,7 +592,14 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
                         if (!pval[rt]) lo = bf16x4{}, hi = bf16x4{};
                         a[rt][pl] = bf6::cat8(lo, hi);
                     }
-                mma_block9(lds + ((nbm + e) % GR_NBUF) * GR_BLK, lds + GRB_P3 + e * GRAM_P3_BLOCK, tro, a, acc);
+            };
+            load_ext(0, a0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                __syncthreads();
+                if (e + 1 < 4) load_ext(e + 1, (e & 1) ? a0 : a1);
+                mma_block9(lds + ((nbm + e) % GR_NBUF) * GR_BLK, lds + GRB_P3 + e * GRAM_P3_BLOCK, tro, (e & 1) ? a1 : a0,
+                           acc);
             }
         }
     }
@@ -694,18 +701,39 @@ __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char
     const int c = u / ngroups, m = u - c * ngroups;
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    // staging: every load of a thread issued before its first LDS store (a load -> store loop waited out one L2 / HBM
+    // latency per trip: ~10 trips for the 90-KB fp64 Gt)
     const double* gt = A.gt64 + c * A.gt_cs2;
-    for (int e = tid; e < 101 * 56; e += GR_THREADS) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    constexpr int GSL = (101 * 56 + GR_THREADS - 1) / GR_THREADS;       // 10 f64x2 per thread
+    f64x2 gv[GSL];
+#pragma unroll
+    for (int k = 0; k < GSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 101 * 56 - 1);        // clamped slots rewrite the last pair
         const int v = e / 56, q = e - v * 56;
-        typedef double f64x2 __attribute__((ext_vector_type(2)));
-        *reinterpret_cast<f64x2*>(gts + v * 112 + 2 * q) = *reinterpret_cast<const f64x2*>(gt + v * 112 + 2 * q);
+        gv[k] = *reinterpret_cast<const f64x2*>(gt + v * 112 + 2 * q);
     }
     const float* zb = A.zb + c * A.zb_cs;
-    for (int e = tid; e < 32 * 101; e += GR_THREADS) {
+    constexpr int ZSL = (32 * 101 + GR_THREADS - 1) / GR_THREADS;        // 6 per thread
+    float zv[ZSL];
+#pragma unroll
+    for (int k = 0; k < ZSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 32 * 101 - 1);
         const int row = e / 101, v = e - row * 101, n = 32 * m + row;
-        float z = 0.f;
-        if (n < A.N) z = v < 100 ? zb[(int64_t)n * A.ldz + v] : 1.f;
-        zbt[v * 32 + row] = z;
+        zv[k] = v < 100 ? zb[(int64_t)min(n, A.N - 1) * A.ldz + v] : 1.f;
+        if (n >= A.N) zv[k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < GSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 101 * 56 - 1);
+        const int v = e / 56, q = e - v * 56;
+        *reinterpret_cast<f64x2*>(gts + v * 112 + 2 * q) = gv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < ZSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 32 * 101 - 1);
+        const int row = e / 101, v = e - row * 101;
+        zbt[v * 32 + row] = zv[k];
     }
     __syncthreads();
     const int n32 = 32 * m, ng = n32 / 256, w8 = (n32 % 256) / 32;
@@ -719,7 +747,17 @@ __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char
         const int rt = tile / 7, t = tile - rt * 7;
         using acc_t = std::conditional_t<GRAM_DZB_FP64 != 0, double, float>;
         acc_t ts[4] = {0, 0, 0, 0};
-        for (int ss = 0; ss < nslab; ++ss) {
+        int ss = 0;
+        for (; ss + 8 <= nslab; ss += 8) {                // eight slab loads in flight, then the adds in order
+            f32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const f32x4*>(tb + (ss + k) * sstride + tile * 256);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ts[r] += (acc_t)v[k][r];
+        }
+        for (; ss < nslab; ++ss) {
             const f32x4 v = *reinterpret_cast<const f32x4*>(tb + ss * sstride + tile * 256);
 #pragma unroll
             for (int r = 0; r < 4; ++r) ts[r] += (acc_t)v[r];
