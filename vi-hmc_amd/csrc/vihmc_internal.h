@@ -252,6 +252,10 @@ struct ReduceJob {
     // tiled = 1: the slabs hold the bf16x6 backward's dW accumulator tiles as they stand (bwd_tile_off), len = the
     // tiled slab's floats; the sums are scattered to dst = [n_out][ldi] weights + [n_out] bias (the db column NI4)
     int32_t tiled, ntj, n_out, n_in, ldi;
+    // samp != null (weight-gradient jobs of a plan that samples a subset of the parameters): samp[dst offset] = 1
+    // where the gather reads the sum (a sampled parameter); a quad of four outputs none of which is read is neither
+    // summed nor written (the slab loads are most of the reduce's bytes)
+    const uint8_t* samp;
 };
 // Tiled dW partial slab of the bf16x6 backward kernels: 16x16 tiles (row tile tn of the outputs n, column tile t of
 // the inputs j, t < ntj), lane-major float4 quads (lane l = 16 lg + lr holds rows n = 16 tn + 4 lg + r, column

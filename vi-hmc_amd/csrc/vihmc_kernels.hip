@@ -191,9 +191,34 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
         if (grouped && (int)blockIdx.x * 256 >= J.len) return;   // block-uniform
         const bool ok = 4 * q < J.len;
         if (!grouped && !ok) return;
+        // quad -> (row tile, column tile, lane) -> rows n = 16 tn + 4 lg + r, column j = 16 t + lr
+        const int f = 4 * (ok ? q : 0), big = 6 * J.ntj * 256;
+        int tn, t, lane;
+        if (f < big) {
+            const int T = f >> 8;
+            tn = T / J.ntj;
+            t = T - tn * J.ntj;
+            lane = (f & 255) >> 2;
+        } else {
+            tn = 6;
+            t = (f - big) >> 6;
+            lane = ((f - big) & 63) >> 2;
+        }
+        const int j = 16 * t + (lane & 15), ni4 = (J.n_in + 3) & ~3;
+        bool need = ok;
+        if (J.samp && ok) {
+            need = false;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int nn = 16 * tn + 4 * (lane >> 4) + r;
+                if (nn >= J.n_out) continue;
+                if (j < J.n_in) need |= J.samp[(int64_t)nn * J.ldi + j] != 0;
+                else if (j == ni4) need |= J.samp[(int64_t)J.n_out * J.ldi + nn] != 0;
+            }
+        }
         const float* sp = J.src + c * J.in_cs + (ok ? 4 * q : 0);
         const int64_t st = J.part_stride;
-        const int n = ok ? J.n_parts : 0;
+        const int n = need ? J.n_parts : 0;
         float4 s = {0.f, 0.f, 0.f, 0.f};
         if (grouped) {
             int p = g;
@@ -218,7 +243,7 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
             }
             if (g > 0) tsum[g - 1][x] = s;
             __syncthreads();
-            if (g != 0 || !ok) return;
+            if (g != 0 || !need) return;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 s.x += tsum[k][x].x;
@@ -248,20 +273,7 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
                 s.w += v.w;
             }
         }
-        // quad -> (row tile, column tile, lane) -> rows n = 16 tn + 4 lg + r, column j = 16 t + lr
-        const int f = 4 * q, big = 6 * J.ntj * 256;
-        int tn, t, lane;
-        if (f < big) {
-            const int T = f >> 8;
-            tn = T / J.ntj;
-            t = T - tn * J.ntj;
-            lane = (f & 255) >> 2;
-        } else {
-            tn = 6;
-            t = (f - big) >> 6;
-            lane = ((f - big) & 63) >> 2;
-        }
-        const int j = 16 * t + (lane & 15), ni4 = (J.n_in + 3) & ~3;
+        if (!need) return;
         float* d = J.dst + c * J.dst_cs;
         const float sv[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
@@ -284,10 +296,11 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
         if ((int)blockIdx.x * 256 >= J.len) return;   // whole block past this job (the grid fits the longest job)
         const int x = threadIdx.x & 63, g = threadIdx.x >> 6;
         const int eg = (blockIdx.x * 64 + x) * 4;
-        const bool ok = eg < J.len;
+        bool ok = eg < J.len;
+        if (J.samp && ok) ok = (J.samp[eg] | J.samp[eg + 1] | J.samp[eg + 2] | J.samp[eg + 3]) != 0;
         const float* sp = J.src + c * J.in_cs + (ok ? eg : 0);
         const int64_t st = J.part_stride;
-        const int n = ok ? J.n_parts : 0;               // lanes past the end load nothing
+        const int n = ok ? J.n_parts : 0;               // lanes past the end (or with no sampled output) load nothing
         float4 s = {0.f, 0.f, 0.f, 0.f};
         int p = g;
         for (; p + 28 < n; p += 32) {
@@ -325,6 +338,7 @@ __global__ __launch_bounds__(256) void k_reduce(const ReduceJob* jobs, int n_job
     }
     const int e = (blockIdx.x * blockDim.x + threadIdx.x) * (vec ? 4 : 1);
     if (e >= J.len) return;
+    if (J.samp && !(vec ? (J.samp[e] | J.samp[e + 1] | J.samp[e + 2] | J.samp[e + 3]) : J.samp[e])) return;
     const float* src = J.src + c * J.in_cs + e;
     const int n = J.n_parts;
     const int64_t st = J.part_stride;

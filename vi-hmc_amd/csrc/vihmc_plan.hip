@@ -170,6 +170,7 @@ struct vihmc_plan {
     ReduceJob* jobsB = nullptr;
     ReduceJob* jobsW = nullptr;      // dW partial reduces: row-major slabs (fp32 backward)
     ReduceJob* jobsWt = nullptr;     // ... tiled slabs for the layers the bf16x6 backward kernels run
+    uint8_t* gsamp = nullptr;        // [dp] 1 at the packed positions of sampled parameters (K < D only)
     int n_jobsW = 0, max_lenW = 0, lenB = 0;
 
     std::vector<int32_t> fmap_host;    // flat parameter index -> packed offset (sensitivity output map)
@@ -704,6 +705,12 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     }
     if (int rc = p->upload(&p->smap_w, sw.data(), p->K)) return rc;
     if (int rc = p->upload(&p->smap_wt, swt.data(), p->K)) return rc;
+    if (p->K < p->D) {
+        // the weight-gradient reduce sums only quads that hold a sampled parameter (bench: K = 10 % of D)
+        std::vector<uint8_t> smp((size_t)p->dp, 0);
+        for (int k = 0; k < p->K; ++k) smp[(size_t)sw[k]] = 1;
+        if (int rc = p->upload(&p->gsamp, smp.data(), p->dp)) return rc;
+    }
     if (int rc = prior_setup(p, prior_mu, prior_sd)) return rc;
 
     const int C = p->maxC;
@@ -920,6 +927,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
                 j.len = L.n_out * L.ldi + L.n_out;
                 j.dst = p->gp + L.wp;
                 j.dst_cs = p->dp;
+                j.samp = p->gsamp ? p->gsamp + L.wp : nullptr;
                 p->max_lenW = std::max(p->max_lenW, j.len);
                 jw.push_back(j);
                 if (tiled[net][li]) {
