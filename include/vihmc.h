@@ -162,6 +162,20 @@ int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, con
                      const float* g_in, float* g_out, float* logp_out, const float* eps, const float* inv_mass,
                      int L, int C, void* stream);
 
+/* DeepONet plans: one gradient evaluation of a data shard inside hamiltorch's Integrator.SPLITTING trajectory over
+ * two shards with the end gradient reused (Operator_network/HMC/main_HMC_splitting.py:361-369, config 4; the
+ * momentum / position updates of HMCRunner._trajectory around that evaluation), the updates
+ * applied in place by the evaluation's gradient gather instead of torch elementwise kernels:
+ *   mode 1: p += kick g; p += kick g; theta += drift p   (this shard's two kicks, then the drift to the next shard)
+ *   mode 2: p += kick g                                  (the trajectory's last kick)
+ * each update one fma, as torch.add(x, y, alpha=a), so the trajectory is bitwise the torch-op path. theta [C, K]
+ * and p [C, K] are device arrays updated in place (theta is also this evaluation's input). grad [C, K] receives g;
+ * logp [C] (or NULL: gradient only) the log-prob at the input theta. scatter_into (mode 1, may be NULL): the plan
+ * of the NEXT evaluation (same network layout), into whose packed weights / images the gather writes the new
+ * theta, which that evaluation then skips with scattered_in = 1. */
+int vihmc_split_step(vihmc_plan* p, float* theta, float* momentum, int C, float* grad, float* logp, int mode, float kick,
+                     float drift, vihmc_plan* scatter_into, int scattered_in, void* stream);
+
 /* Plan introspection: 0 = DeepONet, 1 = MLP; D; K; max_chains; device bytes owned. */
 /* Sensitivity scores of every parameter at theta (chain 0 of the plan, [K] device):
  *   out[d] = sigma[d]^2 * mean over outputs of (d f / d theta_d)^2,  d < D, flat (named_parameters) order.

@@ -296,11 +296,17 @@ struct ScatterArgs {
 struct LeapArgs {
     float* p;               // [C, K]
     float* th;              // [C, K]
-    const float* eps;       // [C]
-    const float* inv_mass;  // [K] or null
+    const float* eps;       // [C] (mode 0)
+    const float* inv_mass;  // [K] or null (mode 0)
     int32_t last;
     ScatterArgs sc;         // scatter the new theta (not on the last step); packed == null: the next evaluation does
     int32_t scattered_in;   // this evaluation's theta is already scattered (skip its k_scatter)
+    // mode 1 / 2: the splitting integrator's steps around one shard's gradient g (hamiltorch Integrator.SPLITTING with
+    // two shards and the reused end gradient, HMCRunner._trajectory): 1 = p += kick g twice (this shard's kick of the
+    // forward sweep and of the reverse sweep, or the reverse sweep's last kick and the next step's first), then
+    // theta += drift p; 2 = p += kick g once (the trajectory's last kick). Each update one fma, as torch.add(alpha=).
+    int32_t mode;
+    float kick, drift;
 };
 // the log-prob finalisation fused into the gradient gather (logp == null: none); cnt: [maxC] zeroed counters
 struct FinalizeArgs {

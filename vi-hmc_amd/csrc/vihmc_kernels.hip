@@ -405,7 +405,7 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp
     double lp = 0.0;
     // leapfrog step: its operands (momentum, inverse mass, the scatter's offsets) are loaded with the gather's
     float e = 0.f;
-    if (LEAP) e = lf.eps[c];
+    if (LEAP && lf.mode == 0) e = lf.eps[c];
     const bool scat = LEAP && !lf.last && lf.sc.packed != nullptr;
     for (int kb = k0 + threadIdx.x; kb < k1; kb += GATHER_U * GATHER_THREADS) {
         float thv[GATHER_U], muv[GATHER_U], ivv[GATHER_U], gpv[GATHER_U], pv[GATHER_U], imv[GATHER_U];
@@ -436,7 +436,17 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp
             // contraction pragma around them (the fused trajectory is bitwise the step-by-step path)
             const float g = __builtin_fmaf(-__fmul_rn(d, iv), inv_scale, gpv[u]);
             if (grad) grad[o] = g;
-            if (LEAP) {
+            if (LEAP && lf.mode != 0) {
+                // the splitting integrator's kicks and drift (LeapArgs.mode), one fma each as torch.add(alpha=)
+                float pn = __builtin_fmaf(lf.kick, g, pv[u]);
+                if (lf.mode == 1) {
+                    pn = __builtin_fmaf(lf.kick, g, pn);
+                    const float tn = __builtin_fmaf(lf.drift, pn, th);
+                    lf.th[o] = tn;
+                    if (scat) scatter_store(lf.sc.packed, lf.sc.dp, lf.sc.si, c, sx[u], tn);
+                }
+                lf.p[o] = pn;
+            } else if (LEAP) {
 #pragma clang fp contract(off)
                 float pn = pv[u] + e * g;
                 if (lf.last) {

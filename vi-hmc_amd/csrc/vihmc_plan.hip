@@ -1661,6 +1661,33 @@ int vihmc_grad(vihmc_plan* p, const float* theta, int C, float* grad, void* stre
     });
 }
 
+int vihmc_split_step(vihmc_plan* p, float* theta, float* momentum, int C, float* grad, float* logp, int mode, float kick,
+                     float drift, vihmc_plan* scatter_into, int scattered_in, void* stream) {
+    return guarded([&]() -> int {
+        if (!p || !theta || !momentum || !grad) return fail("null argument");
+        if (p->kind != 0) return fail("vihmc_split_step needs a DeepONet plan");
+        if (C < 1 || C > p->maxC) return fail("C must be in [1, max_chains]");
+        if (mode != 1 && mode != 2) return fail("vihmc_split_step: mode must be 1 or 2");
+        if (scatter_into && (scatter_into->kind != 0 || scatter_into->dp != p->dp || scatter_into->K != p->K ||
+                             scatter_into->maxC < C))
+            return fail("vihmc_split_step: scatter_into must be a DeepONet plan of the same layout");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        LeapArgs lf{};
+        lf.p = momentum;
+        lf.th = theta;
+        lf.mode = mode;
+        lf.kick = kick;
+        lf.drift = drift;
+        lf.scattered_in = scattered_in ? 1 : 0;
+        if (mode == 1 && scatter_into) {
+            vihmc_plan* q = scatter_into;
+            const ScatterImg si = scatter_img(q);
+            lf.sc = ScatterArgs{q->packed, q->dp, q->smap_w, q->smap_wt, q->img_by_scatter ? si : ScatterImg{}};
+        }
+        return deeponet_eval(p, theta, C, logp, grad, nullptr, s, &lf);
+    });
+}
+
 int vihmc_mlp_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, const float* p_in, float* p_out,
                          const float* g_in, float* g_out, float* logp_out, const float* eps, const float* inv_mass,
                          int L, int C, void* stream) {

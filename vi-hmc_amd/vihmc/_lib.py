@@ -62,6 +62,8 @@ SIGNATURES = {
                                      c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "vihmc_trajectory": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_int, c_int, c_void_p]),
+    "vihmc_split_step": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, ctypes.c_float,
+                                 ctypes.c_float, c_void_p, c_int, c_void_p]),
     "vihmc_sensitivity": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "vihmc_plan_set_data": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "vihmc_plan_set_trunk_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),

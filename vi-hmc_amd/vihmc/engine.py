@@ -164,6 +164,32 @@ class _Engine:
         _lib.check(rc, "vihmc_trajectory")
         return th_out, p_out, lp, g_out
 
+    def split_step(self, theta: torch.Tensor, momentum: torch.Tensor, mode: int, kick: float, drift: float = 0.0,
+                   scatter_into=None, scattered_in: bool = False, want_logp: bool = False):
+        """vihmc_split_step: this shard's gradient at theta [C, K] (a float32 device tensor updated IN PLACE, as is
+        momentum) with the splitting integrator's updates around it applied by the gradient gather -- mode 1:
+        p += kick g twice, then theta += drift p, scattered into `scatter_into`'s weights (the next shard's engine);
+        mode 2: p += kick g. Returns (logp or None, grad). Bitwise the torch.add(alpha=) sequence of
+        HMCRunner._trajectory's splitting branch."""
+        if self._sample_rng is not None:
+            raise RuntimeError("cfg.sample_data redraws the trunk rows per evaluation: use the step-by-step path")
+        if (theta.dtype != torch.float32 or not theta.is_contiguous() or theta.device != self.device
+                or tuple(theta.shape[1:]) != (self.K,)):
+            raise ValueError("theta must be a contiguous float32 [C, K] tensor on the plan's device (updated in place)")
+        if momentum.shape != theta.shape or momentum.dtype != torch.float32 or not momentum.is_contiguous() \
+                or momentum.device != self.device:
+            raise ValueError("momentum must match theta (contiguous float32, same device; updated in place)")
+        C = theta.shape[0]
+        grad = torch.empty(C, self.K, device=self.device, dtype=torch.float32)
+        lp = torch.empty(C, device=self.device, dtype=torch.float32) if want_logp else None
+        with torch.cuda.device(self.device):
+            rc = self.L.vihmc_split_step(self._plan, theta.data_ptr(), momentum.data_ptr(), C, grad.data_ptr(),
+                                         None if lp is None else lp.data_ptr(), int(mode), float(kick), float(drift),
+                                         None if scatter_into is None else scatter_into._plan, int(bool(scattered_in)),
+                                         self._stream())
+        _lib.check(rc, "vihmc_split_step")
+        return lp, grad
+
     def set_data(self, x_branch: torch.Tensor, y: torch.Tensor):
         """vihmc_plan_set_data (DeepONet): new branch rows [N, in_branch] and targets [N, P], same N / P."""
         xb = torch.as_tensor(x_branch).to(device=self.device, dtype=torch.float32).contiguous()

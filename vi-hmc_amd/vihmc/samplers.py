@@ -332,6 +332,8 @@ class HMCRunner:
             p = p - (0.5 * eps) * g_new
             return th, p, lp_new, g_new
         sub = eps / (2 * (M - 1))
+        if self._fused_split(eps):
+            return self._trajectory_split_fused(th, g, p, eps)
         g0_cached = g if self.reuse else None
         gm = lp0_end = None
         # one fused kernel per update (torch.add with alpha; eps is a host float here) instead of a scale and
@@ -364,6 +366,45 @@ class HMCRunner:
         for m in range(1, M):
             lp_sum = lp_sum + evs[m].logp(th)
         return th, p, lp_sum, gm
+
+    def _fused_split(self, eps) -> bool:
+        """The splitting trajectory with its updates inside the engines' gradient gathers (vihmc_split_step): two
+        DeepONet shards, the reused end gradient, a scalar step, no mass matrix (the torch path's own restrictions
+        for the updates it fuses); engine attribute ``fused_split = False`` turns it off."""
+        if not (self.splitting and self.M == 2 and self.reuse and self.inv_mass is None and not torch.is_tensor(eps)):
+            return False
+        if self.device.type != "cuda" or not all(isinstance(e, EngineEvaluator) for e in self.evs):
+            return False
+        from .engine import DeepONetEngine
+        return all(isinstance(e.engine, DeepONetEngine) and getattr(e.engine, "fused_split", True)
+                   and e.engine._sample_rng is None for e in self.evs)
+
+    def _trajectory_split_fused(self, th, g, p, eps):
+        """HMCRunner._trajectory's splitting branch for M = 2 with reuse, the kicks and drifts applied by the
+        evaluations' gradient gathers. The loop body there, per step: [m = 0] p += h g0; th += s p; [m = 1] g1 at th;
+        p += h g1; (reverse) [m = 1, reused] p += h g1; th += s p; [m = 0] g0 at th; p += h g0. The opening
+        p += h g; th += s p stays two torch.add; then every shard-1 evaluation applies its two kicks and the drift
+        (mode 1) and writes the new position into shard 0's weights, and every shard-0 evaluation applies its kick,
+        the next step's kick and the drift into shard 1 (mode 1), the last one only its kick (mode 2) -- the same
+        fma per update as torch.add(alpha=), so bitwise the torch-op path."""
+        ev0, ev1 = self.evs
+        e0, e1 = ev0.engine, ev1.engine
+        L, C = self.L, th.shape[0]
+        half = 0.5 * eps
+        sub = eps / 2
+        p = torch.add(p, g, alpha=half)
+        th = torch.add(th, p, alpha=sub)                 # new tensors: the caller's state stays for a rejection
+        lp0_end = g0 = None
+        for step in range(L):
+            ev1.n_grad += C
+            e1.split_step(th, p, 1, half, sub, scatter_into=e0, scattered_in=step > 0)
+            ev0.n_grad += C
+            if step == L - 1:
+                lp0_end, g0 = e0.split_step(th, p, 2, half, want_logp=True, scattered_in=True)
+            else:
+                _, g0 = e0.split_step(th, p, 1, half, sub, scatter_into=e1, scattered_in=True)
+        lp_sum = lp0_end + ev1.logp(th)
+        return th, p, lp_sum, g0
 
     def step(self):
         """One HMC iteration for every chain (hamiltorch ``sample`` loop body)."""
