@@ -927,7 +927,10 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
                 j.len = L.n_out * L.ldi + L.n_out;
                 j.dst = p->gp + L.wp;
                 j.dst_cs = p->dp;
-                j.samp = p->gsamp ? p->gsamp + L.wp : nullptr;
+                // only jobs over many slabs (one or two chains: ~160 row chunks per trunk layer) gain from skipping the
+                // unsampled quads; with a few slabs per chain (16 chains) the mask's own loads cost more than the
+                // skipped slab loads (k_reduce 22.7 -> 26.9 us per launch, profiles/r05sb_samp_ab.txt)
+                j.samp = p->gsamp && L.n_chunks >= REDUCE_GROUP_MIN ? p->gsamp + L.wp : nullptr;
                 p->max_lenW = std::max(p->max_lenW, j.len);
                 jw.push_back(j);
                 if (tiled[net][li]) {
