@@ -1319,7 +1319,11 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         stats_job.sel = 1;
         stats_job.bits = resid;
     }
-    const bool snap = !gram && guard_live(p);          // every chain computed its likelihood: a fit snapshot
+    // every chain computed its likelihood: a fit snapshot -- only while the plan runs the Gram form, its one reader (a
+    // one-chain plan's device-to-host copy cost ~4 us per evaluation, profiles/r05lt_c1_trace.txt); otherwise the
+    // history restarts, so no stale snapshot decides once the form comes on (plan options)
+    const bool snap = !gram && guard_live(p) && gram_on(p);
+    if (!gram_on(p)) p->n_snap = 0;
     if (snap) {
         stats_job.fit = p->fit_dev;
         stats_job.ysq = p->ysq_dev;
