@@ -48,8 +48,8 @@
 #define FWD_DMA_ONLY 0
 // slab count from which a reduce block's four waves split the slabs (k_reduce)
 #define REDUCE_GROUP_MIN 32
-// gradient-gather K slices per chain (16: 256 blocks at C = 16, 8.8 us)
-#define GATHER_SPLIT_N 64
+// gradient-gather K slices per chain at most (launch_gather_prior picks ~256 blocks over all chains)
+#define GATHER_SPLIT_N 256
 // the fp32-MFMA contraction (k_contract_ws + k_contract2) and fused forward forms (0: the round-1 generic kernels)
 #define VIHMC_CONTRACT_WS 1
 #define VIHMC_FUSED_FWD 1

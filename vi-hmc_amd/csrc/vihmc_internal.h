@@ -81,7 +81,7 @@ struct RowdotArgs {
 // ---------------------------------------------------------------------------------------------
 constexpr int BWD_SUB = 32;
 
-constexpr int GATHER_SPLIT_MAX = 64;
+constexpr int GATHER_SPLIT_MAX = 256;
 struct BwdProb {
     const float* D;  int64_t d_cs;  int32_t ldd;
     const float* WT; int64_t wt_cs; int32_t ldw;

@@ -476,9 +476,10 @@ __global__ __launch_bounds__(GATHER_THREADS) void k_gather_prior(const float* gp
     if (!is_last || threadIdx.x >= 64) return;
     __threadfence();
     const int lane = threadIdx.x;
-    double t = lane < (int)gridDim.x ? __hip_atomic_load(lp_part + c * gridDim.x + lane, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT)
-                                     : 0.0;
+    // lane l adds partials l, l + 64, ... in order (one term each up to 64 slices: the round-4 order), then the butterfly
+    double t = 0.0;
+    for (int i = lane; i < (int)gridDim.x; i += 64)
+        t += __hip_atomic_load(lp_part + c * gridDim.x + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
     if (lane == 0) {
@@ -978,13 +979,14 @@ hipError_t launch_gather_prior(const float* gp, int64_t gp_cs, const int32_t* sm
                                const float* prior_mu, const float* prior_inv_var, double prior_const,
                                float prior_scale, const float* lik, int C, float* logp, float* grad,
                                double* lp_part, uint32_t* fin_cnt, hipStream_t s, const LeapArgs* leap) {
-    static_assert(GATHER_SPLIT <= 64, "one lane per partial");
     // logp == null: no log-prob wanted (inner leapfrog steps); else the last block of each chain finalises it
     const FinalizeArgs fin{logp, lik, prior_const, fin_cnt};
     if (logp && !fin_cnt) return hipErrorInvalidValue;
-    // slices per chain: at least one element per thread (K / 1024) and at least ~256 blocks over all chains, at most
-    // GATHER_SPLIT (C = 16, K = 17,240: 17 slices of ~1,014 elements instead of 64 of 270 -- 3/4 of the threads idle)
-    const int split = std::min(GATHER_SPLIT, std::max({1, (K + GATHER_THREADS - 1) / GATHER_THREADS, (256 + C - 1) / C}));
+    // slices per chain: at least one element per thread (K / 1024) and ~256 blocks over all chains where each keeps
+    // >= 256 elements, at most GATHER_SPLIT (C = 16, K = 17,240: 17 slices of ~1,014 elements instead of 64 of 270 --
+    // 3/4 of the threads idle; config 4 at one chain, K = 172,401: 256 slices, every CU, instead of 64)
+    const int split = std::min(GATHER_SPLIT, std::max({1, (K + GATHER_THREADS - 1) / GATHER_THREADS,
+                                                       std::min((256 + C - 1) / C, (K + 255) / 256)}));
     if (leap)
         hipLaunchKernelGGL(k_gather_prior<true>, dim3(split, C), dim3(GATHER_THREADS), 0, s, gp, gp_cs, smap,
                            theta, K, prior_mu, prior_inv_var, prior_scale, grad, lp_part, *leap, fin);
