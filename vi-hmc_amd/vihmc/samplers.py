@@ -305,6 +305,7 @@ class HMCRunner:
                                and all(isinstance(e, EngineEvaluator) for e in self.evs))
         self._rows = torch.arange(C, device=device) * S_cap
         self.n = 0
+        self._z_ahead = None      # the next iteration's momenta, drawn while this one runs on the device
 
     def _eps(self):
         if not self.nuts:
@@ -412,7 +413,8 @@ class HMCRunner:
         if n >= self.num_samples:
             raise RuntimeError("all samples drawn")
         rng = self.rng
-        z = rng.draw_momentum()
+        z = self._z_ahead if self._z_ahead is not None else rng.draw_momentum()
+        self._z_ahead = None
         logu = None if self.strict else rng.draw_logu()
         p = z if self.mass_sqrt is None else z * self.mass_sqrt
         th, lp, g = self.cur
@@ -420,6 +422,7 @@ class HMCRunner:
             ke0 = _kinetic(p, self.inv_mass)
             th_new, p, lp_new, g_new = self._trajectory(th, g, p, self._eps())
             rho, err = self._accept_fused(n, lp, ke0, th_new, _kinetic(p, self.inv_mass), lp_new, g_new, logu)
+            self._draw_ahead(n)
             self._adapt(n, rho, err)
             self.n += 1
             return
@@ -453,8 +456,17 @@ class HMCRunner:
         self.cur = nxt
         self.accepted[:, n] = acc
         self.trace[:, n] = nxt[1]
+        self._draw_ahead(n)
         self._adapt(n, torch.where(err, torch.full_like(rho, float("nan")), rho), err)
         self.n += 1
+
+    def _draw_ahead(self, n):
+        """Iteration n + 1's momenta, drawn on the host now -- after iteration n's last draw (its accept uniform), so
+        each chain's stream keeps hamiltorch's order -- while iteration n runs on the device: config 4's 172,401 CPU
+        normals per chain otherwise left the GPU idle ~0.33 ms per iteration (profiles/r05lt_c1_trace.txt). Only for
+        the runner's private per-chain generators, and only when an iteration n + 1 exists."""
+        if self.rng.mode == "per_chain" and self.device.type == "cuda" and n + 1 < self.num_samples:
+            self._z_ahead = self.rng.draw_momentum()
 
     def _accept_fused(self, n, lp, ke0, th_new, ke1, lp_new, g_new, logu):
         """The accept block above for CUDA chains in one vihmc_hmc_accept launch (the same kinetic energies and
