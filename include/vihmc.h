@@ -137,6 +137,16 @@ int vihmc_hmc_accept(int C, int K, int n, int burn, const float* lp0, const floa
                      uint8_t* accepted, int64_t acc_ld, float* trace, int64_t tr_ld, float* rho, uint8_t* err,
                      void* stream);
 
+/* Kinetic energies ke[c] = 0.5 sum_k p[c][k] inv_mass[k] p[c][k] (inv_mass [K] device or NULL = identity) of C
+ * chains of K parameters, p [C][K] device, in ONE launch. Replaces hamiltorch's kinetic term of `hamiltonian`
+ * (0.5 p.p, or 0.5 p.(inv_mass p)) that HMCRunner computed as 0.5 * (p * p).sum(1) -- four
+ * launches. Summed in fp64 in a fixed order (slice partials, then the slices in order), rounded once to fp32.
+ * Workspace: part [C * vihmc_kinetic_slices(K)] doubles and cnt [C] uint32 ZEROED before the first call (every call
+ * leaves them zeroed again); one workspace per stream. */
+int vihmc_kinetic_slices(int K);
+int vihmc_kinetic(const float* p, const float* inv_mass, int C, int K, float* ke, double* part, uint32_t* cnt,
+                  void* stream);
+
 /* Forward only: logp [C] and the network output out [C, N, P] (DeepONet) or [C, N, out_dim] (BNN).
  * Replaces log_prob_func(..., predict=True) -> (logp, output) (main_VI_HMC_burgers.py:175-176). */
 int vihmc_forward(vihmc_plan* p, const float* theta, int C, float* logp, float* out, void* stream);

@@ -345,6 +345,11 @@ struct AcceptArgs {
     float* rho; uint8_t* err;                   // [C]: rho (NaN where the chain failed), 1 = failed
 };
 hipError_t launch_hmc_accept(const AcceptArgs& a, int C, hipStream_t s);
+// vihmc_kinetic (k_kinetic): kinetic energies of C chains; part [C][kinetic_slices(K)] fp64, cnt [C] zeroed once
+constexpr int KINETIC_MAX_SLICES = 256;
+int kinetic_slices(int K);
+hipError_t launch_kinetic(const float* p, const float* inv_mass, int C, int K, float* ke, double* part, uint32_t* cnt,
+                          hipStream_t s);
 
 struct FusedNet {
     const float* in; int64_t in_cs; int32_t ldin;   // activations feeding the first fused layer

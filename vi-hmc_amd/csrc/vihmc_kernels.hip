@@ -621,6 +621,62 @@ __global__ __launch_bounds__(256) void k_hmc_accept_chain(AcceptArgs a, int C) {
     a.trace[(int64_t)c * a.tr_ld + a.n] = lp_next;
 }
 
+// Kinetic energies 0.5 sum_k p[c][k] (m[k] p[c][k]) (m = the inverse mass, or 1) of C chains in ONE launch: grid
+// (S slices, C), each block sums its contiguous slice in fp64 (4 loads per thread in flight), fixed-order block tree;
+// the chain's last block to finish (arrival counter, reset by it) adds the S partials in order and writes the fp32
+// energy. Replaces the sampler's 0.5 * (p * p).sum(1) -- a product, a memset, a reduction and a scale, four launches
+// (~21 us at config 4's 172,401 parameters, profiles/r05lt_c1_trace.txt) -- twice per HMC iteration.
+constexpr int KIN_THREADS = 1024, KIN_U = 4;
+__global__ __launch_bounds__(KIN_THREADS) void k_kinetic(const float* p, const float* inv_mass, int K, float* ke,
+                                                         double* part, uint32_t* cnt) {
+    __shared__ double sh[KIN_THREADS / 64];
+    __shared__ int is_last;
+    const int c = blockIdx.y, S = gridDim.x;
+    const int per = (K + S - 1) / S;
+    const int k0 = blockIdx.x * per, k1 = min(K, k0 + per);
+    const float* pc = p + (int64_t)c * K;
+    double s = 0.0;
+    for (int kb = k0 + threadIdx.x; kb < k1; kb += KIN_U * KIN_THREADS) {
+        float v[KIN_U], m[KIN_U];
+#pragma unroll
+        for (int u = 0; u < KIN_U; ++u) {
+            const int k = min(kb + u * KIN_THREADS, k1 - 1);
+            v[u] = pc[k];
+            m[u] = inv_mass ? inv_mass[k] : 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < KIN_U; ++u)
+            if (kb + u * KIN_THREADS < k1) s += (double)(v[u] * (m[u] * v[u]));
+    }
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) {
+        part[(int64_t)c * S + blockIdx.x] = s;
+        __threadfence();
+        is_last = atomicAdd(cnt + c, 1u) == (uint32_t)S - 1;
+    }
+    __syncthreads();
+    if (!is_last || threadIdx.x >= 64) return;
+    __threadfence();
+    const int lane = threadIdx.x;
+    double t = 0.0;
+    for (int i = lane; i < S; i += 64)
+        t += __hip_atomic_load(part + (int64_t)c * S + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) {
+        ke[c] = (float)(0.5 * t);
+        cnt[c] = 0u;
+    }
+}
+
+int kinetic_slices(int K) { return std::max(1, std::min(KINETIC_MAX_SLICES, (K + KIN_U * KIN_THREADS - 1) / (KIN_U * KIN_THREADS))); }
+
+hipError_t launch_kinetic(const float* p, const float* inv_mass, int C, int K, float* ke, double* part, uint32_t* cnt,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(k_kinetic, dim3(kinetic_slices(K), C), dim3(KIN_THREADS), 0, s, p, inv_mass, K, ke, part, cnt);
+    return hipGetLastError();
+}
+
 hipError_t launch_hmc_accept(const AcceptArgs& a, int C, hipStream_t s) {
     hipLaunchKernelGGL(k_hmc_accept, dim3((a.K + ACC_U * 256 - 1) / (ACC_U * 256), C), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_hmc_accept_chain, dim3((C + 255) / 256), dim3(256), 0, s, a, C);

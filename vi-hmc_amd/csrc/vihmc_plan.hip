@@ -1750,6 +1750,18 @@ int vihmc_trajectory(vihmc_plan* p, const float* theta_in, float* theta_out, con
     });
 }
 
+int vihmc_kinetic_slices(int K) { return K >= 1 ? kinetic_slices(K) : -1; }
+
+int vihmc_kinetic(const float* p, const float* inv_mass, int C, int K, float* ke, double* part, uint32_t* cnt,
+                  void* stream) {
+    return guarded([&]() -> int {
+        if (C < 1 || K < 1) return fail("vihmc_kinetic: C, K >= 1");
+        if (!p || !ke || !part || !cnt) return fail("null argument");
+        HIPCHK(launch_kinetic(p, inv_mass, C, K, ke, part, cnt, static_cast<hipStream_t>(stream)));
+        return 0;
+    });
+}
+
 int vihmc_hmc_accept(int C, int K, int n, int burn, const float* lp0, const float* lp1, const float* ke0,
                      const float* ke1, const float* logu, const float* th1, const float* g1,
                      float* th_last, float* lp_last, float* g_last, float* th_bp, float* lp_bp, float* g_bp,

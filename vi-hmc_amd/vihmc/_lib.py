@@ -58,6 +58,8 @@ SIGNATURES = {
                                                                                    c_void_p, c_int64, c_void_p,
                                                                                    c_int64, c_void_p, c_void_p,
                                                                                    c_void_p]),
+    "vihmc_kinetic_slices": (c_int, [c_int]),
+    "vihmc_kinetic": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vihmc_mlp_trajectory": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_int, c_int, c_void_p]),
     "vihmc_trajectory": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -305,7 +305,35 @@ class HMCRunner:
                                and all(isinstance(e, EngineEvaluator) for e in self.evs))
         self._rows = torch.arange(C, device=device) * S_cap
         self.n = 0
+        # kinetic energies in one vihmc_kinetic launch (engine evaluators on CUDA; both accept forms use it, so they
+        # stay bitwise equal) instead of 0.5 * (p * p).sum(1)'s four; its workspace is zeroed once here
+        self._native_ke = device.type == "cuda" and all(isinstance(e, EngineEvaluator) for e in self.evs)
+        self._ke_ws = None
         self._z_ahead = None      # the next iteration's momenta, drawn while this one runs on the device
+
+    def _ke(self, p):
+        """The kinetic energy of every chain [C] (hamiltorch's 0.5 p.p, or 0.5 p.(inv_mass p))."""
+        if not self._native_ke:
+            return _kinetic(p, self.inv_mass)
+        import ctypes
+        from . import _lib
+        L = _lib.lib()
+        C, K = p.shape
+        if self._ke_ws is None:
+            S = int(L.vihmc_kinetic_slices(K))
+            self._ke_ws = (torch.zeros(C * S, dtype=torch.float64, device=self.device),
+                           torch.zeros(C, dtype=torch.int32, device=self.device))
+        part, cnt = self._ke_ws
+        p = p.to(torch.float32).contiguous()
+        im = None if self.inv_mass is None else self.inv_mass.to(torch.float32).contiguous()
+        ke = torch.empty(C, device=self.device)
+
+        def ptr(t):
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        with torch.cuda.device(self.device):
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+            _lib.check(L.vihmc_kinetic(ptr(p), ptr(im), C, K, ptr(ke), ptr(part), ptr(cnt), stream), "vihmc_kinetic")
+        return ke
 
     def _eps(self):
         if not self.nuts:
@@ -419,16 +447,16 @@ class HMCRunner:
         p = z if self.mass_sqrt is None else z * self.mass_sqrt
         th, lp, g = self.cur
         if self._accept_native:
-            ke0 = _kinetic(p, self.inv_mass)
+            ke0 = self._ke(p)
             th_new, p, lp_new, g_new = self._trajectory(th, g, p, self._eps())
-            rho, err = self._accept_fused(n, lp, ke0, th_new, _kinetic(p, self.inv_mass), lp_new, g_new, logu)
+            rho, err = self._accept_fused(n, lp, ke0, th_new, self._ke(p), lp_new, g_new, logu)
             self._draw_ahead(n)
             self._adapt(n, rho, err)
             self.n += 1
             return
-        H0 = -lp + _kinetic(p, self.inv_mass)
+        H0 = -lp + self._ke(p)
         th_new, p, lp_new, g_new = self._trajectory(th, g, p, self._eps())
-        H1 = -lp_new + _kinetic(p, self.inv_mass)
+        H1 = -lp_new + self._ke(p)
         d = H0 - H1
         rho = torch.where(torch.isnan(d), torch.zeros_like(d), torch.clamp(d, max=0.0))
         ok = torch.isfinite(lp) & torch.isfinite(lp_new)
