@@ -1,5 +1,6 @@
 """Config 4's split HMC leg with the end-point value evaluation on a side stream (HMCRunner.side_value) on and off,
-alternating: python profiles/scripts/probes/probe_side.py [reps]"""
+alternating: python profiles/scripts/probes/probe_side.py [reps]. Ran against the side-stream change that was measured
+and not kept (profiles/r05s2_side_stream_ab.txt); on the current tree both arms run the same code."""
 import json
 import os
 import sys
