@@ -172,6 +172,8 @@ struct vihmc_plan {
     ReduceJob* jobsWt = nullptr;     // ... tiled slabs for the layers the bf16x6 backward kernels run
     uint8_t* gsamp = nullptr;        // [dp] 1 at the packed positions of sampled parameters (K < D only)
     int n_jobsW = 0, max_lenW = 0, lenB = 0;
+    int spanWt = 0;                  // k_reduce grid for jobsWt in max_len units: 256 x the most x-blocks a tiled job
+                                     // uses (a tiled job over < REDUCE_GROUP_MIN slabs sums 1024 floats per block)
 
     std::vector<int32_t> fmap_host;    // flat parameter index -> packed offset (sensitivity output map)
 
@@ -942,6 +944,8 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
                     j.ldi = L.ldi;
                     p->max_lenW = std::max(p->max_lenW, j.len);
                 }
+                p->spanWt = std::max(p->spanWt, !j.tiled ? j.len
+                                                : 256 * cdiv(j.len, j.n_parts >= REDUCE_GROUP_MIN ? 256 : 1024));
                 jt.push_back(j);
             }
         }
@@ -1431,7 +1435,8 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
             }
         }
         if (bwd_stop) HIPCHK(hipEventRecord(bwd_stop, s));
-        HIPCHK(launch_reduce(p->bwd_bf16x6 ? p->jobsWt : p->jobsW, p->n_jobsW, p->max_lenW, C, s, &stats_job));
+        HIPCHK(launch_reduce(p->bwd_bf16x6 ? p->jobsWt : p->jobsW, p->n_jobsW, p->bwd_bf16x6 ? p->spanWt : p->max_lenW,
+                             C, s, &stats_job));
     }
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
                                p->lik.prior_scale, p->lik_buf, C, logp, want_grad ? grad : nullptr, p->lp_part, p->fin_cnt, s,
