@@ -172,8 +172,7 @@ struct vihmc_plan {
     ReduceJob* jobsWt = nullptr;     // ... tiled slabs for the layers the bf16x6 backward kernels run
     uint8_t* gsamp = nullptr;        // [dp] 1 at the packed positions of sampled parameters (K < D only)
     int n_jobsW = 0, max_lenW = 0, lenB = 0;
-    int spanWt = 0;                  // k_reduce grid for jobsWt in max_len units: 256 x the most x-blocks a tiled job
-                                     // uses (a tiled job over < REDUCE_GROUP_MIN slabs sums 1024 floats per block)
+    int spanA = 0, spanB = 0, spanW = 0, spanWt = 0;   // k_reduce grid extents of the job lists (reduce_span)
 
     std::vector<int32_t> fmap_host;    // flat parameter index -> packed offset (sensitivity output map)
 
@@ -625,6 +624,29 @@ GramArgs gram_args(vihmc_plan* p, int C) {
     return a;
 }
 
+// k_reduce grid extent of a job list in max_len units (grid x = span / 256): the x-blocks its jobs use. A block sums
+// 256 floats (grouped and scalar forms) or 1,024 (vector / tiled jobs below REDUCE_GROUP_MIN slabs); a grid sized by
+// the longest job's floats left up to three quarters of its blocks exiting at once (16 chains: k_reduce 22.9 -> 21.8
+// us per launch, profiles/r05s2_span_ab.txt)
+int reduce_span(const ReduceJob* jobs, int n) {
+    int span = 0;
+    for (int i = 0; i < n; ++i) {
+        const ReduceJob& J = jobs[i];
+        const bool grouped = J.n_parts >= REDUCE_GROUP_MIN;
+        int per = 256;
+        if (J.tiled) {
+            per = grouped ? 256 : 1024;
+        } else {
+            // k_reduce's own test for the float4 forms
+            const bool vec = ((J.len | J.part_stride | J.in_cs | J.dst_cs) & 3) == 0 &&
+                             ((reinterpret_cast<uintptr_t>(J.src) | reinterpret_cast<uintptr_t>(J.dst)) & 15) == 0;
+            per = vec && !grouped ? 1024 : 256;
+        }
+        span = std::max(span, 256 * cdiv(J.len, per));
+    }
+    return span;
+}
+
 int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb, const float* tf, const float* y,
                    const float* frozen, const int64_t* idx, const float* prior_mu, const float* prior_sd) {
     if (d->n_branch_layers < 1 || d->n_trunk_layers < 1) return fail("empty branch or trunk");
@@ -875,6 +897,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         jb.dst = p->nets[0].delta[0];
         jb.dst_cs = p->nets[0].delta_cs;
         p->lenB = jb.len;
+        p->spanB = reduce_span(&jb, 1);
         if (int rc = p->upload(&p->jobsB, &jb, 1)) return rc;
         if (p->qchunksA > 1) {
             ReduceJob ja{};
@@ -888,6 +911,7 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
             p->lenA = ja.len;
             // both contraction reduces in one launch (independent outputs: branch and trunk deltas)
             const ReduceJob both[2] = {jb, ja};
+            p->spanA = reduce_span(both, 2);
             if (int rc = p->upload(&p->jobsA, both, 2)) return rc;
         }
         // two job lists over the same slabs: row-major (fp32 backward) and, for the layers the bf16x6 kernels run
@@ -944,12 +968,12 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
                     j.ldi = L.ldi;
                     p->max_lenW = std::max(p->max_lenW, j.len);
                 }
-                p->spanWt = std::max(p->spanWt, !j.tiled ? j.len
-                                                : 256 * cdiv(j.len, j.n_parts >= REDUCE_GROUP_MIN ? 256 : 1024));
                 jt.push_back(j);
             }
         }
         p->n_jobsW = (int)jw.size();
+        p->spanW = reduce_span(jw.data(), (int)jw.size());
+        p->spanWt = reduce_span(jt.data(), (int)jt.size());
         if (int rc = p->upload(&p->jobsW, jw.data(), (int64_t)jw.size())) return rc;
         if (int rc = p->upload(&p->jobsWt, jt.data(), (int64_t)jt.size())) return rc;
     }
@@ -1377,8 +1401,8 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         HIPCHK(launch_contract(q, C, true, s));
         if (stop) HIPCHK(hipEventRecord(stop, s));
         const ChainBits* only = mixed ? &resid : nullptr;
-        if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 2, std::max(p->lenA, p->lenB), C, s, nullptr, only));
-        else HIPCHK(launch_reduce(p->jobsB, 1, p->lenB, C, s, nullptr, only));
+        if (p->qchunksA > 1) HIPCHK(launch_reduce(p->jobsA, 2, p->spanA, C, s, nullptr, only));
+        else HIPCHK(launch_reduce(p->jobsB, 1, p->spanB, C, s, nullptr, only));
         }
 
         // backward through both MLPs, last layer first: one fused launch per layer (branch + trunk
@@ -1435,7 +1459,7 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
             }
         }
         if (bwd_stop) HIPCHK(hipEventRecord(bwd_stop, s));
-        HIPCHK(launch_reduce(p->bwd_bf16x6 ? p->jobsWt : p->jobsW, p->n_jobsW, p->bwd_bf16x6 ? p->spanWt : p->max_lenW,
+        HIPCHK(launch_reduce(p->bwd_bf16x6 ? p->jobsWt : p->jobsW, p->n_jobsW, p->bwd_bf16x6 ? p->spanWt : p->spanW,
                              C, s, &stats_job));
     }
     HIPCHK(launch_gather_prior(p->gp, p->dp, p->smap_w, theta, p->K, p->prior_mu, p->prior_iv, p->prior_const,
