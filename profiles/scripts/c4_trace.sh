@@ -1,0 +1,10 @@
+#!/bin/bash
+# Kernel trace of config 4's split HMC leg alone, summarised per half-shard evaluation (trace_summary.py).
+TAG=${TAG:-r05c4t}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p $ROOT/gpurun_out
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $ROOT/gpurun_out/${TAG}_kt -o t -- \
+    python3 $ROOT/profiles/scripts/probes/probe_c4.py > $ROOT/gpurun_out/${TAG}_kt.log 2>&1 || exit 1
+python3 $ROOT/profiles/scripts/diag/trace_summary.py $(ls $ROOT/gpurun_out/${TAG}_kt/*kernel_trace.csv | head -1) > $ROOT/gpurun_out/${TAG}_trace.txt 2>&1
+cat $ROOT/gpurun_out/${TAG}_trace.txt; tail -1 $ROOT/gpurun_out/${TAG}_kt.log
