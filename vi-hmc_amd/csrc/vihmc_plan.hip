@@ -628,6 +628,8 @@ GramArgs gram_args(vihmc_plan* p, int C) {
 // 256 floats (grouped and scalar forms) or 1,024 (vector / tiled jobs below REDUCE_GROUP_MIN slabs); a grid sized by
 // the longest job's floats left up to three quarters of its blocks exiting at once (16 chains: k_reduce 22.9 -> 21.8
 // us per launch, profiles/r05s2_span_ab.txt)
+constexpr int CONTRACT_B_MIN_Q = 160;   // side-B trunk rows per workgroup, at least (bf16x6 k_contract_bf_b)
+
 int reduce_span(const ReduceJob* jobs, int n) {
     int span = 0;
     for (int i = 0; i < n; ++i) {
@@ -872,6 +874,10 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
         if (p->W == 100) {
             // bf16x6 side B (k_contract_bf_b, 256 owner rows, 1 workgroup per CU): ~256 workgroups
             qc = std::max(1, (int)std::lround(256.0 / ((double)C * cdiv(p->N, CONTRACT_BF_B_OWN))));
+            // at least CONTRACT_B_MIN_Q trunk rows per workgroup: below that its time is its prologue, and every further
+            // chunk adds an N x ldz partial slab to the reduce (config 4's N = 500 shards: 128 slabs of 80 rows,
+            // 28.7 MB for a 0.2-MB result)
+            qc = std::min(qc, std::max(1, cdiv(p->P, CONTRACT_B_MIN_Q)));
             qc = std::min(qc, cdiv(p->P, CONTRACT_SPLIT_ROWS));
         }
         p->qperB = (int)(((int64_t)cdiv(p->P, qc) + CONTRACT_SPLIT_ROWS - 1) / CONTRACT_SPLIT_ROWS * CONTRACT_SPLIT_ROWS);
