@@ -36,6 +36,10 @@ BOUNDS = {
     ('test_bf16x6_paths_match_fp32_mfma_paths', 'grad_relnorm'): 3e-06,   # max 6.77e-07 over 1
     ('test_bf16x6_paths_match_fp32_mfma_paths', 'logp_rel'): 2e-07,   # max 0 over 1 (floor: one fp32 ulp-level difference allowed)
     ('test_bnn_chains_gpu_vs_scalar_reference', 'pos_maxabs'): 3e-07,   # max 5.96e-08 over 3
+    # round 6 calibration (r06c): L = 196, 980 leapfrog steps per chain -- the fp32 rounding differences between the
+    # engine's and the CPU's dot products grow along the stiff BNN trajectories; accept sequences identical
+    ('test_bnn_config3_eight_chains_vs_scalar_reference', 'pos_maxabs'): 3e-03,   # max 5.93e-04 over 8 chains
+    ('test_centred_guard_protects_a_poor_centre', 'grad_relnorm'): 3e-07,   # max 5.04e-08 over 2 (r06c)
     ('test_bnn_engine_matches_golden', 'grad_elem'): 2e-06,   # max 3.13e-07 over 8
     ('test_bnn_engine_matches_golden', 'grad_relnorm'): 8e-07,   # max 1.87e-07 over 8
     ('test_bnn_engine_matches_golden', 'logp_rel'): 5e-07,   # max 1.02e-07 over 16
@@ -76,6 +80,8 @@ BOUNDS = {
     ('test_gram_grad_refshape_vs_fp64_oracle', 'grad_relnorm'): 2e-07,   # max 3.71e-08 over 4
     ('test_gram_guard_switch_per_chain', 'grad_relnorm'): 2e-07,   # max 3.82e-08 over 2
     ('test_gram_loss_forms_vs_fp64_oracle', 'grad_relnorm'): 2e-07,   # max 3.99e-08 over 8
+    ('test_good_fit_trajectory_vs_reference_sampler', 'mean_rel_l2'): 3e-06,   # max 6.67e-07 over 3 (r06b)
+    ('test_good_fit_trajectory_vs_reference_sampler', 'pos_maxabs'): 3e-08,   # max 7.45e-09 over 3 (r06b)
     ('test_gram_option_off_is_the_residual_form', 'grad_relnorm'): 3e-08,   # max 5.03e-09 over 1
     ('test_gram_trajectories_vs_reference_sampler', 'mean_rel_l2'): 3e-06,   # max 6.01e-07 over 2
     ('test_gram_trajectories_vs_reference_sampler', 'pos_maxabs'): 3e-07,   # max 5.96e-08 over 8

@@ -250,20 +250,25 @@ def test_gram_loss_forms_vs_fp64_oracle(loss, tau, cuda_device):
 FIT_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gpurun_out", "gram_fit_table.json")
 
 
-FIT_REALIZATIONS = 3
-GRAM_TOL = 2e-3      # the Gram form's gradient error above the default guard threshold (measured 7.7e-4 at fit 0.13)
+FIT_REALIZATIONS = 5
+FIT_RATIO_BAR = 2.0  # each engine form's median error <= 2x the reference's own fp32 closure's
 
 
 @pytest.mark.parametrize("noise", [1e-2, 1e-3, 1e-4, 1e-5, 1e-6])
 def test_gram_precision_vs_fit(noise, cuda_device):
-    """The Gram form's cancellation (Zb^ Gt vs y Zt^) grows with |y| / |S - y|: full Burgers shape, theta AT the
-    teacher with the frozen weights at the teacher too (mu_noise = 0), so the residual is the data noise alone
-    (sum r^2 / sum y^2 ~ noise^2 / E y^2). A flat prior (sd 1e3) leaves the likelihood gradient, whose error the
-    cancellation affects. Three thetas per fit (the teacher and two copies moved by 1e-6 relative: one fit, three
-    independent rounding realisations -- a single gradient's fp32 error is a random draw, dominated by the mean of S
-    through d/db0), each against the fp64 oracle: the engine's Gram form, its residual form, and the reference's own
-    fp32 closure (TorchDeepONetRef: the reference's torch ops on the CPU, the yardstick of VERDICT r4 item 6). Table
-    -> gpurun_out/gram_fit_table.json (profiles/r05_gram_fit_table.json)."""
+    """The gradient's fp32 error against fp64 as the fit improves: full Burgers shape, theta AT the teacher with the
+    frozen weights at the teacher too (mu_noise = 0), so the residual is the data noise alone (sum r^2 / sum y^2 ~
+    noise^2 / E y^2: 0.13 .. 1.5e-11). A flat prior (sd 1e3) leaves the likelihood gradient. Five thetas per fit (the
+    teacher and copies moved by 1e-6 relative: one fit, independent rounding realisations -- a single gradient's fp32
+    error is a random draw), each against the fp64 oracle: the engine's centred Gram form (the default), its uncentred
+    Gram form (plan option gram_center = 0), its residual form, and the reference's own fp32 closure (TorchDeepONetRef:
+    the reference's torch ops on the CPU, the yardstick). Bar: the medians of the centred Gram and the residual form
+    within FIT_RATIO_BAR of the reference's at every fit (the residual form: at fits >= 1e-5; its remaining excess is
+    the side-A contraction's S rounding at the scale of |y|, profiles/r06c_resid_parts.txt). The uncentred form's
+    cancellation (y Zt^ vs Zb^ Gt, each ~
+    sqrt(P) |y| / |S - y| larger than their difference) is recorded, not asserted. The default fit guard compares sum
+    r^2 with sum y~^2 (~1 here): the centred form runs at every fit. Table -> gpurun_out/gram_fit_table.json
+    (profiles/r06_gram_fit_table.json)."""
     from oracle.deeponet_ref import TorchDeepONetRef
     from vihmc.data import deeponet_problem
     from vihmc.engine import DeepONetEngine, trunk_features
@@ -279,28 +284,33 @@ def test_gram_precision_vs_fit(noise, cuda_device):
     eng = DeepONetEngine(spec, p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, sd, "NLL", 1.0,
                          max_chains=R, device=cuda_device)
     eng.option("gram_min_chains", 1)
-    k_default = eng.get_option("gram_guard")
-    eng.option("gram_guard", 0)                      # measure the Gram form itself at every fit
+    assert eng.get_option("gram_center") == 1 and eng.get_option("tanh_cr") == 1 and eng.get_option("gram_guard") == 1
     tt = torch.tensor(np.stack(ths), device=cuda_device)
-    gg = eng.grad(tt).cpu().numpy()
-    assert eng.get_option("gram") & 2
+    # the default plan: two log-prob evaluations give the guard its previous-but-one snapshot, then gradient-only
+    eng.logp_grad(tt)
     lp, gres = eng.logp_grad(tt)
+    gg = eng.grad(tt).cpu().numpy()
+    assert eng.get_option("gram_chains") == R, "centred: every chain's sum r^2 / sum y~^2 is ~1, far above 10^-1"
     gres = gres.cpu().numpy()
+    eng.option("gram_center", 0)
+    eng.option("gram_guard", 0)                      # the uncentred form itself at every fit
+    gu = eng.grad(tt).cpu().numpy()
+    assert eng.get_option("gram_chains") == R
+    eng.close()
     lay = deeponet_layout(spec.in_branch, spec.width_branch, spec.depth_branch, spec.in_trunk, spec.width_trunk,
                           spec.depth_trunk, spec.out)
     ref32 = TorchDeepONetRef(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, 0.0, sd, "NLL", 1.0)
-    # a second fp32 yardstick: the same closure with a correctly rounded tanh (fp64 tanh rounded to fp32) -- what an
-    # ideal fp32 implementation of the reference's ops gives; one rounding realisation differs from another by ~3x
+    # a second fp32 yardstick: the same closure with a correctly rounded tanh (fp64 tanh rounded to fp32)
     ref32cr = TorchDeepONetRef(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, 0.0, sd, "NLL", 1.0)
     ref32cr.act = lambda z: torch.tanh(z.double()).float()
-    cols = {"gram": [], "residual": [], "ref_fp32": [], "ref_fp32_cr_tanh": []}
+    cols = {"gram": [], "gram_uncentred": [], "residual": [], "ref_fp32": [], "ref_fp32_cr_tanh": []}
     fit = None
     for i, th in enumerate(ths):
         rl, rg, _ = np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, 0.0, sd, "NLL", 1.0)
-        _, g32 = ref32.logp_grad(th)
         cols["gram"].append(rel_norm(gg[i], rg))
+        cols["gram_uncentred"].append(rel_norm(gu[i], rg))
         cols["residual"].append(rel_norm(gres[i], rg))
-        cols["ref_fp32"].append(rel_norm(g32, rg))
+        cols["ref_fp32"].append(rel_norm(ref32.logp_grad(th)[1], rg))
         cols["ref_fp32_cr_tanh"].append(rel_norm(ref32cr.logp_grad(th)[1], rg))
         if i == 0:
             # fit ratio from the log-likelihood: ll = -0.5 sum r^2 (v = 1: the log v term is 0); prior part removed
@@ -310,26 +320,40 @@ def test_gram_precision_vs_fit(noise, cuda_device):
     row = {"noise": noise, "fit_ratio": fit, "realizations": R,
            **{f"{k}_relnorm": v for k, v in cols.items()}, **{f"{k}_median": v for k, v in med.items()},
            "gram_over_ref_fp32": med["gram"] / med["ref_fp32"],
+           "gram_uncentred_over_ref_fp32": med["gram_uncentred"] / med["ref_fp32"],
            "residual_over_ref_fp32": med["residual"] / med["ref_fp32"]}
     print(json.dumps(row))
     os.makedirs(os.path.dirname(FIT_TABLE), exist_ok=True)
     rows = json.load(open(FIT_TABLE)) if os.path.exists(FIT_TABLE) else []
     rows = [r for r in rows if r["noise"] != noise] + [row]
     json.dump(sorted(rows, key=lambda r: -r["noise"]), open(FIT_TABLE, "w"), indent=1)
-    # Both sides of the default guard (k = 1: the Gram form only at fits >= 0.1): above the threshold the Gram form's
-    # error stays within GRAM_TOL of the gradient norm; below it a default plan sends the chains to the residual form
-    # (decided from the previous-but-one snapshot: two log-prob evaluations first), bit for bit the residual gradient.
-    assert k_default == 1
-    eng.option("gram_guard", k_default)
-    eng.logp_grad(tt)
-    eng.logp_grad(tt)
-    g_def = eng.grad(tt)
-    if fit >= 10.0 ** -k_default:
-        assert eng.get_option("gram_chains") == R
-        assert med["gram"] <= GRAM_TOL, row
-    else:
-        assert eng.get_option("gram_chains") == 0
-        assert torch.equal(g_def.cpu(), torch.tensor(gres)), "guarded chains: the residual-form gradient"
+    assert row["gram_over_ref_fp32"] <= FIT_RATIO_BAR, row
+    if fit >= 1e-5:        # the verdict's range (fits 1e-1 .. 1e-5); below it the residual form is recorded only
+        assert row["residual_over_ref_fp32"] <= FIT_RATIO_BAR, row
+
+
+def test_centred_guard_protects_a_poor_centre(cuda_device):
+    """The centred form's terms scale with y~ = y - S0 (S0: the output at the frozen weights): with a poor centre (frozen
+    weights 0.05 N(0, 1) off the data's generator; every parameter sampled, K = D) and chains AT the generator, sum r^2 /
+    sum y~^2 ~ 1e-7 -- the centred cancellation regime -- and the default guard sends those chains to the residual
+    form, bit for bit; chains at the centre keep the Gram form."""
+    from vihmc.data import deeponet_problem
+    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.layout import DeepONetSpec
+    p = deeponet_problem(seed=5, n=64, nt=21, nx=21, noise=1e-4, mu_noise=0.05, k=None)
+    eng = DeepONetEngine(DeepONetSpec(), p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, 0.1,
+                         "NLL", 1.0, max_chains=4, device=cuda_device)
+    assert eng.get_option("gram_center") == 1 and eng.get_option("gram_guard") == 1
+    t = p.teacher[p.grad_ind].astype(np.float32)
+    m = p.mu[p.grad_ind].astype(np.float32)
+    th = torch.tensor(np.stack([t, t, m, m]), device=cuda_device)
+    _, g_res = eng.logp_grad(th)
+    eng.logp_grad(th)
+    g = eng.grad(th)
+    assert eng.get_option("gram_chains") == 2
+    assert torch.equal(g[:2], g_res[:2]), "guarded chains: the residual-form gradient"
+    for i in (2, 3):
+        parity.check("grad_relnorm", rel_norm(g[i].cpu().numpy(), g_res[i].cpu().numpy()), f"Gram chain {i}")
 
 
 def _teacher_problem():
@@ -339,12 +363,14 @@ def _teacher_problem():
     return deeponet_problem(seed=5, n=64, nt=21, nx=21, noise=1e-6, mu_noise=0.0)
 
 
-def _guard_engine(p, C, dev, k=6):
-    """The guard mechanism tests run threshold 10^-6 (the teacher chains below it, the perturbed ones above)."""
+def _guard_engine(p, C, dev, k=6, center=0):
+    """The guard mechanism tests run threshold 10^-6 (the teacher chains below it, the perturbed ones above) on the
+    uncentred form, whose fit scale is sum y^2 (centred, the teacher chains' sum r^2 / sum y~^2 is ~1: y~ is the noise)."""
     from vihmc.engine import DeepONetEngine, trunk_features
     from vihmc.layout import DeepONetSpec
     eng = DeepONetEngine(DeepONetSpec(), p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, 0.1,
                          "NLL", 1.0, max_chains=C, device=dev)
+    eng.option("gram_center", center)
     eng.option("gram_guard", k)
     return eng
 

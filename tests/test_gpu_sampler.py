@@ -54,6 +54,46 @@ def test_bnn_chains_gpu_vs_scalar_reference(cuda_device):
     _compare(res, fn, th0, seeds, 15, 10, 5e-4, burn=2)
 
 
+def test_bnn_config3_eight_chains_vs_scalar_reference(cuda_device):
+    """Config 3's per-GPU geometry (BASELINE.json: 64 BNN chains over 8 GPUs = 8 chains per plan; Neural_network/VI_HMC/
+    main_VI_HMC.py:458-460 runs its chains one after the other): an 8-chain plan on the fused trajectory kernel
+    (k_mlp_traj_bnn, one wave per chain) at the reference's L = 196, eps = 5e-4, 8 seeds, 6 samples with one burn-in
+    iteration, each chain against the scalar hamiltorch restatement with the reference's torch log-prob: identical
+    accept sequences, positions within the recorded bound. Seeds 100..112 minus 101 (its sample 2 decision lies 0.004
+    from the uniform: below MARGIN_FLOOR) and 108..111 (all-accept duplicates), chosen on the CPU oracle alone."""
+    from vihmc.engine import MLPEngine
+    from vihmc.samplers import ChainRNG, EngineEvaluator, run_chains
+    c = bnn_case("bnn_vi_hmc")
+    g = c.g
+    C = 8
+    eng = MLPEngine(c.spec, c.data["x_train"], c.data["y_train"], g["mu"], c.idx, c.prior_mu, c.prior_sd, c.loss,
+                    c.tau_out, max_chains=C, device=cuda_device)
+    ev = EngineEvaluator(eng)
+    assert ev.fused_trajectory and eng.get_option("mlp_fast")
+    th0 = torch.tensor(c.thetas[0])
+    seeds = [100, 102, 103, 104, 105, 106, 107, 112]
+    res = run_chains(ev, th0[None].repeat(C, 1), 6, 196, 5e-4, burn=1, rng=ChainRNG(C, th0.numel(), cuda_device,
+                                                                                    seeds=seeds))
+    fn = TorchBNNRef(mlp_layout(), c.data["x_train"], c.data["y_train"], g["mu"], c.idx,
+                     prior_list=list(g["prior_var"]), loss=c.loss, tau_out=c.tau_out).log_prob
+    # 980 leapfrog steps per chain: the fp32 rounding differences between the engine's and the CPU's dot products grow
+    # along the trajectory (the BNN likelihood's precision 400 makes it stiff), so the positions carry their own bound;
+    # the accept decisions must agree exactly
+    drift = []
+    for ci, sd in enumerate(seeds):
+        out, st = HR.sample(fn, th0, 6, 196, 5e-4, burn=1, generator=torch.Generator().manual_seed(sd),
+                            return_stats=True)
+        margin = min(abs(a - b) for a, b in zip(st["rhos"], st["logus"]))
+        assert margin > MARGIN_FLOOR, f"seed {sd}: a borderline accept decision ({margin:.2e})"
+        assert res.accepted[ci].cpu().tolist() == st["accepts"], (ci, sd)
+        mine = [t.cpu() for t in res.chain(ci)]
+        assert len(mine) == len(out)
+        drift.append(max(float((a - b).abs().max()) for a, b in zip(mine, out)))
+    print("position drift per chain:", [f"{d:.2e}" for d in drift])
+    parity.check("pos_maxabs", max(drift), f"8 chains x 6 samples x L = 196")
+    assert 0 < float(res.accepted.float().mean()) < 1
+
+
 def test_deeponet_chains_gpu_vs_scalar_reference(cuda_device):
     from vihmc.engine import DeepONetEngine, trunk_features
     from vihmc.samplers import ChainRNG, EngineEvaluator, run_chains

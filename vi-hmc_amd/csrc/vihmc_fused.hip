@@ -40,6 +40,7 @@ __device__ __forceinline__ float tanh_f(float x) { return tanh_acc(x); }
 template <int ACT>
 __device__ __forceinline__ float act_t(float z) {
     if constexpr (ACT == ACT_TANH) return (FWD_ABL & 2) ? z : tanh_f(z);
+    else if constexpr (ACT == ACT_TANH_CR) return (FWD_ABL & 2) ? z : tanh_cr(z);   // each net's last hidden layer
     else if constexpr (ACT == ACT_RELU) return fmaxf(z, 0.f);
     else return z;
 }
@@ -187,6 +188,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd_fused(FusedArgs args) {
         float4 h6;
         const int act = N.act[j];
         if (act == ACT_TANH) fused_layer<ACT_TANH>(wb, a, atl, lr, lg, orsrc, ooff, na, h6);
+        else if (act == ACT_TANH_CR) fused_layer<ACT_TANH_CR>(wb, a, atl, lr, lg, orsrc, ooff, na, h6);
         else if (act == ACT_RELU) fused_layer<ACT_RELU>(wb, a, atl, lr, lg, orsrc, ooff, na, h6);
         else fused_layer<ACT_ID>(wb, a, atl, lr, lg, orsrc, ooff, na, h6);
         VIHMC_FW_STORE((j + 1) & 1)
@@ -407,6 +409,7 @@ constexpr int IN0_KMAX = 111;                       // 6 full 16-long k blocks +
 __host__ __device__ constexpr int in0_ldw(int k4) { return k4 + ((24 - (k4 & 15)) & 15); }   // rowdot_ldb
 __device__ __forceinline__ float in0_act(int act, float z) {
     if (act == ACT_TANH) return tanh_f(z);
+    if (act == ACT_TANH_CR) return tanh_cr(z);
     if (act == ACT_RELU) return fmaxf(z, 0.f);
     return z;
 }
@@ -669,6 +672,7 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
             const float* wtail = reinterpret_cast<const float*>(bbuf + FWD_WTAIL);
             const float h6f = h[6].x;
             if (act == ACT_TANH) tf_layer<ACT_TANH>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, hoffj, h);
+            else if (act == ACT_TANH_CR) tf_layer<ACT_TANH_CR>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, hoffj, h);
             else if (act == ACT_RELU) tf_layer<ACT_RELU>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, hoffj, h);
             else tf_layer<ACT_ID>(wb, bias, wtail, hp, h6f, lr, lg, orsrc, hoffj, h);
 #if FWD_STAMP
@@ -679,6 +683,7 @@ __global__ __launch_bounds__((NW + ND) * 64, 1) void k_fwd_fused_bf(FusedArgs ar
             bf16x4 h6[3];
             bf_split_operand(h, hp, h6);
             if (act == ACT_TANH) bf_layer<ACT_TANH>(wb, bias, hp, h6, lr, lg, orsrc, hoffj, h);
+            else if (act == ACT_TANH_CR) bf_layer<ACT_TANH_CR>(wb, bias, hp, h6, lr, lg, orsrc, hoffj, h);
             else if (act == ACT_RELU) bf_layer<ACT_RELU>(wb, bias, hp, h6, lr, lg, orsrc, hoffj, h);
             else bf_layer<ACT_ID>(wb, bias, hp, h6, lr, lg, orsrc, hoffj, h);
         }

@@ -56,6 +56,14 @@ static_assert(GRB_LDS <= 160 * 1024, "k_gram_b LDS");
 static_assert(GRAM_P3_BLOCK % 1024 == 0, "whole DMA pieces");
 constexpr int GR_CW = 8;                                  // compute waves (32 rows each)
 constexpr int GR_THREADS = 64 * (GR_CW + 1);              // + one DMA wave
+// centred form (GramArgs::center): k_gram_a's Gram units stream the output image AND the centre's image (ring slots
+// of two blocks); k_gram_b runs 8 extension blocks (-Gb, then -Hb) and its dZb units stage Gt (fp64), Ht (fp32),
+// dB^T and B0^T
+constexpr int GR_LDS_C = GR_NBUF * 2 * GR_BLK;            // 126 KB
+constexpr int GRB_LDS_TC = GR_LDS + 8 * GRAM_P3_BLOCK;    // 120.5 KB
+constexpr int GRB_DZBC = 101 * 112 * 8 + 101 * 112 * 4 + 2 * 101 * 32 * 4;   // 161,600 B
+constexpr int GRB_LDS_C = GRB_LDS_TC > GRB_DZBC ? GRB_LDS_TC : GRB_DZBC;
+static_assert(GR_LDS_C <= 160 * 1024 && GRB_LDS_C <= 160 * 1024, "centred Gram LDS");
 
 // position of k (0..31) inside a 32-long block of the A images: lane group lg holds k = 4lg..4lg+3, 16+4lg..+3
 __host__ __device__ inline int kpos(int k) { return k < 16 ? 8 * (k >> 2) + (k & 3) : 8 * ((k - 16) >> 2) + 4 + (k & 3); }
@@ -93,6 +101,49 @@ __device__ __forceinline__ void dma_role(unsigned char* lds, int lane, int nb, F
 __device__ __forceinline__ void load_b(const unsigned char* buf, int tro, int t, bf16x8 (&b)[3]) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) b[pl] = bf6::tr_frag(buf + pl * GR_PL, tro, 16 * t);
+}
+
+// the centred Gram units' DMA wave: block i of the output image (s0) and of the centre's image (s1) into ring slot
+// i % 3 (two blocks, 42 one-KB pieces), the order and counted waits of dma_role
+__device__ __forceinline__ void dma_role2(unsigned char* lds, int lane, int nb, const unsigned char* s0,
+                                          const unsigned char* s1) {
+    auto issue = [&](int i) __attribute__((always_inline)) {
+        const unsigned char* a = s0 + (int64_t)i * CONTRACT_SPLIT_BLOCK;
+        const unsigned char* b = s1 + (int64_t)i * CONTRACT_SPLIT_BLOCK;
+        unsigned char* d = lds + (i % GR_NBUF) * 2 * GR_BLK;
+        for (int k = 0; k < GR_PIECES; ++k) bf6::glds16_asm(a + k * 1024 + lane * 16, d + k * 1024);
+        for (int k = 0; k < GR_PIECES; ++k) bf6::glds16_asm(b + k * 1024 + lane * 16, d + GR_BLK + k * 1024);
+    };
+    if (nb > 0) issue(0);
+    if (nb > 1) issue(1);
+    if (nb > 1) asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int i = 0; i < nb; ++i) {
+        __syncthreads();
+        if (i + 2 < nb) {
+            issue(i + 2);
+            asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+}
+
+// fp32 value of three exact bf16 planes ((x0 + x1) + x2 is exact: the partial sums are x rounded to 16 / 24 bits)
+__device__ __forceinline__ float unsplit(__bf16 a, __bf16 b, __bf16 c) { return ((float)a + (float)b) + (float)c; }
+
+// d = z - r of two pre-split fragments: one rounded fp32 subtraction, then the exact three-way split
+__device__ __forceinline__ void delta_frag(const bf16x8 (&z)[3], const bf16x8 (&r)[3], bf16x8 (&d)[3]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = unsplit(z[0][j], z[1][j], z[2][j]) - unsplit(r[0][j], r[1][j], r[2][j]);
+        const __bf16 a = (__bf16)x;
+        const float rr = x - (float)a;
+        const __bf16 b = (__bf16)rr;
+        d[0][j] = a;
+        d[1][j] = b;
+        d[2][j] = (__bf16)(rr - (float)b);
+    }
 }
 
 #if GR_STAMP
@@ -267,13 +318,62 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         gr_real[gr_sidx][0][1] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
+    const bool cgram = A.center && kind != 0;             // centred Gram unit: G and H over the slab
     if (wave == GR_CW) {
+        if (cgram) {
+            const unsigned char* ref = (kind == 2 ? A.cbimg : A.ctimg) + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
+            dma_role2(lds, lane, nb, src0, ref);
+        } else {
 #if GR_STAMP
         dma_role(lds, lane, nb, [&](int i) { return src0 + (int64_t)i * CONTRACT_SPLIT_BLOCK; },
                  [&](int i, int k) { GR_ST(i, k) });
 #else
         dma_role(lds, lane, nb, [&](int i) { return src0 + (int64_t)i * CONTRACT_SPLIT_BLOCK; });
 #endif
+        }
+    } else if (cgram) {
+        // ---------------- centred Gram unit (c, s): G = Z^T Z (28 upper tiles) and H = dZ^T Z (49 tiles) ----------
+        // over the slab's blocks of one side (kind 1: Z = Zt^, dZ = Zt^ - T0; kind 2: Z = Zb^, dZ = Zb^ - B0). Compute
+        // wave vt < 7 owns row tile vt: H (vt, 0..6) and G (vt, vt..6), sharing each column fragment; its dZ fragment
+        // is formed once per block from the two images' planes (delta_frag). fp32 MFMA accumulation over the slab
+        // (in the centred form both matrices multiply residual-sized operands), fp64 across the slabs (k_gram_sum).
+        const int vt = wave;
+        f32x4 hacc[7], gacc[7];
+#pragma unroll
+        for (int t = 0; t < 7; ++t) hacc[t] = gacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < nb; ++i) {
+            __syncthreads();
+            if (vt < 7) {
+                const unsigned char* zbuf = lds + (i % GR_NBUF) * 2 * GR_BLK;
+                bf16x8 za[3], ra[3], da[3];
+                load_b(zbuf, tro, vt, za);
+                load_b(zbuf + GR_BLK, tro, vt, ra);
+                delta_frag(za, ra, da);
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    bf16x8 b[3];
+                    load_b(zbuf, tro, t, b);
+                    hacc[t] = six(da, b, hacc[t]);
+                    if (t >= vt) gacc[t] = six(za, b, gacc[t]);
+                }
+            }
+        }
+        if (vt < 7) {
+            float* hp = (kind == 1 ? A.ht_part + c * A.ht_cs : A.hb_part + c * A.hb_cs) +
+                        ((int64_t)s * 49 + vt * 7) * 256 + 4 * lane;
+#pragma unroll
+            for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(hp + t * 256) = hacc[t];
+            // G (vt, t >= vt) at its index in the row-major upper-triangle list (k_gram_sum's decode)
+            double* gp = (kind == 1 ? A.gt_part + c * A.gt_cs : A.gb_part + c * A.gb_cs) + (int64_t)s * 28 * 256 +
+                         4 * lane;
+            const int j0 = 7 * vt - vt * (vt - 1) / 2 - vt;
+#pragma unroll
+            for (int t = 0; t < 7; ++t)
+                if (t >= vt) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) gp[(j0 + t) * 256 + r] = (double)gacc[t][r];
+                }
+        }
     } else if (kind == 0) {
         // ---------------- T_b = y Zt^ (A = YA rows, 16-B loads one block ahead in two register sets) ----------
         const int n0 = 256 * ng + 32 * wave;
@@ -419,12 +519,52 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
 // different product orders (not bitwise equal), and mirroring there made two threads write one element with different
 // values -- the nondeterminism of profiles/r04e_nondet.txt / r04j_nondet3.txt (one element of Gt, then dZb).
 // ---------------------------------------------------------------------------------------------------------------
+// -Gb / -Hb pre-split from an fp64 sum into FOUR bf16 planes (~32 significant bits): element (v, x) -> extension block
+// v / 32, row v % 32, feature x; planes 0..2 in the block image, plane 3 in the P3 image
+__device__ __forceinline__ void put4(unsigned char* img, unsigned char* p3, int vv, int xx, double val) {
+    double rr = val;
+    __bf16 pl[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        pl[k] = (__bf16)(float)rr;         // rr -> fp32 -> bf16: the fp32 step is exact for k >= 1 (|rr| small)
+        rr -= (double)(float)pl[k];
+    }
+    unsigned char* q = img + (vv / 32) * CONTRACT_SPLIT_BLOCK + (vv % 32) * bf6::PITCH + 2 * xx;
+    *reinterpret_cast<__bf16*>(q) = pl[0];
+    *reinterpret_cast<__bf16*>(q + GR_PL) = pl[1];
+    *reinterpret_cast<__bf16*>(q + 2 * GR_PL) = pl[2];
+    *reinterpret_cast<__bf16*>(p3 + (vv / 32) * GRAM_P3_BLOCK + (vv % 32) * bf6::PITCH + 2 * xx) = pl[3];
+}
+
 __global__ __launch_bounds__(256) void k_gram_sum(GramArgs A) {
     const int x0 = blockIdx.x, c = blockIdx.y;
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
+    const int nh = A.center ? 98 : 0;                     // centred: 49 Ht tiles, then 49 Hb tiles
+    if (x0 >= 56 && x0 < 56 + nh) {
+        // H tile: fixed-order fp64 sum of the fp32 slab partials; Ht -> fp32 [112][112] (the dZb epilogue), -Hb -> the
+        // 4-plane B blocks of k_gram_b's second extension set; the column sums of the exact d ll / d b0:
+        // Ht[v][101] = sum_p dT[p][v], Hb[v][100] = sum_n dB[n][v]
+        const bool hb = x0 - 56 >= 49;
+        const int tile = (x0 - 56) % 49, vt = tile / 7, t = tile % 7;
+        const int l = threadIdx.x >> 2, r = threadIdx.x & 3;
+        const float* part = (hb ? A.hb_part + c * A.hb_cs : A.ht_part + c * A.ht_cs) + tile * 256 + threadIdx.x;
+        const int ns = hb ? A.Sb : A.St;
+        double sum = 0.0;
+#pragma unroll 16
+        for (int ss = 0; ss < ns; ++ss) sum += (double)part[(int64_t)ss * 49 * 256];
+        const int v = 16 * vt + 4 * (l >> 4) + r, x = 16 * t + (l & 15);
+        if (!hb) {
+            A.ht[c * A.gt_cs2 + v * 112 + x] = (float)sum;
+            if (x == 101) A.gcol[c * A.gcol_cs + 3 * 112 + v] = sum;
+        } else {
+            put4(A.hbimg + c * A.gbimg_cs, A.hb3img + c * 4 * GRAM_P3_BLOCK, v, x, -sum);
+            if (x == 100) A.gcol[c * A.gcol_cs + 2 * 112 + v] = sum;
+        }
+        return;
+    }
     if (x0 >= 56) {
         const int64_t sstride = (int64_t)A.NG * GR_CW * 14 * 256;
-        const int64_t e = ((int64_t)(x0 - 56) * 256 + threadIdx.x) * 4;
+        const int64_t e = ((int64_t)(x0 - 56 - nh) * 256 + threadIdx.x) * 4;
         const float* src = A.tb_part + c * A.tb_cs + e;
         double v[4] = {0.0, 0.0, 0.0, 0.0};               // fp64 over the slabs, one rounding at the end
 #pragma unroll 16
@@ -466,23 +606,8 @@ __global__ __launch_bounds__(256) void k_gram_sum(GramArgs A) {
     // Element (v, x) -> extension block v / 32, row v % 32, feature x; planes 0..2 in the block image, plane 3 in gb3img
     unsigned char* gbi = A.gbimg + c * A.gbimg_cs;
     unsigned char* gb3 = A.gb3img + c * 4 * GRAM_P3_BLOCK;
-    const double val = -sum;
-    auto put = [&](int vv, int xx) __attribute__((always_inline)) {
-        double rr = val;
-        __bf16 pl[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            pl[k] = (__bf16)(float)rr;         // rr -> fp32 -> bf16: the fp32 step is exact for k >= 1 (|rr| small)
-            rr -= (double)(float)pl[k];
-        }
-        unsigned char* q = gbi + (vv / 32) * CONTRACT_SPLIT_BLOCK + (vv % 32) * bf6::PITCH + 2 * xx;
-        *reinterpret_cast<__bf16*>(q) = pl[0];
-        *reinterpret_cast<__bf16*>(q + GR_PL) = pl[1];
-        *reinterpret_cast<__bf16*>(q + 2 * GR_PL) = pl[2];
-        *reinterpret_cast<__bf16*>(gb3 + (vv / 32) * GRAM_P3_BLOCK + (vv % 32) * bf6::PITCH + 2 * xx) = pl[3];
-    };
-    put(v, x);
-    if (vt != t) put(x, v);
+    put4(gbi, gb3, v, x, -sum);
+    if (vt != t) put4(gbi, gb3, x, v, -sum);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -494,9 +619,11 @@ __global__ __launch_bounds__(256) void k_gram_sum(GramArgs A) {
 // d ll / d b0 slot (pt * 8 + w) of the chain.
 // ---------------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char* lds);
+__device__ __forceinline__ void dzb_unit_c(const GramArgs& A, int u, unsigned char* lds);
 __device__ __forceinline__ void gram_tt_epilogue(const GramArgs& A, int c, int pt, int wave, int lane,
                                                  const f32x4 (&acc)[2][7]);
 
+template <int CEN>
 __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     int list, u;
@@ -505,7 +632,8 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     unit_of(blockIdx.x, A.upx_b, A.PT * A.SB * A.C, A.C * ((A.N + 31) / 32), list, u, false);
     if (list < 0) return;
     if (list == 1) {                   // the dZb epilogue units fill the tail of the T_t rounds (k_gram_a is done)
-        dzb_unit(A, u, lds);
+        if (CEN) dzb_unit_c(A, u, lds);
+        else dzb_unit(A, u, lds);
         return;
     }
     // T_t unit (pt, sb, c): chains minor, so the chains sharing one YB slab (rows, k range) run on one XCD
@@ -515,21 +643,30 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int kb0 = sb * A.SLB;
     const int nbm = min(A.SLB, A.nblkN - kb0);            // this split's branch blocks (>= 1: SB = cdiv(nblkN, SLB))
-    const bool ext = sb == A.SB - 1;                      // the last split also runs the 4 extension blocks
-    const int nb = nbm + (ext ? 4 : 0);
+    const bool ext = sb == A.SB - 1;                      // the last split also runs the extension blocks
+    const int next = CEN ? 8 : 4;                         // centred: -Gb (A = dT rows), then -Hb (A = T0 rows)
+    const int nb = nbm + (ext ? next : 0);
     const int p0 = 256 * pt + 32 * wave;
     f32x4 acc[2][7];
     if (wave == GR_CW) {
         const unsigned char* bsrc = A.bimg + c * A.bimg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
         const unsigned char* gsrc = A.gbimg + c * A.gbimg_cs;
+        const unsigned char* hsrc = CEN ? A.hbimg + c * A.gbimg_cs : nullptr;
         if (ext) {
-            // the 4th -Gb planes of the 4 extension blocks, first: dma_role's counted waits retire them with block 0
+            // the 4th planes of the extension blocks, first: dma_role's counted waits retire them with block 0
             const unsigned char* p3 = A.gb3img + c * 4 * GRAM_P3_BLOCK;
             for (int k = 0; k < 4 * GRAM_P3_BLOCK / 1024; ++k)
                 bf6::glds16_asm(p3 + k * 1024 + lane * 16, lds + GRB_P3 + k * 1024);
+            if (CEN) {
+                const unsigned char* h3 = A.hb3img + c * 4 * GRAM_P3_BLOCK;
+                for (int k = 0; k < 4 * GRAM_P3_BLOCK / 1024; ++k)
+                    bf6::glds16_asm(h3 + k * 1024 + lane * 16, lds + GRB_P3 + 4 * GRAM_P3_BLOCK + k * 1024);
+            }
         }
         dma_role(lds, lane, nb, [&](int i) {
-            return i < nbm ? bsrc + (int64_t)i * CONTRACT_SPLIT_BLOCK : gsrc + (int64_t)(i - nbm) * CONTRACT_SPLIT_BLOCK;
+            return i < nbm ? bsrc + (int64_t)i * CONTRACT_SPLIT_BLOCK
+                           : (i - nbm < 4 ? gsrc + (int64_t)(i - nbm) * CONTRACT_SPLIT_BLOCK
+                                          : hsrc + (int64_t)(i - nbm - 4) * CONTRACT_SPLIT_BLOCK);
         });
     } else {
         const int tro = bf6::tr_lane_off(lr, lg);
@@ -567,7 +704,62 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
             step(i + 1, a1, a0);
         }
         if (i < nbm) step(i, a0, a1);
-        if (ext) {
+        if (CEN && ext) {
+            // centred extension: acc -= dT Gb (blocks 0..3, B = -Gb) and acc -= T0 Hb (blocks 4..7, B = -Hb). A lane (lr,
+            // lg) = row p, features 32f + 4lg + j (j < 4) and 32f + 16 + 4lg + j - 4 (j >= 4) of dT = Zt^ - T0 (formed
+            // from the two images' planes: exact fp32 values, one rounded subtraction, an exact re-split) or of T0;
+            // rows past P read 0
+            const unsigned char* trow[2];
+            const unsigned char* crow[2];
+            bool pval[2];
+#pragma unroll
+            for (int rt = 0; rt < 2; ++rt) {
+                const int p = p0 + 16 * rt + lr;
+                pval[rt] = p < A.P;
+                const int pc = min(p, A.P - 1);
+                const int64_t off = (int64_t)(pc / 32) * CONTRACT_SPLIT_BLOCK + (pc % 32) * bf6::PITCH;
+                trow[rt] = A.timg + c * A.timg_cs + off;
+                crow[rt] = A.ctimg + off;
+            }
+            auto load_ext_c = [&](int e, bf16x8 (&a)[2][3]) __attribute__((always_inline)) {
+                const int f = e & 3;
+#pragma unroll
+                for (int rt = 0; rt < 2; ++rt) {
+                    bf16x4 lo[3], hi[3], clo[3], chi[3];
+#pragma unroll
+                    for (int pl = 0; pl < 3; ++pl) {
+                        const int q = pl * GR_PL + 2 * (32 * f + 4 * lg);
+                        clo[pl] = *reinterpret_cast<const bf16x4*>(crow[rt] + q);
+                        chi[pl] = f < 3 ? *reinterpret_cast<const bf16x4*>(crow[rt] + q + 32) : bf16x4{};
+                        if (e < 4) {
+                            lo[pl] = *reinterpret_cast<const bf16x4*>(trow[rt] + q);
+                            hi[pl] = f < 3 ? *reinterpret_cast<const bf16x4*>(trow[rt] + q + 32) : bf16x4{};
+                        }
+                    }
+                    if (e < 4) {
+                        const bf16x8 z[3] = {bf6::cat8(lo[0], hi[0]), bf6::cat8(lo[1], hi[1]), bf6::cat8(lo[2], hi[2])};
+                        const bf16x8 r[3] = {bf6::cat8(clo[0], chi[0]), bf6::cat8(clo[1], chi[1]),
+                                             bf6::cat8(clo[2], chi[2])};
+                        delta_frag(z, r, a[rt]);
+                    } else {
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) a[rt][pl] = bf6::cat8(clo[pl], chi[pl]);
+                    }
+                    if (!pval[rt]) {
+#pragma unroll
+                        for (int pl = 0; pl < 3; ++pl) a[rt][pl] = bf16x8{};
+                    }
+                }
+            };
+            load_ext_c(0, a0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                __syncthreads();
+                if (e + 1 < 8) load_ext_c(e + 1, (e & 1) ? a0 : a1);
+                mma_block9(lds + ((nbm + e) % GR_NBUF) * GR_BLK, lds + GRB_P3 + e * GRAM_P3_BLOCK, tro, (e & 1) ? a1 : a0,
+                           acc);
+            }
+        } else if (ext) {
             // extension: acc -= Zt^ Gb (B blocks hold -Gb); A lane (lr, lg) = Zt^[p][32e + 4lg + j] (j < 4) and
             // [32e + 16 + 4lg + j - 4] (j >= 4), two 8-B loads per plane from the trunk image row; rows past P read 0
             const unsigned char* trow[2];
@@ -648,8 +840,16 @@ __device__ __forceinline__ void gram_tt_epilogue(const GramArgs& A, int c, int p
         if (pt == 0 && wave == 0) {
             const double* col = A.gcol + c * A.gcol_cs;
             double ss = 0.0;
-            for (int v = 0; v <= 100; ++v) ss = fma(col[v], col[112 + v], ss);
-            db = (double)A.gscale * (ss - *A.ysum);
+            if (A.center) {
+                // centred: sum (S + b0 - y) = sum_v (sum_n dB[n][v]) (sum_p Zt^[p][v]) + (sum_n B0[n][v]) (sum_p dT[p][v])
+                // - sum y~, every term of the residual's size
+                for (int v = 0; v <= 100; ++v) ss = fma(col[2 * 112 + v], col[112 + v], ss);
+                for (int v = 0; v <= 100; ++v) ss = fma(A.ccol[v], col[3 * 112 + v], ss);
+                db = (double)A.gscale * (ss - *A.cysum);
+            } else {
+                for (int v = 0; v <= 100; ++v) ss = fma(col[v], col[112 + v], ss);
+                db = (double)A.gscale * (ss - *A.ysum);
+            }
         }
         st[0] = 0.0;
         st[1] = db;
@@ -780,6 +980,115 @@ __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char
     }
 }
 
+// Centred dZb epilogue unit (c, 32-row group m): dZb[n][x] = gscale (sum_v dB[n][v] Gt[v][x] + B0[n][v] Ht[v][x]
+// - sum_s T~_b[s][n][x]), dB = Zb^ - B0 (column 100: 1 - 1 = 0, B0[n][100] = 1), the T_b slabs over y~. LDS: Gt fp64
+// [101][112], Ht fp32 [101][112], dB^T and B0^T [101][32] fp32; the sums in fp64 as dzb_unit's.
+__device__ __forceinline__ void dzb_unit_c(const GramArgs& A, int u, unsigned char* lds) {
+    double* gts = reinterpret_cast<double*>(lds);
+    float* hts = reinterpret_cast<float*>(gts + 101 * 112);
+    float* dbt = hts + 101 * 112;
+    float* b0t = dbt + 101 * 32;
+    const int ngroups = (A.N + 31) / 32;
+    const int c = u / ngroups, m = u - c * ngroups;
+    if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const double* gt = A.gt64 + c * A.gt_cs2;
+    const float* ht = A.ht + c * A.gt_cs2;
+    constexpr int GSL = (101 * 56 + GR_THREADS - 1) / GR_THREADS;       // f64x2 of Gt per thread
+    constexpr int HSL = (101 * 28 + GR_THREADS - 1) / GR_THREADS;       // f32x4 of Ht per thread
+    constexpr int ZSL = (32 * 101 + GR_THREADS - 1) / GR_THREADS;
+    f64x2 gv[GSL];
+    f32x4 hv[HSL];
+#pragma unroll
+    for (int k = 0; k < GSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 101 * 56 - 1);
+        const int v = e / 56, q = e - v * 56;
+        gv[k] = *reinterpret_cast<const f64x2*>(gt + v * 112 + 2 * q);
+    }
+#pragma unroll
+    for (int k = 0; k < HSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 101 * 28 - 1);
+        const int v = e / 28, q = e - v * 28;
+        hv[k] = *reinterpret_cast<const f32x4*>(ht + v * 112 + 4 * q);
+    }
+    const float* zb = A.zb + c * A.zb_cs;
+    float dv[ZSL], bv[ZSL];
+#pragma unroll
+    for (int k = 0; k < ZSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 32 * 101 - 1);
+        const int row = e / 101, v = e - row * 101, n = 32 * m + row;
+        const int64_t o = (int64_t)min(n, A.N - 1) * A.ldz + min(v, 99);
+        const float z = zb[o], b0 = A.cb0[o];
+        dv[k] = v < 100 ? z - b0 : 0.f;
+        bv[k] = v < 100 ? b0 : 1.f;
+        if (n >= A.N) dv[k] = bv[k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < GSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 101 * 56 - 1);
+        const int v = e / 56, q = e - v * 56;
+        *reinterpret_cast<f64x2*>(gts + v * 112 + 2 * q) = gv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < HSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 101 * 28 - 1);
+        const int v = e / 28, q = e - v * 28;
+        *reinterpret_cast<f32x4*>(hts + v * 112 + 4 * q) = hv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < ZSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 32 * 101 - 1);
+        const int row = e / 101, v = e - row * 101;
+        dbt[v * 32 + row] = dv[k];
+        b0t[v * 32 + row] = bv[k];
+    }
+    __syncthreads();
+    const int n32 = 32 * m, ng = n32 / 256, w8 = (n32 % 256) / 32;
+    const bool pre = A.tb_sum != nullptr;
+    const float* tb = (pre ? A.tb_sum + c * A.tbs_cs : A.tb_part + c * A.tb_cs) +
+                      ((int64_t)(ng * GR_CW + w8) * 14) * 256 + 4 * lane;
+    const int64_t sstride = (int64_t)A.NG * GR_CW * 14 * 256;
+    const int nslab = pre ? 1 : A.S;
+    float* out = A.dzb + c * A.dzb_cs;
+    for (int tile = wv; tile < 14; tile += GR_THREADS / 64) {
+        const int rt = tile / 7, t = tile - rt * 7;
+        double ts[4] = {0, 0, 0, 0};
+        int ss = 0;
+        for (; ss + 8 <= nslab; ss += 8) {
+            f32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const f32x4*>(tb + (ss + k) * sstride + tile * 256);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) ts[r] += (double)v[k][r];
+        }
+        for (; ss < nslab; ++ss) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(tb + ss * sstride + tile * 256);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ts[r] += (double)v[r];
+        }
+        double gz[4] = {0, 0, 0, 0};
+        const int x = 16 * t + lr;
+        for (int v = 0; v < 101; ++v) {
+            const f32x4 d = *reinterpret_cast<const f32x4*>(dbt + v * 32 + 16 * rt + 4 * lg);
+            const f32x4 b = *reinterpret_cast<const f32x4*>(b0t + v * 32 + 16 * rt + 4 * lg);
+            const double g = gts[v * 112 + x];
+            const double h = (double)hts[v * 112 + x];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gz[r] = fma((double)d[r], g, fma((double)b[r], h, gz[r]));
+        }
+        if (x < 100) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = n32 + 16 * rt + 4 * lg + r;
+                if (n < A.N) out[(int64_t)n * A.ldz + x] = (float)((double)A.gscale * (gz[r] - ts[r]));
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // Pre-split data images (once per plan / data change): YA = y [n][p] (k = p blocks in kpos order), YB = y^T [p][n]
 // (k = n blocks). Padding rows / columns stay zero (the plan zeroes the allocation).
@@ -802,6 +1111,66 @@ __global__ __launch_bounds__(256) void k_gram_yimg(const float* y, int N, int P,
     yb[ib] = a;
     yb[ib + yb_plane] = b;
     yb[ib + 2 * yb_plane] = cc;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Centred data (once per plan / data change, gram_center): yc[n][p] = y[n][p] - (sum_v B0[n][v] T0[p][v] + b0), the
+// products and sums in fp64 (exact products of fp32 values), rounded once; 64 x 64 output tiles, B0 / T0 rows staged
+// in LDS. Block (0, 0) also writes col[v] = sum_n B0[n][v] in fp64 (v < W), col[W] = N.
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_center_y(const float* y, const float* B0, const float* T0, const float* b0p, int N,
+                                                  int P, int W, int ldz, float* yc, double* col) {
+    __shared__ float bs[64][101];
+    __shared__ float ts[64][101];
+    const int p0 = blockIdx.x * 64, n0 = blockIdx.y * 64, tid = threadIdx.x;
+    for (int e = tid; e < 64 * W; e += 256) {
+        const int r = e / W, v = e - r * W;
+        bs[r][v] = n0 + r < N ? B0[(int64_t)(n0 + r) * ldz + v] : 0.f;
+        ts[r][v] = p0 + r < P ? T0[(int64_t)(p0 + r) * ldz + v] : 0.f;
+    }
+    __syncthreads();
+    const int tx = tid & 15, ty = tid >> 4;                  // 4 x 4 outputs: n = n0 + ty + 16 i, p = p0 + tx + 16 j
+    double acc[4][4] = {};
+    for (int v = 0; v < W; ++v) {
+        double a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = bs[ty + 16 * i][v], b[i] = ts[tx + 16 * i][v];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
+    }
+    const double bb = (double)*b0p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + ty + 16 * i, p = p0 + tx + 16 * j;
+            if (n < N && p < P) {
+                const int64_t e = (int64_t)n * P + p;
+                yc[e] = (float)((double)y[e] - (acc[i][j] + bb));
+            }
+        }
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid <= W) {
+        double sum = 0.0;
+        if (tid < W)
+            for (int n = 0; n < N; ++n) sum += (double)B0[(int64_t)n * ldz + tid];
+        else sum = (double)N;
+        col[tid] = sum;
+    }
+}
+
+hipError_t launch_center_y(const float* y, const float* B0, const float* T0, const float* b0, int N, int P, int W,
+                           int ldz, float* yc, double* col, hipStream_t s) {
+    if (W < 1 || W > 101 || W >= 112) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_center_y, dim3((P + 63) / 64, (N + 63) / 64), dim3(256), 0, s, y, B0, T0, b0, N, P, W, ldz, yc,
+                       col);
+    return hipGetLastError();
+}
+
+hipError_t launch_gram_aug(const GramArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld, __bf16* yb,
@@ -834,9 +1203,13 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     if (a.Sb < 1 || a.SLb < 1 || a.Sb * a.SLb < a.nblkN || (a.Sb - 1) * a.SLb >= a.nblkN || !a.gb_part)
         return hipErrorInvalidValue;
     if (a.S > GRAM_TB_DIRECT ? !a.tb_sum : a.tb_sum != nullptr) return hipErrorInvalidValue;
+    if (a.center && (!a.cbimg || !a.ctimg || !a.cb0 || !a.ccol || !a.cysum || !a.ht_part || !a.hb_part || !a.ht ||
+                     !a.hbimg || !a.hb3img))
+        return hipErrorInvalidValue;
     // the T_b units take the Gram-t tiles (one per wave) when a slab has >= 4 of them (>= 32 waves for 28 tiles);
-    // fewer n groups keep the Gram-t units (two or four tiles per T_b wave spill registers)
-    const int gt = a.NG >= 4 ? 1 : 0;
+    // fewer n groups keep the Gram-t units (two or four tiles per T_b wave spill registers). Centred: the Gram units
+    // stream the centre's image beside the outputs' and compute G with H (Gram-t units of their own)
+    const int gt = a.NG >= 4 && !a.center ? 1 : 0;
     const int n1 = a.NG * a.S * a.C, n2 = a.C * ((gt ? 0 : a.St) + a.Sb);
     a.upx_a = (n1 + 7) / 8;
     const int gpx = (n2 + 7) / 8;
@@ -845,9 +1218,10 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     if (!a.aug_done) hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
     const dim3 ga(8 * (a.upx_a + gpx));
     if (gt) hipLaunchKernelGGL(k_gram_a<1>, ga, dim3(GR_THREADS), GR_LDS, s, a);
-    else hipLaunchKernelGGL(k_gram_a<0>, ga, dim3(GR_THREADS), GR_LDS, s, a);
-    hipLaunchKernelGGL(k_gram_sum, dim3(56 + (a.tb_sum ? a.NG * 28 : 0), a.C), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_gram_b, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GRB_LDS, s, a);
+    else hipLaunchKernelGGL(k_gram_a<0>, ga, dim3(GR_THREADS), a.center ? GR_LDS_C : GR_LDS, s, a);
+    hipLaunchKernelGGL(k_gram_sum, dim3(56 + (a.center ? 98 : 0) + (a.tb_sum ? a.NG * 28 : 0), a.C), dim3(256), 0, s, a);
+    if (a.center) hipLaunchKernelGGL(k_gram_b<1>, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GRB_LDS_C, s, a);
+    else hipLaunchKernelGGL(k_gram_b<0>, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GRB_LDS, s, a);
     if (a.SB > 1) hipLaunchKernelGGL(k_gram_tt, dim3(a.PT * GR_CW, a.C), dim3(64), 0, s, a);
     return hipGetLastError();
 }

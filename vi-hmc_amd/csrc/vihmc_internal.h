@@ -30,6 +30,43 @@ __device__ __forceinline__ float tanh_acc(float x) {
     const float big = copysignf(fmaf(-2.f, t * __builtin_amdgcn_rcpf(1.f + t), 1.f), x);
     return ax < 0.625f ? small : big;
 }
+// tanh correctly rounded to fp32 (all but ~1 in 10^6 arguments, where the fp64 value lies within 2^-44 of a rounding
+// midpoint): tanh(a) = em / (em + 2), em = expm1(2a) evaluated in fp64 (Cody-Waite reduction 2a = k ln2 + r,
+// |r| <= ln2 / 2, expm1(r) to r^11, 2^k expm1(r) + (2^k - 1)), the quotient from v_rcp_f64 with one correction. The
+// epilogue of each net's LAST hidden layer (plan option tanh_cr, round 6): the output layer is linear, so that layer's
+// rounding reaches Z, and through the N x P contraction S - y, without an averaging nonlinearity in between -- and
+// tanh_acc's rounding, although unbiased over [-inf, inf], is a smooth function of the argument, so over a smooth grid of
+// 10^4 trunk points its local bias adds up coherently: the reference's fp32 closure with tanh_acc in that one layer
+// has 3.4x its gradient error against fp64 at fit 1.5e-3, with tanh_acc in the other seven layers 1.0x
+// (profiles/r06_tanh_layers.txt). ~25 fp64 instructions.
+__device__ __forceinline__ float tanh_cr(float x) {
+    const double a = fmin(fabs((double)x), 20.0);
+    const double u = 2.0 * a;
+    const double k = __builtin_rint(u * 1.4426950408889634);
+    double r = fma(-k, 6.93147180369123816490e-01, u);      // ln2_hi (32 significant bits: k ln2_hi exact)
+    r = fma(-k, 1.90821492927058770002e-10, r);             // ln2_lo
+    double p = 2.505210838544172e-08;                       // 1/11!
+    p = fma(p, r, 2.755731922398589e-07);
+    p = fma(p, r, 2.7557319223985893e-06);
+    p = fma(p, r, 2.48015873015873e-05);
+    p = fma(p, r, 1.984126984126984e-04);
+    p = fma(p, r, 1.388888888888889e-03);
+    p = fma(p, r, 8.333333333333333e-03);
+    p = fma(p, r, 4.1666666666666664e-02);
+    p = fma(p, r, 1.6666666666666666e-01);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    const double s = __builtin_ldexp(1.0, (int)k);
+    const double em = fma(s, p * r, s - 1.0);
+    const double den = em + 2.0;
+    const double rc = __builtin_amdgcn_rcp(den);
+    const double y0 = em * rc;
+    const double y = fma(fma(-y0, den, em), rc, y0);
+    return copysignf((float)y, x);
+}
+// forward-epilogue activation code of a layer whose tanh is tanh_cr (the plans set it on each net's last hidden layer;
+// the backward treats it as ACT_TANH)
+enum { ACT_TANH_CR = 4 };
 enum { MODE_FWD = 0, MODE_BWD = 1 };
 
 // contraction geometry (vihmc_contract.hip): 4 waves x 32 owner rows per workgroup, 16-row Q chunks
@@ -204,10 +241,32 @@ struct GramArgs {
     int32_t aug_done;                                      // feature 100 of both images already written
     float gscale;
     int32_t sel; ChainBits bits;                           // sel = 1: chains whose bit is set exit (residual form)
+    // Centred data (plan option gram_center, round 6): y = S0 + y~ with S0 = B0 T0^T the output at the plan's centre
+    // weights (the frozen vector); ya / yb then hold y~, and with dB = Zb^ - B0, dT = Zt^ - T0
+    //     dZb^ = gscale (dB Gt + B0 Ht - y~ Zt^),   Ht = dT^T Zt^
+    //     dZt^ = gscale (dT Gb + T0 Hb - y~^T Zb^), Hb = dB^T Zb^
+    // every term of the size of the residual, not of y. center = 0: the uncentred form above.
+    int32_t center;
+    const unsigned char* cbimg;                            // B0 pre-split image (one chain's qsplitA layout)
+    const unsigned char* ctimg;                            // T0 pre-split image (one chain's qsplitB layout)
+    const float* cb0;                                      // B0 fp32 rows [N][ldz]
+    const double* ccol;                                    // [112] sum_n B0[n][v] (fp64)
+    const double* cysum;                                   // sum y~ (fp64)
+    float* ht_part; int64_t ht_cs;                         // [C][St][49 tiles][256] Ht slabs (fp32 per slab)
+    float* hb_part; int64_t hb_cs;                         // [C][Sb][49 tiles][256] Hb slabs
+    float* ht;                                             // [C][112][112] Ht (fp32, gt_cs2)
+    unsigned char* hbimg;                                  // [C][4 blocks] -Hb pre-split (gbimg_cs)
+    unsigned char* hb3img;                                 // [C][4][GRAM_P3_BLOCK]: 4th bf16 plane of -Hb
 };
 constexpr int GRAM_P3_BLOCK = 32 * 224;   // bytes of one 32-row plane of a pre-split block (the 4th plane of -Gb)
 constexpr int GRAM_TB_DIRECT = 8;   // up to this many T_b slabs the dZb epilogue units sum them themselves
 hipError_t launch_gram(const GramArgs& a, hipStream_t s);
+// feature 100 (and trunk feature 101) of the pre-split output images of a.C chains (k_gram_aug)
+hipError_t launch_gram_aug(const GramArgs& a, hipStream_t s);
+// the centred data y~ = y - (B0 T0^T + b0) in fp64, rounded once (B0 [N][ldz], T0 [P][ldz] fp32 rows, b0 at *b0),
+// and col[v] = sum_n B0[n][v] (v < W; col[W] = N) in fp64
+hipError_t launch_center_y(const float* y, const float* B0, const float* T0, const float* b0, int N, int P, int W,
+                           int ldz, float* yc, double* col, hipStream_t s);
 hipError_t launch_gram_yimg(const float* y, int N, int P, __bf16* ya, int64_t ya_plane, int ya_ld, __bf16* yb,
                             int64_t yb_plane, int yb_ld, hipStream_t s);
 

@@ -17,12 +17,13 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ float act_apply_l(int act, float z) {
     if (act == ACT_TANH) return tanh_acc(z);
+    if (act == ACT_TANH_CR) return tanh_cr(z);
     if (act == ACT_RELU) return fmaxf(z, 0.f);
     return z;
 }
 
 __device__ __forceinline__ float act_grad_from_out_l(int act, float h) {
-    if (act == ACT_TANH) return 1.f - h * h;
+    if (act == ACT_TANH || act == ACT_TANH_CR) return 1.f - h * h;
     if (act == ACT_RELU) return h > 0.f ? 1.f : 0.f;
     return 1.f;
 }

@@ -237,6 +237,33 @@ struct vihmc_plan {
     unsigned char* ggb3 = nullptr;  // [C][4 blocks][32][112] bf16: the 4th plane of -Gb (k_gram_b extension blocks)
     double* gstats = nullptr;
     int64_t gstats_cs = 0;
+    // Centred data (plan option gram_center, default 1; round 6): the Gram form runs on y~ = y - S0, S0 =
+    // B0 T0^T + b0 the network output at the centre weights (the frozen vector, chain 0's packed weights at creation),
+    // so its two data products scale with the residual, not with y. Built lazily (ensure_centre) before the first
+    // evaluation that needs it after creation / a data change, on chain 0's slot with its state saved around it.
+    int gram_center = 1;
+    bool centre_stale = true;
+    int tanh_cr = 1;                  // plan option: each net's last hidden layer with the correctly rounded tanh_cr
+    int debug_dz = 0;                 // plan option (diagnostics): keep each evaluation's dZ_b / dZ_t
+    float* dzb_snap = nullptr;
+    float* dzt_snap = nullptr;
+    unsigned char* cimgB = nullptr;   // B0 pre-split image (qsplitA_cs bytes)
+    unsigned char* cimgT = nullptr;   // T0 pre-split image (qsplitB_cs bytes)
+    float* cB0 = nullptr;             // B0 fp32 rows [N][ldz]
+    double* ccol = nullptr;           // [112] sum_n B0[n][v]
+    double* cysq = nullptr;           // [sum y~^2, sum y~] (the fit guard's scale when centred; d ll / d b0)
+    float* cpk = nullptr;             // the centre's packed weights (dp floats)
+    unsigned char* cwimg = nullptr;   // ... its forward weight images (wimg_cs bytes, when kept by the scatter)
+    unsigned char* cwtimg = nullptr;  // ... its backward W^T images (wtimg_cs bytes)
+    float* save_pk = nullptr;         // chain 0's state while the centre is evaluated on its slot
+    unsigned char* save_wimg = nullptr;
+    unsigned char* save_wtimg = nullptr;
+    float* ght_part = nullptr;        // [C][St][49][256] Ht slabs
+    float* ghb_part = nullptr;        // [C][Sb][49][256] Hb slabs
+    int64_t ght_cs = 0, ghb_cs = 0;
+    float* ght = nullptr;             // [C][112][112] Ht
+    unsigned char* ghb = nullptr;     // [C][4 blocks] -Hb pre-split
+    unsigned char* ghb3 = nullptr;    // [C][4][GRAM_P3_BLOCK] its 4th plane
     bool last_gram = false;       // the last gradient evaluation ran the Gram form (get_option gram: bit 1)
     int last_gram_chains = 0;     // ... for this many of its chains (get_option gram_chains)
     int64_t n_grad_calls = 0;     // DeepONet gradient evaluations (calls) since creation / reset (get_option grad_evals)
@@ -499,19 +526,90 @@ int gram_setup(vihmc_plan* p, int C) {
     if (int rc = p->alloc(&p->fit_dev, C)) return rc;
     if (int rc = p->alloc(&p->ysq_dev, 2)) return rc;           // sum y^2, sum y
     if (int rc = p->alloc(&p->ysq_part, 2 * YSQ_PARTS)) return rc;
-    if (int rc = p->alloc(&p->gcol, 2 * 112 * (int64_t)C)) return rc;
+    if (int rc = p->alloc(&p->gcol, 4 * 112 * (int64_t)C)) return rc;
+    // centred form: the centre's images / rows and column sums, the H slabs and sums, chain 0's save area
+    if (int rc = p->alloc(&p->cimgB, p->qsplitA_cs)) return rc;
+    if (int rc = p->alloc(&p->cimgT, p->qsplitB_cs)) return rc;
+    if (int rc = p->alloc(&p->cB0, (int64_t)p->N * p->ldz)) return rc;
+    if (int rc = p->alloc(&p->ccol, 112)) return rc;
+    if (int rc = p->alloc(&p->cysq, 2)) return rc;
+    p->ght_cs = (int64_t)p->gSt * 49 * 256;
+    p->ghb_cs = (int64_t)p->gSb * 49 * 256;
+    if (int rc = p->alloc(&p->ght_part, p->ght_cs * C)) return rc;
+    if (int rc = p->alloc(&p->ghb_part, p->ghb_cs * C)) return rc;
+    if (int rc = p->alloc(&p->ght, (int64_t)112 * 112 * C)) return rc;
+    if (int rc = p->alloc(&p->ghb, (int64_t)4 * CONTRACT_SPLIT_BLOCK * C)) return rc;
+    if (int rc = p->alloc(&p->ghb3, (int64_t)4 * GRAM_P3_BLOCK * C)) return rc;
     HIPCHK(hipHostMalloc((void**)&p->fit_host, sizeof(float) * 2 * (size_t)C));
     for (auto& e : p->fit_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     p->gram_alloc = true;
     return 0;
 }
 
-// data images + the fit guard's sum y^2, whenever the plan's data change (the guard's history starts over)
+// data images + the fit guard's sum y^2, whenever the plan's data change (the guard's history starts over). Centred
+// (gram_center): the images hold y~ and are built with the centre by ensure_centre, before the next evaluation that
+// can use them.
 int gram_images(vihmc_plan* p, hipStream_t s) {
     if (!p->gram_alloc) return 0;
-    HIPCHK(launch_gram_yimg(p->y, p->N, p->P, p->gya, p->gya_plane, p->gya_ld, p->gyb, p->gyb_plane, p->gyb_ld, s));
     HIPCHK(launch_ysq(p->y, (int64_t)p->N * p->P, p->ysq_part, p->ysq_dev, s));
     p->n_snap = 0;
+    p->centre_stale = true;
+    if (!p->gram_center)
+        HIPCHK(launch_gram_yimg(p->y, p->N, p->P, p->gya, p->gya_plane, p->gya_ld, p->gyb, p->gyb_plane, p->gyb_ld, s));
+    return 0;
+}
+
+int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img, bool gram_only);
+
+// The centre of the centred Gram form: the network output at the centre weights (cpk, the frozen vector) evaluated on
+// chain 0's slot -- its packed weights and weight images saved and restored around it, so a state the previous
+// gather scattered there survives -- then y~ = y - S0 (fp64, k_center_y) into the G^T scratch, the data images of y~,
+// sum y~^2 / sum y~. Called at the start of an evaluation (nothing of it has run yet), outside graph capture.
+int ensure_centre(vihmc_plan* p, hipStream_t s) {
+    if (!p->gram_alloc || !p->gram_center || !p->centre_stale || !p->cpk) return 0;
+    const size_t pkb = sizeof(float) * (size_t)p->dp;
+    const bool wi = p->img_by_scatter && p->wimg && p->cwimg;
+    const bool wt = p->img_by_scatter && p->wtimg && p->cwtimg;
+    HIPCHK(hipMemcpyAsync(p->save_pk, p->packed, pkb, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(p->packed, p->cpk, pkb, hipMemcpyDeviceToDevice, s));
+    if (wi) {
+        HIPCHK(hipMemcpyAsync(p->save_wimg, p->wimg, (size_t)p->wimg_cs, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(p->wimg, p->cwimg, (size_t)p->wimg_cs, hipMemcpyDeviceToDevice, s));
+    }
+    if (wt) {
+        HIPCHK(hipMemcpyAsync(p->save_wtimg, p->wtimg, (size_t)p->wtimg_cs, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(p->wtimg, p->cwtimg, (size_t)p->wtimg_cs, hipMemcpyDeviceToDevice, s));
+    }
+    p->img_by_fwd = false;
+    if (int rc = deeponet_forward_layers(p, 1, s, true, false)) return rc;
+    Net& b = p->nets[0];
+    Net& t = p->nets[1];
+    if (!p->img_by_fwd) {
+        HIPCHK(launch_split_blocks(b.act + b.h_off.back(), b.act_cs, p->ldz, p->N, p->qsplitA, p->qsplitA_cs, 1, s));
+        HIPCHK(launch_split_blocks(t.act + t.h_off.back(), t.act_cs, p->ldz, p->P, p->qsplitB, p->qsplitB_cs, 1, s));
+        GramArgs ga{};
+        ga.bimg = p->qsplitA;
+        ga.timg = p->qsplitB;
+        ga.b0 = p->packed;
+        ga.N = p->N;
+        ga.P = p->P;
+        ga.C = 1;
+        HIPCHK(launch_gram_aug(ga, s));
+    }
+    p->img_by_fwd = false;
+    HIPCHK(hipMemcpyAsync(p->cimgB, p->qsplitA, (size_t)p->qsplitA_cs, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(p->cimgT, p->qsplitB, (size_t)p->qsplitB_cs, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(p->cB0, b.act + b.h_off.back(), sizeof(float) * (size_t)p->N * p->ldz,
+                          hipMemcpyDeviceToDevice, s));
+    float* yc = p->gT;                                    // scratch: G^T of chain 0 (>= N P floats)
+    HIPCHK(launch_center_y(p->y, p->cB0, t.act + t.h_off.back(), p->cpk, p->N, p->P, p->W, p->ldz, yc, p->ccol, s));
+    HIPCHK(launch_gram_yimg(yc, p->N, p->P, p->gya, p->gya_plane, p->gya_ld, p->gyb, p->gyb_plane, p->gyb_ld, s));
+    HIPCHK(launch_ysq(yc, (int64_t)p->N * p->P, p->ysq_part, p->cysq, s));
+    HIPCHK(hipMemcpyAsync(p->packed, p->save_pk, pkb, hipMemcpyDeviceToDevice, s));
+    if (wi) HIPCHK(hipMemcpyAsync(p->wimg, p->save_wimg, (size_t)p->wimg_cs, hipMemcpyDeviceToDevice, s));
+    if (wt) HIPCHK(hipMemcpyAsync(p->wtimg, p->save_wtimg, (size_t)p->wtimg_cs, hipMemcpyDeviceToDevice, s));
+    p->centre_stale = false;
+    p->n_snap = 0;                                        // the fit scale changed: the guard's history starts over
     return 0;
 }
 
@@ -601,8 +699,23 @@ GramArgs gram_args(vihmc_plan* p, int C) {
     a.stats = p->gstats;
     a.stats_cs = p->gstats_cs;
     a.gcol = p->gcol;
-    a.gcol_cs = 2 * 112;
+    a.gcol_cs = 4 * 112;
     a.ysum = p->ysq_dev + 1;
+    a.center = p->gram_center ? 1 : 0;
+    if (a.center) {
+        a.cbimg = p->cimgB;
+        a.ctimg = p->cimgT;
+        a.cb0 = p->cB0;
+        a.ccol = p->ccol;
+        a.cysum = p->cysq + 1;
+        a.ht_part = p->ght_part;
+        a.ht_cs = p->ght_cs;
+        a.hb_part = p->ghb_part;
+        a.hb_cs = p->ghb_cs;
+        a.ht = p->ght;
+        a.hbimg = p->ghb;
+        a.hb3img = p->ghb3;
+    }
     a.b0 = p->packed;
     a.b0_cs = p->dp;
     a.N = p->N;
@@ -986,6 +1099,22 @@ int build_deeponet(vihmc_plan* p, const vihmc_deeponet_desc* d, const float* xb,
     // weight images maintained by the scatter (after the activation layout, which fused_args reads)
     if (p->wimg)
         if (int rc = image_maps(p, d, idx)) return rc;
+    if (p->gram_alloc) {
+        // the centred Gram form's centre: chain 0's packed weights (and images) now, i.e. the frozen vector
+        if (int rc = p->alloc(&p->cpk, p->dp)) return rc;
+        if (int rc = p->alloc(&p->save_pk, p->dp)) return rc;
+        HIPCHK(hipMemcpy(p->cpk, p->packed, sizeof(float) * (size_t)p->dp, hipMemcpyDeviceToDevice));
+        if (p->wimg && p->img_by_scatter) {
+            if (int rc = p->alloc(&p->cwimg, p->wimg_cs)) return rc;
+            if (int rc = p->alloc(&p->save_wimg, p->wimg_cs)) return rc;
+            HIPCHK(hipMemcpy(p->cwimg, p->wimg, (size_t)p->wimg_cs, hipMemcpyDeviceToDevice));
+        }
+        if (p->wtimg && p->img_by_scatter) {
+            if (int rc = p->alloc(&p->cwtimg, p->wtimg_cs)) return rc;
+            if (int rc = p->alloc(&p->save_wtimg, p->wtimg_cs)) return rc;
+            HIPCHK(hipMemcpy(p->cwtimg, p->wtimg, (size_t)p->wtimg_cs, hipMemcpyDeviceToDevice));
+        }
+    }
     if (int rc = gram_images(p, nullptr)) return rc;
     HIPCHK(hipDeviceSynchronize());
     return 0;
@@ -1018,6 +1147,13 @@ bool fused_forward_ok(const vihmc_plan* p) {
     return true;
 }
 
+// the forward epilogue's activation code of layer j of a net: each net's last hidden tanh layer runs the correctly
+// rounded tanh_cr (plan option tanh_cr, default 1; vihmc_internal.h), every other layer its own activation
+int fwd_act(const vihmc_plan* p, const Net& n, int j) {
+    const int a = n.L[j].act;
+    return a == ACT_TANH && p->tanh_cr && j == (int)n.L.size() - 2 ? (int)ACT_TANH_CR : a;
+}
+
 void fused_args(vihmc_plan* p, int C, FusedArgs& a) {
     a.C = C;
     a.packed = p->packed;
@@ -1035,7 +1171,7 @@ void fused_args(vihmc_plan* p, int C, FusedArgs& a) {
         for (int j = 1; j < (int)n.L.size(); ++j) {
             f.h_off[j - 1] = n.h_off[j];
             f.w_off[j - 1] = n.L[j].wp;
-            f.act[j - 1] = n.L[j].act;
+            f.act[j - 1] = fwd_act(p, n, j);
         }
         f.rows = n.rows;
     }
@@ -1069,7 +1205,7 @@ int launch_forward_fused(vihmc_plan* p, int C, hipStream_t s, bool img, bool in0
             f.ldx = n.ld_in;
             f.k0 = L.n_in;
             f.ldw0 = L.ldi;
-            f.act0 = L.act;
+            f.act0 = fwd_act(p, n, 0);
             f.w0_off = L.wp;
             f.b0_off = L.bias;
         }
@@ -1165,7 +1301,7 @@ int deeponet_forward_layers(vihmc_plan* p, int C, hipStream_t s, bool img, bool 
             q.M = n.rows;
             q.Nn = L.n_out;
             q.K = L.n_in;
-            q.act = L.act;
+            q.act = fwd_act(p, n, j);
             q.ntiles = cdiv(n.rows, ROWDOT_WAVES * 16 * ms);
             // long contractions (the branch input layer: K = 101 on the f32 MFMA) one tile per workgroup: with
             // two they set the launch, 45 -> 35.5 us (the trunk input layer, K = 5, shares it at two tiles per
@@ -1284,6 +1420,9 @@ bool bwd_chain_args(vihmc_plan* p, int C, BwdChainArgs& a) {
 
 int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, float* grad, float* out,
                        hipStream_t s, const LeapArgs* leap) {
+    // the centred Gram form's centre (data images of y~, the fit guard's scale), before anything of this evaluation
+    if (gram_on(p) && !p->capturing)
+        if (int rc = ensure_centre(p, s)) return rc;
     const ScatterImg si = scatter_img(p);
     if (!(leap && leap->scattered_in))
         HIPCHK(launch_scatter(p->packed, p->dp, C, theta, p->K, p->smap_w, p->smap_wt, s, p->img_by_scatter ? &si : nullptr));
@@ -1359,8 +1498,9 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
     const bool snap = !gram && guard_live(p) && gram_on(p);
     if (!gram_on(p)) p->n_snap = 0;
     if (snap) {
+        // centred: the fit guard compares sum r^2 with sum y~^2 (the Gram form's terms now scale with y~, not y)
         stats_job.fit = p->fit_dev;
-        stats_job.ysq = p->ysq_dev;
+        stats_job.ysq = p->gram_center ? p->cysq : p->ysq_dev;
     }
     if (!want_grad) HIPCHK(launch_contract_stats(stats_job, C, s));
     if (want_grad) {
@@ -1411,6 +1551,16 @@ int deeponet_eval_body(vihmc_plan* p, const float* theta, int C, float* logp, fl
         else HIPCHK(launch_reduce(p->jobsB, 1, p->spanB, C, s, nullptr, only));
         }
 
+        // diagnostics (plan option debug_dz): the contraction's dZ_b / dZ_t of every chain kept for
+        // vihmc_plan_debug_copy("dzb_snap" / "dzt_snap") -- the layer backward overwrites delta[0]
+        if (p->debug_dz) {
+            if (!p->dzb_snap) {
+                if (int rc = p->alloc(&p->dzb_snap, b.delta_cs * p->maxC)) return rc;
+                if (int rc = p->alloc(&p->dzt_snap, t.delta_cs * p->maxC)) return rc;
+            }
+            HIPCHK(hipMemcpyAsync(p->dzb_snap, b.delta[0], sizeof(float) * b.delta_cs * C, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(p->dzt_snap, t.delta[0], sizeof(float) * t.delta_cs * C, hipMemcpyDeviceToDevice, s));
+        }
         // backward through both MLPs, last layer first: one fused launch per layer (branch + trunk
         // grouped) computes delta_{l-1} and the dW / db partial slabs
         int cur[2] = {0, 0};
@@ -1720,8 +1870,10 @@ int vihmc_split_step(vihmc_plan* p, float* theta, float* momentum, int C, float*
         lf.mode = mode;
         lf.kick = kick;
         lf.drift = drift;
-        lf.scattered_in = scattered_in ? 1 : 0;
-        if (mode == 1 && scatter_into) {
+        // plan option fuse_scatter = 0 (the A/B path, as in vihmc_trajectory): such a plan receives no scatter from
+        // the previous shard's gather and runs its own k_scatter, whatever the caller says
+        lf.scattered_in = scattered_in && p->fuse_scatter ? 1 : 0;
+        if (mode == 1 && scatter_into && scatter_into->fuse_scatter) {
             vihmc_plan* q = scatter_into;
             const ScatterImg si = scatter_img(q);
             lf.sc = ScatterArgs{q->packed, q->dp, q->smap_w, q->smap_wt, q->img_by_scatter ? si : ScatterImg{}};
@@ -2069,7 +2221,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, timing_every, fwd_wimg, fwd_in0, skip_zt, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, timing_every, fwd_wimg, fwd_in0, skip_zt, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_active, gram_center, tanh_cr, debug_dz, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -2101,6 +2253,22 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
         else if (value < 0 || (double)value > (double)p->N * (double)p->P) return fail("lik_count must be in [0, N P]");
         else p->lik_count = value;
     }
+    else if (k == "gram_active") return fail("plan option 'gram_active' is read-only");
+    else if (k == "debug_dz") {
+        p->debug_dz = value ? 1 : 0;
+        return 0;
+    }
+    else if (k == "tanh_cr") {                                  // forward: the centre (a forward output) is stale
+        p->tanh_cr = value ? 1 : 0;
+        p->centre_stale = true;
+    }
+    else if (k == "gram_center") {                              // centred Gram form (1) or y itself (0)
+        if ((value ? 1 : 0) != p->gram_center) {
+            p->gram_center = value ? 1 : 0;
+            if (int rc = gram_images(p, nullptr)) return rc;    // y images now, or the centre at the next evaluation
+            HIPCHK(hipDeviceSynchronize());
+        }
+    }
     else if (k == "grad_evals" || k == "gram_evals") {          // counters: any value resets both
         p->n_grad_calls = p->n_gram_calls = p->n_gram_chain_evals = 0;
         return 0;
@@ -2129,6 +2297,13 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     else if (k == "bwd_chain") *value = p->bwd_chain | (p->last_bwd_chain ? 2 : 0);
     else if (k == "gram") *value = (p->gram && p->gram_alloc ? 1 : 0) | (p->last_gram ? 2 : 0);
     else if (k == "gram_min_chains") *value = p->gram_min_chains;
+    // whether this plan's gradient-only evaluations can take the Gram form at all (gram, width, max_chains >=
+    // gram_min_chains, no target mask, and a plan beyond GUARD_MAXC chains only with the fit guard off): a plan that
+    // falls back to the residual form for its chain count says so here
+    else if (k == "gram_active") *value = gram_on(p) ? 1 : 0;
+    else if (k == "gram_center") *value = p->gram_center;
+    else if (k == "tanh_cr") *value = p->tanh_cr;
+    else if (k == "debug_dz") *value = p->debug_dz;
     else if (k == "grad_evals") *value = (int)std::min<int64_t>(p->n_grad_calls, INT32_MAX);
     else if (k == "gram_evals") *value = (int)std::min<int64_t>(p->n_gram_calls, INT32_MAX);
     else if (k == "gram_chains") *value = p->last_gram_chains;
@@ -2183,6 +2358,17 @@ int vihmc_plan_debug_copy(vihmc_plan* p, const char* name, void* dst, int64_t* b
         else if (k == "gram_gb") src = p->ggb, n = 4 * (int64_t)CONTRACT_SPLIT_BLOCK * C;
         else if (k == "gram_tt") src = p->gtt_part, n = 4 * p->gtt_cs * C;
         else if (k == "gram_stats") src = p->gstats, n = 8 * p->gstats_cs * C;
+        else if (k == "gram_ht") src = p->ght, n = 4 * 112 * 112 * C;
+        else if (k == "dzb_snap") src = p->dzb_snap, n = 4 * b.delta_cs * C;
+        else if (k == "dzt_snap") src = p->dzt_snap, n = 4 * t.delta_cs * C;
+        else if (k == "gram_ht_part") src = p->ght_part, n = 4 * p->ght_cs * C;
+        else if (k == "gram_hb_part") src = p->ghb_part, n = 4 * p->ghb_cs * C;
+        else if (k == "gram_gcol") src = p->gcol, n = 8 * 4 * 112 * C;
+        else if (k == "center_bimg") src = p->cimgB, n = p->cimgB ? p->qsplitA_cs : 0;
+        else if (k == "center_timg") src = p->cimgT, n = p->cimgT ? p->qsplitB_cs : 0;
+        else if (k == "center_b0") src = p->cB0, n = p->cB0 ? 4 * (int64_t)p->N * p->ldz : 0;
+        else if (k == "center_col") src = p->ccol, n = p->ccol ? 8 * 112 : 0;
+        else if (k == "center_ysq") src = p->cysq, n = p->cysq ? 16 : 0;
         else return fail("vihmc_plan_debug_copy: unknown buffer " + k);
         if (!src) n = 0;
         *bytes = n;

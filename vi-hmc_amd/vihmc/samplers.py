@@ -148,9 +148,33 @@ class ChainRNG:
         else:
             raise ValueError(f"unknown rng mode {mode!r}")
         self._pin = self.device.type == "cuda"
+        self._ahead = None             # (generator states before the draw, momenta) of prefetch_momentum
+
+    def prefetch_momentum(self):
+        """Draw the NEXT draw_momentum()'s momenta now (the runner does this while the device works). Transparent to
+        every other use of this object: the generators' states before the draw are kept, and any other draw that
+        comes first rewinds them and drops the prefetch, so each chain's stream keeps hamiltorch's call order whoever
+        else draws from it."""
+        if self.mode != "per_chain" or self._ahead is not None:
+            return
+        states = [g.get_state() for g in self.gens]
+        self._ahead = (states, self._draw_momentum())
+
+    def _rewind(self):
+        if self._ahead is not None:
+            for g, st in zip(self.gens, self._ahead[0]):
+                g.set_state(st)
+            self._ahead = None
 
     def draw_momentum(self) -> torch.Tensor:
         """Standard-normal momenta [C, K] on the device (hamiltorch gibbs)."""
+        if self._ahead is not None:
+            z = self._ahead[1]
+            self._ahead = None
+            return z
+        return self._draw_momentum()
+
+    def _draw_momentum(self) -> torch.Tensor:
         if self.mode == "global":
             return torch.normal(torch.zeros(self.K, device=self.device), torch.ones(self.K, device=self.device))[None]
         z = torch.empty(self.C, self.K, pin_memory=self._pin)
@@ -161,6 +185,7 @@ class ChainRNG:
     def draw_logu(self, mask=None) -> torch.Tensor:
         """log(torch.rand(1)) per chain on the device (hamiltorch's accept draw, computed on the CPU);
         chains with mask[c] False do not consume their stream (value -inf)."""
+        self._rewind()
         if self.mode == "global":
             if mask is not None and not mask[0]:        # hamiltorch raised LogProbError: no draw
                 return torch.full((1,), float("-inf"), device=self.device)
@@ -307,9 +332,11 @@ class HMCRunner:
         self.n = 0
         # kinetic energies in one vihmc_kinetic launch (engine evaluators on CUDA; both accept forms use it, so they
         # stay bitwise equal) instead of 0.5 * (p * p).sum(1)'s four; its workspace is zeroed once here
-        self._native_ke = device.type == "cuda" and all(isinstance(e, EngineEvaluator) for e in self.evs)
+        # strict_rng (the hamiltorch drop-in sample()) keeps the reference's fp32 0.5 * (p * p).sum(): accept decisions
+        # within a few ulps of the margin then fall as hamiltorch's do
+        self._native_ke = (device.type == "cuda" and not self.strict
+                           and all(isinstance(e, EngineEvaluator) for e in self.evs))
         self._ke_ws = None
-        self._z_ahead = None      # the next iteration's momenta, drawn while this one runs on the device
 
     def _ke(self, p):
         """The kinetic energy of every chain [C] (hamiltorch's 0.5 p.p, or 0.5 p.(inv_mass p))."""
@@ -441,8 +468,7 @@ class HMCRunner:
         if n >= self.num_samples:
             raise RuntimeError("all samples drawn")
         rng = self.rng
-        z = self._z_ahead if self._z_ahead is not None else rng.draw_momentum()
-        self._z_ahead = None
+        z = rng.draw_momentum()                 # prefetched by _draw_ahead at the end of the previous iteration
         logu = None if self.strict else rng.draw_logu()
         p = z if self.mass_sqrt is None else z * self.mass_sqrt
         th, lp, g = self.cur
@@ -491,10 +517,11 @@ class HMCRunner:
     def _draw_ahead(self, n):
         """Iteration n + 1's momenta, drawn on the host now -- after iteration n's last draw (its accept uniform), so
         each chain's stream keeps hamiltorch's order -- while iteration n runs on the device: config 4's 172,401 CPU
-        normals per chain otherwise left the GPU idle ~0.33 ms per iteration (profiles/r05lt_c1_trace.txt). Only for
-        the runner's private per-chain generators, and only when an iteration n + 1 exists."""
+        normals per chain otherwise left the GPU idle ~0.33 ms per iteration (profiles/r05lt_c1_trace.txt). The
+        prefetch lives in the ChainRNG, which rewinds it if anything else draws first, so a caller-supplied generator
+        shared with other code keeps hamiltorch's order; only when an iteration n + 1 exists."""
         if self.rng.mode == "per_chain" and self.device.type == "cuda" and n + 1 < self.num_samples:
-            self._z_ahead = self.rng.draw_momentum()
+            self.rng.prefetch_momentum()
 
     def _accept_fused(self, n, lp, ke0, th_new, ke1, lp_new, g_new, logu):
         """The accept block above for CUDA chains in one vihmc_hmc_accept launch (the same kinetic energies and

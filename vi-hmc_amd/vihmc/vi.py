@@ -321,9 +321,11 @@ class BatchEngines:
         y, count = self.canonical(batch[1], batch[2])
         eng.set_data(xb, y)
         masked = count < xb.shape[0] * self.P
-        # options only on a change: vihmc_plan_option drops the plan's captured graphs (VIHMC_GRAPH=1)
-        for k, v in (("y_masked", 1 if masked else 0), ("lik_count", count if masked else 0)):
-            if eng.get_option(k) != v:
+        # options only on a change: vihmc_plan_option drops the plan's captured graphs (VIHMC_GRAPH=1). The getter of
+        # lik_count returns the EFFECTIVE count (N P when the stored value is 0), so it is compared against that.
+        for k, v, eff in (("y_masked", 1 if masked else 0, 1 if masked else 0),
+                          ("lik_count", count if masked else 0, count)):
+            if eng.get_option(k) != eff:
                 eng.option(k, v)
         self.count = count
         return eng
