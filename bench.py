@@ -160,7 +160,7 @@ def class_flops(eng, spec, prob):
     """Algorithmic FLOP per chain of each timing class (the input layers count with the forward when its launch runs
     them: plan option fwd_in0)."""
     fl = spec.flops_by_kernel(prob.N, prob.P)
-    fl["gram"] = spec.flops_gram(prob.N, prob.P)
+    fl["gram"] = spec.flops_gram(prob.N, prob.P, centred=bool(eng.get_option("gram_center")))
     if eng.get_option("fwd_in0"):
         fl["fwd"] += fl["input"]
     return fl

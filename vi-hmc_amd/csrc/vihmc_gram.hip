@@ -60,8 +60,8 @@ constexpr int GR_THREADS = 64 * (GR_CW + 1);              // + one DMA wave
 // of two blocks); k_gram_b runs 8 extension blocks (-Gb, then -Hb) and its dZb units stage Gt (fp64), Ht (fp32),
 // dB^T and B0^T
 constexpr int GR_LDS_C = GR_NBUF * 2 * GR_BLK;            // 126 KB
-constexpr int GRB_LDS_TC = GR_LDS + 8 * GRAM_P3_BLOCK;    // 120.5 KB
-constexpr int GRB_DZBC = 101 * 112 * 8 + 101 * 112 * 4 + 2 * 101 * 32 * 4;   // 161,600 B
+constexpr int GRB_LDS_TC = GR_LDS;                       // 64.5 KB: no 4th planes
+constexpr int GRB_DZBC = 2 * 101 * 112 * 4 + 2 * 101 * 32 * 4;               // 116,352 B
 constexpr int GRB_LDS_C = GRB_LDS_TC > GRB_DZBC ? GRB_LDS_TC : GRB_DZBC;
 static_assert(GR_LDS_C <= 160 * 1024 && GRB_LDS_C <= 160 * 1024, "centred Gram LDS");
 
@@ -337,14 +337,17 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
         // wave vt < 7 owns row tile vt: H (vt, 0..6) and G (vt, vt..6), sharing each column fragment; its dZ fragment
         // is formed once per block from the two images' planes (delta_frag). fp32 MFMA accumulation over the slab
         // (in the centred form both matrices multiply residual-sized operands), fp64 across the slabs (k_gram_sum).
+        // Balance: compute wave 7 takes G (0, 4..6), (1, 5..6), (2, 6), so the four SIMDs (waves w, w + 4) carry 21 / 20 /
+        // 19 / 17 tiles per block instead of 24 / 20 / 16 / 11 (wave vt keeps G (vt, vt .. lim(vt) - 1))
         const int vt = wave;
+        const int lim = vt < 3 ? 4 + vt : 7;
         f32x4 hacc[7], gacc[7];
 #pragma unroll
         for (int t = 0; t < 7; ++t) hacc[t] = gacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int i = 0; i < nb; ++i) {
             __syncthreads();
+            const unsigned char* zbuf = lds + (i % GR_NBUF) * 2 * GR_BLK;
             if (vt < 7) {
-                const unsigned char* zbuf = lds + (i % GR_NBUF) * 2 * GR_BLK;
                 bf16x8 za[3], ra[3], da[3];
                 load_b(zbuf, tro, vt, za);
                 load_b(zbuf + GR_BLK, tro, vt, ra);
@@ -354,25 +357,44 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_a(GramArgs A) {
                     bf16x8 b[3];
                     load_b(zbuf, tro, t, b);
                     hacc[t] = six(da, b, hacc[t]);
-                    if (t >= vt) gacc[t] = six(za, b, gacc[t]);
+                    if (t >= vt && t < lim) gacc[t] = six(za, b, gacc[t]);
+                }
+            } else {
+                // wave 7: the six G tiles of rows 0..2 the first three waves leave (gacc[k], k = 0..5)
+                bf16x8 a0f[3], a1f[3], a2f[3];
+                load_b(zbuf, tro, 0, a0f);
+                load_b(zbuf, tro, 1, a1f);
+                load_b(zbuf, tro, 2, a2f);
+#pragma unroll
+                for (int t = 4; t < 7; ++t) {
+                    bf16x8 b[3];
+                    load_b(zbuf, tro, t, b);
+                    gacc[t - 4] = six(a0f, b, gacc[t - 4]);                       // (0, 4), (0, 5), (0, 6)
+                    if (t >= 5) gacc[t - 2] = six(a1f, b, gacc[t - 2]);           // (1, 5), (1, 6)
+                    if (t == 6) gacc[5] = six(a2f, b, gacc[5]);                   // (2, 6)
                 }
             }
         }
+        double* gp = (kind == 1 ? A.gt_part + c * A.gt_cs : A.gb_part + c * A.gb_cs) + (int64_t)s * 28 * 256 + 4 * lane;
+        // index of (v, t) in the row-major upper-triangle list (k_gram_sum's decode)
+        auto tri = [](int v, int t) { return 7 * v - v * (v - 1) / 2 + t - v; };
         if (vt < 7) {
             float* hp = (kind == 1 ? A.ht_part + c * A.ht_cs : A.hb_part + c * A.hb_cs) +
                         ((int64_t)s * 49 + vt * 7) * 256 + 4 * lane;
 #pragma unroll
             for (int t = 0; t < 7; ++t) *reinterpret_cast<f32x4*>(hp + t * 256) = hacc[t];
-            // G (vt, t >= vt) at its index in the row-major upper-triangle list (k_gram_sum's decode)
-            double* gp = (kind == 1 ? A.gt_part + c * A.gt_cs : A.gb_part + c * A.gb_cs) + (int64_t)s * 28 * 256 +
-                         4 * lane;
-            const int j0 = 7 * vt - vt * (vt - 1) / 2 - vt;
 #pragma unroll
             for (int t = 0; t < 7; ++t)
-                if (t >= vt) {
+                if (t >= vt && t < lim) {
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) gp[(j0 + t) * 256 + r] = (double)gacc[t][r];
+                    for (int r = 0; r < 4; ++r) gp[tri(vt, t) * 256 + r] = (double)gacc[t][r];
                 }
+        } else {
+            const int tv[6] = {0, 0, 0, 1, 1, 2}, tt[6] = {4, 5, 6, 5, 6, 6};
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gp[tri(tv[k], tt[k]) * 256 + r] = (double)gacc[k][r];
         }
     } else if (kind == 0) {
         // ---------------- T_b = y Zt^ (A = YA rows, 16-B loads one block ahead in two register sets) ----------
@@ -652,16 +674,12 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
         const unsigned char* bsrc = A.bimg + c * A.bimg_cs + (int64_t)kb0 * CONTRACT_SPLIT_BLOCK;
         const unsigned char* gsrc = A.gbimg + c * A.gbimg_cs;
         const unsigned char* hsrc = CEN ? A.hbimg + c * A.gbimg_cs : nullptr;
-        if (ext) {
-            // the 4th planes of the extension blocks, first: dma_role's counted waits retire them with block 0
+        if (ext && !CEN) {
+            // the 4th -Gb planes of the extension blocks, first: dma_role's counted waits retire them with block 0
+            // (centred: the extension terms are of the residual's size, three planes carry them to fp32)
             const unsigned char* p3 = A.gb3img + c * 4 * GRAM_P3_BLOCK;
             for (int k = 0; k < 4 * GRAM_P3_BLOCK / 1024; ++k)
                 bf6::glds16_asm(p3 + k * 1024 + lane * 16, lds + GRB_P3 + k * 1024);
-            if (CEN) {
-                const unsigned char* h3 = A.hb3img + c * 4 * GRAM_P3_BLOCK;
-                for (int k = 0; k < 4 * GRAM_P3_BLOCK / 1024; ++k)
-                    bf6::glds16_asm(h3 + k * 1024 + lane * 16, lds + GRB_P3 + 4 * GRAM_P3_BLOCK + k * 1024);
-            }
         }
         dma_role(lds, lane, nb, [&](int i) {
             return i < nbm ? bsrc + (int64_t)i * CONTRACT_SPLIT_BLOCK
@@ -756,8 +774,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
             for (int e = 0; e < 8; ++e) {
                 __syncthreads();
                 if (e + 1 < 8) load_ext_c(e + 1, (e & 1) ? a0 : a1);
-                mma_block9(lds + ((nbm + e) % GR_NBUF) * GR_BLK, lds + GRB_P3 + e * GRAM_P3_BLOCK, tro, (e & 1) ? a1 : a0,
-                           acc);
+                mma_block(lds + ((nbm + e) % GR_NBUF) * GR_BLK, tro, (e & 1) ? a1 : a0, acc);
             }
         } else if (ext) {
             // extension: acc -= Zt^ Gb (B blocks hold -Gb); A lane (lr, lg) = Zt^[p][32e + 4lg + j] (j < 4) and
@@ -981,30 +998,29 @@ __device__ __forceinline__ void dzb_unit(const GramArgs& A, int u, unsigned char
 }
 
 // Centred dZb epilogue unit (c, 32-row group m): dZb[n][x] = gscale (sum_v dB[n][v] Gt[v][x] + B0[n][v] Ht[v][x]
-// - sum_s T~_b[s][n][x]), dB = Zb^ - B0 (column 100: 1 - 1 = 0, B0[n][100] = 1), the T_b slabs over y~. LDS: Gt fp64
-// [101][112], Ht fp32 [101][112], dB^T and B0^T [101][32] fp32; the sums in fp64 as dzb_unit's.
+// - sum_s T~_b[s][n][x]), dB = Zb^ - B0 (column 100: 1 - 1 = 0, B0[n][100] = 1), the T_b slabs over y~. LDS: Gt and Ht
+// fp32 [101][112], dB^T and B0^T [101][32]. Both Gram terms are of the residual's size here, so their 202-term sum runs
+// in fp32 (dzb_unit's fp64 guarded the uncentred Zb^ Gt, ~sqrt(P) |y| / |S - y| larger than the result); the T~_b
+// slabs are added in fp64.
 __device__ __forceinline__ void dzb_unit_c(const GramArgs& A, int u, unsigned char* lds) {
-    double* gts = reinterpret_cast<double*>(lds);
-    float* hts = reinterpret_cast<float*>(gts + 101 * 112);
+    float* gts = reinterpret_cast<float*>(lds);
+    float* hts = gts + 101 * 112;
     float* dbt = hts + 101 * 112;
     float* b0t = dbt + 101 * 32;
     const int ngroups = (A.N + 31) / 32;
     const int c = u / ngroups, m = u - c * ngroups;
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
-    typedef double f64x2 __attribute__((ext_vector_type(2)));
-    const double* gt = A.gt64 + c * A.gt_cs2;
+    const float* gt = A.gt + c * A.gt_cs2;
     const float* ht = A.ht + c * A.gt_cs2;
-    constexpr int GSL = (101 * 56 + GR_THREADS - 1) / GR_THREADS;       // f64x2 of Gt per thread
-    constexpr int HSL = (101 * 28 + GR_THREADS - 1) / GR_THREADS;       // f32x4 of Ht per thread
+    constexpr int HSL = (101 * 28 + GR_THREADS - 1) / GR_THREADS;       // f32x4 of Gt / Ht per thread
     constexpr int ZSL = (32 * 101 + GR_THREADS - 1) / GR_THREADS;
-    f64x2 gv[GSL];
-    f32x4 hv[HSL];
+    f32x4 gv[HSL], hv[HSL];
 #pragma unroll
-    for (int k = 0; k < GSL; ++k) {
-        const int e = min(tid + GR_THREADS * k, 101 * 56 - 1);
-        const int v = e / 56, q = e - v * 56;
-        gv[k] = *reinterpret_cast<const f64x2*>(gt + v * 112 + 2 * q);
+    for (int k = 0; k < HSL; ++k) {
+        const int e = min(tid + GR_THREADS * k, 101 * 28 - 1);
+        const int v = e / 28, q = e - v * 28;
+        gv[k] = *reinterpret_cast<const f32x4*>(gt + v * 112 + 4 * q);
     }
 #pragma unroll
     for (int k = 0; k < HSL; ++k) {
@@ -1025,15 +1041,10 @@ __device__ __forceinline__ void dzb_unit_c(const GramArgs& A, int u, unsigned ch
         if (n >= A.N) dv[k] = bv[k] = 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < GSL; ++k) {
-        const int e = min(tid + GR_THREADS * k, 101 * 56 - 1);
-        const int v = e / 56, q = e - v * 56;
-        *reinterpret_cast<f64x2*>(gts + v * 112 + 2 * q) = gv[k];
-    }
-#pragma unroll
     for (int k = 0; k < HSL; ++k) {
         const int e = min(tid + GR_THREADS * k, 101 * 28 - 1);
         const int v = e / 28, q = e - v * 28;
+        *reinterpret_cast<f32x4*>(gts + v * 112 + 4 * q) = gv[k];
         *reinterpret_cast<f32x4*>(hts + v * 112 + 4 * q) = hv[k];
     }
 #pragma unroll
@@ -1069,21 +1080,21 @@ __device__ __forceinline__ void dzb_unit_c(const GramArgs& A, int u, unsigned ch
 #pragma unroll
             for (int r = 0; r < 4; ++r) ts[r] += (double)v[r];
         }
-        double gz[4] = {0, 0, 0, 0};
+        float gz[4] = {0.f, 0.f, 0.f, 0.f};
         const int x = 16 * t + lr;
         for (int v = 0; v < 101; ++v) {
             const f32x4 d = *reinterpret_cast<const f32x4*>(dbt + v * 32 + 16 * rt + 4 * lg);
             const f32x4 b = *reinterpret_cast<const f32x4*>(b0t + v * 32 + 16 * rt + 4 * lg);
-            const double g = gts[v * 112 + x];
-            const double h = (double)hts[v * 112 + x];
+            const float g = gts[v * 112 + x];
+            const float h = hts[v * 112 + x];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) gz[r] = fma((double)d[r], g, fma((double)b[r], h, gz[r]));
+            for (int r = 0; r < 4; ++r) gz[r] = fmaf(d[r], g, fmaf(b[r], h, gz[r]));
         }
         if (x < 100) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int n = n32 + 16 * rt + 4 * lg + r;
-                if (n < A.N) out[(int64_t)n * A.ldz + x] = (float)((double)A.gscale * (gz[r] - ts[r]));
+                if (n < A.N) out[(int64_t)n * A.ldz + x] = (float)((double)A.gscale * ((double)gz[r] - ts[r]));
             }
         }
     }

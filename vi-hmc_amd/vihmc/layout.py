@@ -114,12 +114,14 @@ class DeepONetSpec:
         d["contract_b"] = c
         return d
 
-    def flops_gram(self, n: int, p: int) -> float:
+    def flops_gram(self, n: int, p: int, centred: bool = True) -> float:
         """Algorithmic FLOP per chain of the Gram-form gradient-only contraction (vihmc_gram.hip, the inner
         leapfrog evaluations), which replaces side A + side B there: y Zt^ and y^T Zb^ (2 N P (W+1) each) and the
-        (N + P) (W+1)^2 Gram / correction products (Zt^T Zt^, Zb^T Zb^, Zt^ Gb, Zb^ Gt), augmented width W + 1."""
+        (N + P) (W+1)^2 Gram / correction products (Zt^T Zt^, Zb^T Zb^, Zt^ Gb, Zb^ Gt), augmented width W + 1.
+        Centred (plan option gram_center, round 6): also Ht = dT^T Zt^, Hb = dB^T Zb^ and the second correction of
+        each side (B0 Ht, T0 Hb)."""
         wa = self.out + 1
-        return 4.0 * n * p * wa + 4.0 * (n + p) * wa * wa
+        return 4.0 * n * p * wa + (8.0 if centred else 4.0) * (n + p) * wa * wa
 
 
 @dataclass(frozen=True)
