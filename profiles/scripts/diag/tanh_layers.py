@@ -42,7 +42,7 @@ t0 = p.teacher[p.grad_ind].astype(np.float32)
 rng = np.random.default_rng(31)
 ths = [t0] + [(t0 * (1 + 1e-6 * rng.standard_normal(t0.size))).astype(np.float32) for _ in range(2)]
 g64s = [np_logp_grad(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, th, 0.0, SD, "NLL", 1.0)[1] for th in ths]
-for name, kw in [] and [("all", dict(which=set(range(8)))), ("last(7)", dict(which={7})), ("first7(0-6)", dict(which=set(range(7)))),
+for name, kw in [("all", dict(which=set(range(8)))), ("last(7)", dict(which={7})), ("first7(0-6)", dict(which=set(range(7)))),
                  ("last2(6,7)", dict(which={6,7})), ("rand0.3ulp", dict(noise_ulp=0.3)), ("rand1ulp", dict(noise_ulp=1.0))]:
     m = LayerRef(lay, p.branch_in, p.trunk_in, p.y, p.mu, p.grad_ind, 0.0, SD, "NLL", 1.0, **kw)
     e = [np.linalg.norm(m.logp_grad(th)[1] - g) / np.linalg.norm(g) for th, g in zip(ths, g64s)]
