@@ -5,7 +5,7 @@ TAG=${1:-g}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out
 mkdir -p $O
-P="python3 $ROOT/profiles/scripts/probes/probe_classes.py --chains 16 --iters 5 --grad"
+P="python3 $ROOT/profiles/scripts/probes/probe_classes.py --chains 16 --iters 5 --grad ${OPT:+--opt $OPT}"
 G1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
 G2="SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_UNALIGNED_STALL SQ_ACTIVE_INST_VALU"
 cd /tmp && export TMPDIR=/tmp && \

@@ -4,7 +4,7 @@ TAG=${1:-r03}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out
 mkdir -p $O
-P="python3 $ROOT/profiles/scripts/probes/probe_classes.py --chains 16 --iters 5 ${GRAD:+--grad}"
+P="python3 $ROOT/profiles/scripts/probes/probe_classes.py --chains 16 --iters 5 ${GRAD:+--grad} ${OPT:+--opt $OPT}"
 cd /tmp && export TMPDIR=/tmp && \
 timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/${TAG}_fetch -o p -- $P > $O/${TAG}_fetch.log 2>&1 && \
 timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d $O/${TAG}_write -o p -- $P > $O/${TAG}_write.log 2>&1 && \

@@ -451,3 +451,58 @@ def test_gram_guard_fused_trajectory_bitwise_equals_stepwise(cuda_device):
     assert torch.equal(a.accepted, b.accepted)
     assert torch.equal(a.samples[:, :int(a.counts.max())], b.samples[:, :int(b.counts.max())])
     assert torch.equal(a.logp_trace, b.logp_trace)
+
+
+@pytest.mark.parametrize("C", [8, 16])
+def test_gram_pair2_bitwise(C, cuda_device):
+    """Two-chain T_t units (k_gram_b2, plan option gram_pair2; centred form): the same products in the same order per
+    chain as the one-chain units, so dZt and the whole gradient are bit for bit those of gram_pair2 = 0, with the row
+    groups split between the two kernels (1: launch_gram's choice -- C = 16: 32 of the 40 row groups in pairs, C = 8:
+    all of them) or every row group in pairs (2); distinct chains, repeated calls."""
+    c = deeponet_case("deeponet_burgers")
+    base = np.stack([c.thetas[i % len(c.thetas)] for i in range(C)]).astype(np.float32)
+    rng = np.random.default_rng(29)
+    th = torch.tensor(base + 0.02 * rng.standard_normal(base.shape, dtype=np.float32), device=cuda_device)
+    eng = engine_for(c, C, cuda_device)
+    assert eng.get_option("gram_center") == 1 and eng.get_option("gram_pair2") == 0
+    out = {}
+    for v in (0, 1, 2, 1):
+        eng.option("gram_pair2", v)
+        g = eng.grad(th)
+        assert eng.get_option("gram") & 2 and eng.get_option("gram_chains") == C
+        if v in out:
+            assert torch.equal(g, out[v]), f"gram_pair2 = {v} not deterministic"
+        out[v] = g.clone()
+    assert torch.equal(out[1], out[0]) and torch.equal(out[2], out[0])
+
+
+def test_gram_pair2_with_guarded_chains(cuda_device):
+    """A chain pair with one chain guarded (residual form) and one in the Gram form: k_gram_b2 computes the pair and
+    stores only the Gram chain's dZt -- the guarded chains bitwise their residual-form gradient, the others bitwise
+    the one-chain units' result. The poor-centre problem of test_centred_guard_protects_a_poor_centre: chains at the
+    data's generator guarded, chains at the centre not; every row group in pairs (gram_pair2 = 2)."""
+    from vihmc.data import deeponet_problem
+    from vihmc.engine import DeepONetEngine, trunk_features
+    from vihmc.layout import DeepONetSpec
+    p = deeponet_problem(seed=5, n=64, nt=21, nx=21, noise=1e-4, mu_noise=0.05, k=None)
+    t = p.teacher[p.grad_ind].astype(np.float32)
+    m = p.mu[p.grad_ind].astype(np.float32)
+    th = torch.tensor(np.stack([t, m, t, m]), device=cuda_device)
+    res = []
+    for v in (0, 2):
+        eng = DeepONetEngine(DeepONetSpec(), p.branch_in, trunk_features(p.trunk_in), p.y, p.mu, p.grad_ind, 0.0, 0.1,
+                             "NLL", 1.0, max_chains=4, device=cuda_device)
+        eng.option("gram_pair2", v)
+        eng.option("gram_guard", 0)
+        g_all = eng.grad(th).clone()
+        assert eng.get_option("gram_chains") == 4
+        eng.option("gram_guard", 1)
+        _, g_res = eng.logp_grad(th)
+        eng.logp_grad(th)
+        g = eng.grad(th)
+        assert eng.get_option("gram_chains") == 2, eng.get_option("gram_chains")
+        assert torch.equal(g[0::2], g_res[0::2]), "guarded chains: the residual-form gradient"
+        assert torch.equal(g[1::2], g_all[1::2]), "Gram chains: independent of their guarded partners"
+        res.append(g.cpu())
+        eng.close()
+    assert torch.equal(res[0], res[1])

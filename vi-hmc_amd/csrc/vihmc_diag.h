@@ -55,3 +55,5 @@
 #define VIHMC_FUSED_FWD 1
 // Gram form: the dZb epilogue's sums (Zb^ Gt over v, the T_b slabs) in fp64 (0: fp32 fma)
 #define GRAM_DZB_FP64 1
+// Gram form, centred: cost of a two-chain T_t unit (k_gram_b2) in one-chain units, for launch_gram's row-group split
+#define GRAM_B2_RATIO 1.7

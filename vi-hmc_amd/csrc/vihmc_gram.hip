@@ -651,7 +651,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     int list, u;
     // the dZb epilogue units go last: they fill the half round the 640 T_t units leave at 16 chains (0.531 -> 0.519 ms,
     // profiles/r03z_ab_gram_epi_last.txt)
-    unit_of(blockIdx.x, A.upx_b, A.PT * A.SB * A.C, A.C * ((A.N + 31) / 32), list, u, false);
+    unit_of(blockIdx.x, A.upx_b, (A.PT - A.pt2) * A.SB * A.C, A.C * ((A.N + 31) / 32), list, u, false);
     if (list < 0) return;
     if (list == 1) {                   // the dZb epilogue units fill the tail of the T_t rounds (k_gram_a is done)
         if (CEN) dzb_unit_c(A, u, lds);
@@ -660,7 +660,7 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     }
     // T_t unit (pt, sb, c): chains minor, so the chains sharing one YB slab (rows, k range) run on one XCD
     const int g = u / A.C, c = u - g * A.C;
-    const int pt = g / A.SB, sb = g - pt * A.SB;
+    const int pt = A.pt2 + g / A.SB, sb = g % A.SB;       // row groups [0, pt2): k_gram_b2's chain pairs
     if (A.sel && chain_bit(A.bits, c)) return;            // fit guard: residual form for this chain
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
     const int kb0 = sb * A.SLB;
@@ -826,6 +826,179 @@ __global__ __launch_bounds__(GR_THREADS, 1) void k_gram_b(GramArgs A) {
     }
     if (wave == GR_CW) return;
     gram_tt_epilogue(A, c, pt, wave, lane, acc);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// k_gram_b2 (centred form, SB = 1, round 6): T_t units of TWO chains. Unit (pt, pair): chains c0 = 2 pair, c1 = c0 + 1,
+// rows p0 = 256 pt + 32 w of wave w; the 8 waves stream the shared YB rows once for both chains (one A fragment feeds
+// the two chains' products), the two chains' branch-image blocks share a ring slot (2 x 21 KB, 3 slots). No DMA wave:
+// its 256-VGPR share holds the two chains' 112 accumulator registers, so the compute waves issue the block DMA
+// themselves (42 one-KB pieces per block, q = w, w + 8, ...) right after the wait that retires the block before it
+// -- wait_vmcnt0 at every block start: the builtin half tells hipcc every earlier load is retired (its own waits after
+// it do not count the DMA issued next), the asm half covers the DMA it cannot see. A DMA issued at block i is retired
+// by the wait of block i + 1 and read at block i + 2. The extension runs per chain (16 blocks: chain c0's dT Gb, T0 Hb,
+// then c1's), A formed from the chain's trunk image and the centre's. Row groups [0, pt2): launch_gram sizes pt2 so
+// these units fill whole rounds of the chip; k_gram_b takes the rest (and the dZb epilogue units).
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int GB2_THREADS = 64 * GR_CW;
+constexpr int GB2_SLOT = 2 * GR_BLK;
+constexpr int GB2_LDS = GR_NBUF * GB2_SLOT;               // 126 KB
+static_assert(GB2_LDS <= 160 * 1024, "k_gram_b2 LDS");
+
+namespace {
+// one 32-long k block of a wave's two 32 x 112 tiles (chains c0, c1: slot halves 0 / 1), the A fragment shared:
+// B fragments of (tile, chain) step q + 1 read while step q's 12 MFMAs run
+template <typename PRE>
+__device__ __forceinline__ void mma_block2(const unsigned char* slot, int tro, const bf16x8 (&a)[2][3],
+                                           f32x4 (&acc)[2][2][7], PRE pre) {
+    bf16x8 b[2][3];
+    load_b(slot, tro, 0, b[0]);
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+        load_b(slot + GR_BLK, tro, t, b[1]);
+        pre(t);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[0][rt][t] = six(a[rt], b[0], acc[0][rt][t]);
+        if (t < 6) load_b(slot, tro, t + 1, b[0]);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) acc[1][rt][t] = six(a[rt], b[1], acc[1][rt][t]);
+    }
+}
+}  // namespace
+
+__global__ __launch_bounds__(GB2_THREADS, 1) void k_gram_b2(GramArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int np = A.C / 2, n2 = A.pt2 * np, u2x = (n2 + 7) / 8;
+    const int k = blockIdx.x >> 3, j = (blockIdx.x & 7) * u2x + k;   // XCD x: units [x u2x, (x + 1) u2x)
+    if (k >= u2x || j >= n2) return;
+    const int pt = j / np, c0 = 2 * (j - pt * np), c1 = c0 + 1;      // pairs minor: one YB slab per XCD at a time
+    const bool on0 = !(A.sel && chain_bit(A.bits, c0)), on1 = !(A.sel && chain_bit(A.bits, c1));
+    if (!on0 && !on1) return;                             // fit guard: both chains in the residual form
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    const int nbm = A.nblkN, nb = nbm + 16;
+    const int p0 = 256 * pt + 32 * wave;
+    const int tro = bf6::tr_lane_off(lr, lg);
+    const unsigned char* bsrc0 = A.bimg + c0 * A.bimg_cs;
+    const unsigned char* bsrc1 = A.bimg + c1 * A.bimg_cs;
+    auto dma = [&](int i) __attribute__((always_inline)) {
+        unsigned char* slot = lds + (i % GR_NBUF) * GB2_SLOT;
+        if (i < nbm) {
+            const unsigned char* s0 = bsrc0 + (int64_t)i * CONTRACT_SPLIT_BLOCK + lane * 16;
+            const unsigned char* s1 = bsrc1 + (int64_t)i * CONTRACT_SPLIT_BLOCK + lane * 16;
+            for (int q = wave; q < 2 * GR_PIECES; q += GR_CW)
+                bf6::glds16_asm(q < GR_PIECES ? s0 + q * 1024 : s1 + (q - GR_PIECES) * 1024, slot + q * 1024);
+        } else {
+            // extension step s: chain s / 8, block e = s % 8 (-Gb blocks 0..3, then -Hb blocks 0..3)
+            const int s = i - nbm, e = s & 7;
+            const int c = s < 8 ? c0 : c1;
+            const unsigned char* src = (e < 4 ? A.gbimg : A.hbimg) + c * A.gbimg_cs +
+                                       (int64_t)(e & 3) * CONTRACT_SPLIT_BLOCK + lane * 16;
+            for (int q = wave; q < GR_PIECES; q += GR_CW) bf6::glds16_asm(src + q * 1024, slot + q * 1024);
+        }
+    };
+    f32x4 acc[2][2][7];
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) acc[ch][rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const __bf16* yb = A.yb + (int64_t)(p0 + lr) * A.yb_ld + 8 * lg;
+    const int64_t rt16 = 16 * (int64_t)A.yb_ld;
+    bf16x8 a0[2][3], a1[2][3];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a0[rt][pl] = *reinterpret_cast<const bf16x8*>(yb + pl * A.yb_plane + rt * rt16);
+    dma(0);
+    dma(1);
+    auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
+        __syncthreads();                                  // every wave retired block i's pieces; slot (i + 2) % 3 free
+        bf6::wait_vmcnt0();                                    // A(i) and the pieces of block i + 1
+        dma(i + 2);                                       // nb >= 18: always a block i + 2
+        const int ii = min(i + 1, nbm - 1);
+        mma_block2(lds + (i % GR_NBUF) * GB2_SLOT, tro, a, acc, [&](int t) __attribute__((always_inline)) {
+            if (t < 6) {
+                const int rt = t / 3, pl = t % 3;
+                an[rt][pl] = *reinterpret_cast<const bf16x8*>(yb + pl * A.yb_plane + rt * rt16 + 32 * ii);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        });
+    };
+    int i = 0;
+    for (; i + 1 < nbm; i += 2) {
+        step(i, a0, a1);
+        step(i + 1, a1, a0);
+    }
+    if (i < nbm) step(i, a0, a1);
+    // extension, per chain: acc[ch] -= dT Gb (blocks 0..3) and -= T0 Hb (blocks 4..7); A lane (lr, lg) = row p, features
+    // 32f + 4lg + j (j < 4) and 32f + 16 + 4lg + j - 4 (j >= 4) of dT = Zt^ - T0 or of T0; rows past P read 0
+    int64_t roff[2];
+    bool pval[2];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+        const int p = p0 + 16 * rt + lr;
+        pval[rt] = p < A.P;
+        const int pc = min(p, A.P - 1);
+        roff[rt] = (int64_t)(pc / 32) * CONTRACT_SPLIT_BLOCK + (pc % 32) * bf6::PITCH;
+    }
+    // the A operand of extension step s + 1 is loaded (raw bf16 pieces) under step s's products and formed after step
+    // s + 1's wait: formed at load time, hipcc's wait for the loads would also wait for the DMA issued after them
+    struct ExtRaw {
+        bf16x4 lo[2][3], hi[2][3], clo[2][3], chi[2][3];
+    } raw;
+    auto ext_load = [&](int s) __attribute__((always_inline)) {
+        const int e = s & 7, f = e & 3;
+        const unsigned char* tim = A.timg + (s < 8 ? c0 : c1) * A.timg_cs;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) {
+                const int64_t q = roff[rt] + pl * GR_PL + 2 * (32 * f + 4 * lg);
+                raw.clo[rt][pl] = *reinterpret_cast<const bf16x4*>(A.ctimg + q);
+                raw.chi[rt][pl] = f < 3 ? *reinterpret_cast<const bf16x4*>(A.ctimg + q + 32) : bf16x4{};
+                if (e < 4) {
+                    raw.lo[rt][pl] = *reinterpret_cast<const bf16x4*>(tim + q);
+                    raw.hi[rt][pl] = f < 3 ? *reinterpret_cast<const bf16x4*>(tim + q + 32) : bf16x4{};
+                }
+            }
+    };
+    auto ext_form = [&](int s, bf16x8 (&a)[2][3]) __attribute__((always_inline)) {
+        const int e = s & 7;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+            if (e < 4) {
+                bf16x8 z[3], r[3];
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) {
+                    z[pl] = bf6::cat8(raw.lo[rt][pl], raw.hi[rt][pl]);
+                    r[pl] = bf6::cat8(raw.clo[rt][pl], raw.chi[rt][pl]);
+                }
+                delta_frag(z, r, a[rt]);
+            } else {
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) a[rt][pl] = bf6::cat8(raw.clo[rt][pl], raw.chi[rt][pl]);
+            }
+            if (!pval[rt]) {
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) a[rt][pl] = bf16x8{};
+            }
+        }
+    };
+    ext_load(0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int ie = nbm + s;
+        __syncthreads();
+        bf6::wait_vmcnt0();
+        if (s + 2 < 16) dma(ie + 2);
+        bf16x8 a[2][3];
+        ext_form(s, a);
+        if (s + 1 < 16) ext_load(s + 1);
+        mma_block(lds + (ie % GR_NBUF) * GB2_SLOT, tro, a, acc[s >> 3]);
+    }
+    if (on0) gram_tt_epilogue(A, c0, pt, wave, lane, acc[0]);
+    if (on1) gram_tt_epilogue(A, c1, pt, wave, lane, acc[1]);
 }
 
 __device__ __forceinline__ void gram_tt_epilogue(const GramArgs& A, int c, int pt, int wave, int lane,
@@ -1224,13 +1397,27 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     const int n1 = a.NG * a.S * a.C, n2 = a.C * ((gt ? 0 : a.St) + a.Sb);
     a.upx_a = (n1 + 7) / 8;
     const int gpx = (n2 + 7) / 8;
-    a.upx_b = (a.PT * a.SB * a.C + 7) / 8;
+    // two-chain T_t units (k_gram_b2): the row-group count pt2 minimising the rounds of the two launches' T_t units (a
+    // two-chain unit costs GRAM_B2_RATIO one-chain units; ties: the most pairs)
+    a.pt2 = 0;
+    if (a.pair2 == 2 && a.center && a.SB == 1 && a.C >= 2 && a.C % 2 == 0) a.pt2 = a.PT;   // tests: every row group
+    else if (a.pair2 && a.center && a.SB == 1 && a.C >= 2 && a.C % 2 == 0) {
+        double best = 1e30;
+        for (int g = 0; g <= a.PT; ++g) {
+            const int u2x = (g * (a.C / 2) + 7) / 8, u1x = ((a.PT - g) * a.C + 7) / 8;
+            const double cost = GRAM_B2_RATIO * ((u2x + 31) / 32) + (u1x + 31) / 32;
+            if (cost <= best) best = cost, a.pt2 = g;
+        }
+    }
+    a.upx_b = ((a.PT - a.pt2) * a.SB * a.C + 7) / 8;
     const int cpx = (a.C * ((a.N + 31) / 32) + 7) / 8;
     if (!a.aug_done) hipLaunchKernelGGL(k_gram_aug, dim3((a.N + a.P + 255) / 256, a.C), dim3(256), 0, s, a);
     const dim3 ga(8 * (a.upx_a + gpx));
     if (gt) hipLaunchKernelGGL(k_gram_a<1>, ga, dim3(GR_THREADS), GR_LDS, s, a);
     else hipLaunchKernelGGL(k_gram_a<0>, ga, dim3(GR_THREADS), a.center ? GR_LDS_C : GR_LDS, s, a);
     hipLaunchKernelGGL(k_gram_sum, dim3(56 + (a.center ? 98 : 0) + (a.tb_sum ? a.NG * 28 : 0), a.C), dim3(256), 0, s, a);
+    if (a.pt2 > 0)
+        hipLaunchKernelGGL(k_gram_b2, dim3(8 * ((a.pt2 * (a.C / 2) + 7) / 8)), dim3(GB2_THREADS), GB2_LDS, s, a);
     if (a.center) hipLaunchKernelGGL(k_gram_b<1>, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GRB_LDS_C, s, a);
     else hipLaunchKernelGGL(k_gram_b<0>, dim3(8 * (a.upx_b + cpx)), dim3(GR_THREADS), GRB_LDS, s, a);
     if (a.SB > 1) hipLaunchKernelGGL(k_gram_tt, dim3(a.PT * GR_CW, a.C), dim3(64), 0, s, a);

@@ -238,6 +238,9 @@ struct GramArgs {
     int32_t SB, SLB;
     float* tt_part; int64_t tt_cs;
     int32_t upx_a, upx_b;                                  // set by launch_gram
+    // two-chain T_t units (k_gram_b2, round 6): row groups [0, pt2) of chain pairs (2c, 2c + 1) run there; k_gram_b
+    // takes the row groups [pt2, PT) of every chain. Set by launch_gram (pair2 = 0: k_gram_b alone)
+    int32_t pair2, pt2;
     int32_t aug_done;                                      // feature 100 of both images already written
     float gscale;
     int32_t sel; ChainBits bits;                           // sel = 1: chains whose bit is set exit (residual form)

@@ -242,6 +242,7 @@ struct vihmc_plan {
     // so its two data products scale with the residual, not with y. Built lazily (ensure_centre) before the first
     // evaluation that needs it after creation / a data change, on chain 0's slot with its state saved around it.
     int gram_center = 1;
+    int gram_pair2 = 0;               // plan option: centred T_t units of two chains (k_gram_b2; 1: where they fill rounds)
     bool centre_stale = true;
     int tanh_cr = 1;                  // plan option: each net's last hidden layer with the correctly rounded tanh_cr
     int debug_dz = 0;                 // plan option (diagnostics): keep each evaluation's dZ_b / dZ_t
@@ -702,6 +703,7 @@ GramArgs gram_args(vihmc_plan* p, int C) {
     a.gcol_cs = 4 * 112;
     a.ysum = p->ysq_dev + 1;
     a.center = p->gram_center ? 1 : 0;
+    a.pair2 = p->gram_pair2;
     if (a.center) {
         a.cbimg = p->cimgB;
         a.ctimg = p->cimgT;
@@ -2221,7 +2223,7 @@ int vihmc_timing_reset(vihmc_plan* p) {
     return 0;
 }
 
-#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, timing_every, fwd_wimg, fwd_in0, skip_zt, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_active, gram_center, tanh_cr, debug_dz, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
+#define OPTION_KEYS "fwd_bf16x6, contract_bf16x6, bwd_bf16x6, graph, timing_every, fwd_wimg, fwd_in0, skip_zt, fuse_scatter, img_scatter, mlp_fast, bwd_chain, gram, gram_active, gram_center, gram_pair2, tanh_cr, debug_dz, gram_min_chains, gram_guard, grad_evals, gram_evals, gram_chains, gram_chain_evals, y_masked, lik_count"
 
 int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     if (!p || !key) return fail("null argument");
@@ -2261,6 +2263,10 @@ int vihmc_plan_option(vihmc_plan* p, const char* key, int value) {
     else if (k == "tanh_cr") {                                  // forward: the centre (a forward output) is stale
         p->tanh_cr = value ? 1 : 0;
         p->centre_stale = true;
+    }
+    else if (k == "gram_pair2") {                               // two-chain T_t units (bitwise the same dZt);
+        if (value < 0 || value > 2) return fail("gram_pair2: 0, 1 or 2");
+        p->gram_pair2 = value;                                  // 2: on every row group (tests)
     }
     else if (k == "gram_center") {                              // centred Gram form (1) or y itself (0)
         if ((value ? 1 : 0) != p->gram_center) {
@@ -2302,6 +2308,7 @@ int vihmc_plan_get_option(const vihmc_plan* p, const char* key, int* value) {
     // falls back to the residual form for its chain count says so here
     else if (k == "gram_active") *value = gram_on(p) ? 1 : 0;
     else if (k == "gram_center") *value = p->gram_center;
+    else if (k == "gram_pair2") *value = p->gram_pair2;
     else if (k == "tanh_cr") *value = p->tanh_cr;
     else if (k == "debug_dz") *value = p->debug_dz;
     else if (k == "grad_evals") *value = (int)std::min<int64_t>(p->n_grad_calls, INT32_MAX);
