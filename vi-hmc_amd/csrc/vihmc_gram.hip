@@ -912,9 +912,10 @@ __global__ __launch_bounds__(GB2_THREADS, 1) void k_gram_b2(GramArgs A) {
         for (int pl = 0; pl < 3; ++pl) a0[rt][pl] = *reinterpret_cast<const bf16x8*>(yb + pl * A.yb_plane + rt * rt16);
     dma(0);
     dma(1);
+    bf6::wait_vmcnt0();                                   // block 0 is read after the first barrier: retire it before
     auto step = [&](int i, bf16x8 (&a)[2][3], bf16x8 (&an)[2][3]) __attribute__((always_inline)) {
         __syncthreads();                                  // every wave retired block i's pieces; slot (i + 2) % 3 free
-        bf6::wait_vmcnt0();                                    // A(i) and the pieces of block i + 1
+        bf6::wait_vmcnt0();                               // A(i) and the pieces of block i + 1
         dma(i + 2);                                       // nb >= 18: always a block i + 2
         const int ii = min(i + 1, nbm - 1);
         mma_block2(lds + (i % GR_NBUF) * GB2_SLOT, tro, a, acc, [&](int t) __attribute__((always_inline)) {
