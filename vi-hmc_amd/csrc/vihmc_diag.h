@@ -15,8 +15,8 @@
 //    6                    CH_STAMP        per-layer stamps of k_bwd_chain (stamps_chain.py)
 //    7-8                  CB_STAMP        side-A contraction stamps, two placements 1 / 2 (stamps_side_a.py)
 //    9                    GR_STAMP        per-block stamps of k_gram_a's T_b units (stamps_gram.py)
-//    10-11                GR_ABL          Gram ablations: 1 = no A loads in the main loops, 2 = one B fragment per
-//                                         block, 3 = both
+//    10-11                GR_ABL          Gram ablations: 1 = no A loads in the main loops (block 0's), 2 = no block
+//                                         DMA (the ring keeps stale data), 3 = both
 //    12-13                CH_ABL          k_bwd_chain ablations: 1 = no dW MFMAs, 2 = no dX bf16 MFMAs
 //    14-15                GATHER_ABL      leapfrog gather: 1 = no scatter into packed weights / images, 2 = nor theta/p
 //    16                   RD_ONLY_FIRST   grouped row-dot launches run their first problem's workgroups only

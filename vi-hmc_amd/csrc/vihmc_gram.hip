@@ -72,7 +72,8 @@ __host__ __device__ inline int kpos(int k) { return k < 16 ? 8 * (k >> 2) + (k &
 // iteration i (every wave is past block i-1 = buffer (i+2) % 3), then wait for block i+1 (21 newer copies may stay
 // in flight) so the next barrier publishes it. SRC(i) gives block i's global address.
 #define GRAM_DMA_PIECES(SRC, BUF)                                                                             \
-    for (int k = 0; k < GR_PIECES; ++k) bf6::glds16_asm((SRC) + k * 1024 + lane * 16, lds + (BUF) * GR_BLK + k * 1024);
+    for (int k = 0; k < (GR_ABL & 2 ? 0 : GR_PIECES); ++k)                                                     \
+        bf6::glds16_asm((SRC) + k * 1024 + lane * 16, lds + (BUF) * GR_BLK + k * 1024);
 
 struct NoStamp {
     __device__ void operator()(int, int) const {}
@@ -111,8 +112,9 @@ __device__ __forceinline__ void dma_role2(unsigned char* lds, int lane, int nb, 
         const unsigned char* a = s0 + (int64_t)i * CONTRACT_SPLIT_BLOCK;
         const unsigned char* b = s1 + (int64_t)i * CONTRACT_SPLIT_BLOCK;
         unsigned char* d = lds + (i % GR_NBUF) * 2 * GR_BLK;
-        for (int k = 0; k < GR_PIECES; ++k) bf6::glds16_asm(a + k * 1024 + lane * 16, d + k * 1024);
-        for (int k = 0; k < GR_PIECES; ++k) bf6::glds16_asm(b + k * 1024 + lane * 16, d + GR_BLK + k * 1024);
+        for (int k = 0; k < (GR_ABL & 2 ? 0 : GR_PIECES); ++k) bf6::glds16_asm(a + k * 1024 + lane * 16, d + k * 1024);
+        for (int k = 0; k < (GR_ABL & 2 ? 0 : GR_PIECES); ++k)
+            bf6::glds16_asm(b + k * 1024 + lane * 16, d + GR_BLK + k * 1024);
     };
     if (nb > 0) issue(0);
     if (nb > 1) issue(1);
@@ -174,10 +176,9 @@ __device__ __forceinline__ void mma_block(const unsigned char* buf, int tro, con
                                           f32x4 (&acc)[2][7], PRE pre = PRE{}) {
     bf16x8 b[2][3];
     load_b(buf, tro, 0, b[0]);
-    if (GR_ABL & 2) load_b(buf, tro, 1, b[1]);
 #pragma unroll
     for (int t = 0; t < 7; ++t) {
-        if (t < 6 && !(GR_ABL & 2)) load_b(buf, tro, t + 1, b[(t + 1) & 1]);
+        if (t < 6) load_b(buf, tro, t + 1, b[(t + 1) & 1]);
         pre(t);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) acc[rt][t] = six(a[rt], b[t & 1], acc[rt][t]);
