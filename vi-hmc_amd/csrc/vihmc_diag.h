@@ -57,3 +57,5 @@
 #define GRAM_DZB_FP64 1
 // Gram form, centred: cost of a two-chain T_t unit (k_gram_b2) in one-chain units, for launch_gram's row-group split
 #define GRAM_B2_RATIO 1.7
+// centred Gram form, 8+ chains: Gram-t slabs per T_b slab (k_gram_a's Gram-t units GRAM_T_SPLIT times shorter)
+#define GRAM_T_SPLIT 2

@@ -1237,9 +1237,24 @@ __device__ __forceinline__ void dzb_unit_c(const GramArgs& A, int u, unsigned ch
     const int64_t sstride = (int64_t)A.NG * GR_CW * 14 * 256;
     const int nslab = pre ? 1 : A.S;
     float* out = A.dzb + c * A.dzb_cs;
-    for (int tile = wv; tile < 14; tile += GR_THREADS / 64) {
-        const int rt = tile / 7, t = tile - rt * 7;
-        double ts[4] = {0, 0, 0, 0};
+    // tiles wv and wv + 9 (< 14) of the 2 x 7 accumulator tiles. Zb^ Gt + B0 Ht as exact f32 MFMAs (16x16x4: the products
+    // of one instruction accumulate as a sequential fmaf chain over k, MI355X_MICROARCH.md): k step j takes v = 2j, 2j + 1
+    // as (B0 Ht, dB Gt, B0 Ht, dB Gt) -- the order of the former VALU loop (per v: fma(b, h), then fma(d, g)), so the
+    // same roundings, bit for bit (profiles/r06o_dzb_mfma_ab.txt); 51 dependent MFMAs per tile, two tiles' chains
+    // interleaved. The units' time is their staging loads, not these products: 46.6 -> 46.0 us for all 512 units
+    constexpr int NWV = GR_THREADS / 64;
+    const bool two = wv + NWV < 14;
+    const float* asrc = (lg & 1) ? dbt : b0t;
+    const float* bsrc = (lg & 1) ? gts : hts;
+    double ts[2][4];
+    int tl[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int tile = min(wv + NWV * q, 13);
+        tl[q] = tile;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ts[q][r] = 0.0;
+        if (q == 1 && !two) continue;
         int ss = 0;
         for (; ss + 8 <= nslab; ss += 8) {
             f32x4 v[8];
@@ -1248,28 +1263,39 @@ __device__ __forceinline__ void dzb_unit_c(const GramArgs& A, int u, unsigned ch
 #pragma unroll
             for (int k = 0; k < 8; ++k)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) ts[r] += (double)v[k][r];
+                for (int r = 0; r < 4; ++r) ts[q][r] += (double)v[k][r];
         }
         for (; ss < nslab; ++ss) {
             const f32x4 v = *reinterpret_cast<const f32x4*>(tb + ss * sstride + tile * 256);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) ts[r] += (double)v[r];
+            for (int r = 0; r < 4; ++r) ts[q][r] += (double)v[r];
         }
-        float gz[4] = {0.f, 0.f, 0.f, 0.f};
-        const int x = 16 * t + lr;
-        for (int v = 0; v < 101; ++v) {
-            const f32x4 d = *reinterpret_cast<const f32x4*>(dbt + v * 32 + 16 * rt + 4 * lg);
-            const f32x4 b = *reinterpret_cast<const f32x4*>(b0t + v * 32 + 16 * rt + 4 * lg);
-            const float g = gts[v * 112 + x];
-            const float h = hts[v * 112 + x];
+    }
+    f32x4 gz[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const int ao[2] = {16 * (tl[0] / 7) + lr, 16 * (tl[1] / 7) + lr};
+    const int bo[2] = {16 * (tl[0] % 7) + lr, 16 * (tl[1] % 7) + lr};
+    for (int j = 0; j < 51; ++j) {
+        const int v = 2 * j + (lg >> 1);
+        const bool vok = v < 101;
+        const int vc = min(v, 100);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) gz[r] = fmaf(d[r], g, fmaf(b[r], h, gz[r]));
+        for (int q = 0; q < 2; ++q) {
+            if (q == 1 && !two) break;
+            const float av = vok ? asrc[vc * 32 + ao[q]] : 0.f;
+            const float bv = vok ? bsrc[vc * 112 + bo[q]] : 0.f;
+            gz[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, gz[q], 0, 0, 0);
         }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        if (q == 1 && !two) break;
+        const int rt = tl[q] / 7, t = tl[q] - rt * 7;
+        const int x = 16 * t + lr;
         if (x < 100) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int n = n32 + 16 * rt + 4 * lg + r;
-                if (n < A.N) out[(int64_t)n * A.ldz + x] = (float)((double)A.gscale * ((double)gz[r] - ts[r]));
+                if (n < A.N) out[(int64_t)n * A.ldz + x] = (float)((double)A.gscale * ((double)gz[q][r] - ts[q][r]));
             }
         }
     }
@@ -1385,7 +1411,7 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
         return hipErrorInvalidValue;
     if (a.SB < 1 || a.SLB < 1 || a.SB * a.SLB < a.nblkN || (a.SB - 1) * a.SLB >= a.nblkN || (a.SB > 1 && !a.tt_part))
         return hipErrorInvalidValue;
-    if (a.St != a.S || a.SLt != a.SL) return hipErrorInvalidValue;   // the Gram-t tiles ride the T_b slabs
+    if (a.St < 1 || a.SLt < 1 || a.St * a.SLt < a.nblkP || (a.St - 1) * a.SLt >= a.nblkP) return hipErrorInvalidValue;
     if (a.Sb < 1 || a.SLb < 1 || a.Sb * a.SLb < a.nblkN || (a.Sb - 1) * a.SLb >= a.nblkN || !a.gb_part)
         return hipErrorInvalidValue;
     if (a.S > GRAM_TB_DIRECT ? !a.tb_sum : a.tb_sum != nullptr) return hipErrorInvalidValue;
@@ -1396,6 +1422,7 @@ hipError_t launch_gram(const GramArgs& a0, hipStream_t s) {
     // fewer n groups keep the Gram-t units (two or four tiles per T_b wave spill registers). Centred: the Gram units
     // stream the centre's image beside the outputs' and compute G with H (Gram-t units of their own)
     const int gt = a.NG >= 4 && !a.center ? 1 : 0;
+    if (gt && (a.St != a.S || a.SLt != a.SL)) return hipErrorInvalidValue;   // the Gram-t tiles ride the T_b slabs
     const int n1 = a.NG * a.S * a.C, n2 = a.C * ((gt ? 0 : a.St) + a.Sb);
     a.upx_a = (n1 + 7) / 8;
     const int gpx = (n2 + 7) / 8;

@@ -220,6 +220,7 @@ struct vihmc_plan {
     __bf16* gyb = nullptr;        // y^T [PT*256][32 nblkN], 3 planes
     int64_t gya_plane = 0, gyb_plane = 0;
     int gya_ld = 0, gyb_ld = 0, gNG = 0, gS = 0, gSL = 0, gPT = 0, gSB = 1, gSLB = 1, gSt = 1, gSLt = 1;
+    int gStc = 1, gSLtc = 1;      // the centred form's Gram-t units (units of their own: any split, GRAM_T_SPLIT x S)
     float* gtt_part = nullptr;    // T_t split-K slabs (gSB > 1)
     int64_t gtt_cs = 0;
     float* gtb_part = nullptr;
@@ -491,6 +492,10 @@ int gram_setup(vihmc_plan* p, int C) {
     // k_gram_a's time: 45 us, profiles/r04n_c1)
     p->gSt = p->gS;
     p->gSLt = p->gSL;
+    // centred: the Gram-t units (H beside G, ~0.8 of a T_b unit) are k_gram_a's short units that fill the chip around the
+    // 512 T_b units at 16 chains; shorter ones (GRAM_T_SPLIT slabs per T_b slab) pack the rounds tighter
+    p->gSLtc = cdiv(nblkP, std::min(nblkP, p->gS * (C >= 8 ? GRAM_T_SPLIT : 1)));
+    p->gStc = cdiv(nblkP, p->gSLtc);
     p->gSLb = std::min(p->gSL, nblkN);
     p->gSb = cdiv(nblkN, p->gSLb);
     const int ngrp = cdiv(p->N, 32);
@@ -505,7 +510,7 @@ int gram_setup(vihmc_plan* p, int C) {
     if (int rc = p->alloc(&p->gyb, 3 * p->gyb_plane)) return rc;
     p->gtb_cs = (int64_t)p->gS * p->gNG * 8 * 14 * 256;
     if (int rc = p->alloc(&p->gtb_part, p->gtb_cs * C)) return rc;
-    p->ggt_part_cs = (int64_t)p->gSt * 28 * 256;         // the 28 upper tiles per slab
+    p->ggt_part_cs = (int64_t)std::max(p->gSt, p->gStc) * 28 * 256;   // the 28 upper tiles per slab
     if (int rc = p->alloc(&p->ggt_part, p->ggt_part_cs * C)) return rc;
     p->ggb_part_cs = (int64_t)p->gSb * 28 * 256;
     if (int rc = p->alloc(&p->ggb_part, p->ggb_part_cs * C)) return rc;
@@ -534,7 +539,7 @@ int gram_setup(vihmc_plan* p, int C) {
     if (int rc = p->alloc(&p->cB0, (int64_t)p->N * p->ldz)) return rc;
     if (int rc = p->alloc(&p->ccol, 112)) return rc;
     if (int rc = p->alloc(&p->cysq, 2)) return rc;
-    p->ght_cs = (int64_t)p->gSt * 49 * 256;
+    p->ght_cs = (int64_t)p->gStc * 49 * 256;
     p->ghb_cs = (int64_t)p->gSb * 49 * 256;
     if (int rc = p->alloc(&p->ght_part, p->ght_cs * C)) return rc;
     if (int rc = p->alloc(&p->ghb_part, p->ghb_cs * C)) return rc;
@@ -727,8 +732,8 @@ GramArgs gram_args(vihmc_plan* p, int C) {
     a.S = p->gS;
     a.SL = p->gSL;
     a.PT = p->gPT;
-    a.St = p->gSt;
-    a.SLt = p->gSLt;
+    a.St = p->gram_center ? p->gStc : p->gSt;
+    a.SLt = p->gram_center ? p->gSLtc : p->gSLt;
     a.SB = p->gSB;
     a.SLB = p->gSLB;
     a.tt_part = p->gtt_part;
