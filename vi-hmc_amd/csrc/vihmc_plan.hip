@@ -496,7 +496,7 @@ int gram_setup(vihmc_plan* p, int C) {
     // 512 T_b units at 16 chains; shorter ones (GRAM_T_SPLIT slabs per T_b slab) pack the rounds tighter
     p->gSLtc = cdiv(nblkP, std::min(nblkP, p->gS * (C >= 8 ? GRAM_T_SPLIT : 1)));
     p->gStc = cdiv(nblkP, p->gSLtc);
-    p->gSLb = std::min(p->gSL, nblkN);
+    p->gSLb = std::min(p->gSLtc, nblkN);              // the Gram-t cut (16 chains: slabs of 20 and 12 blocks)
     p->gSb = cdiv(nblkN, p->gSLb);
     const int ngrp = cdiv(p->N, 32);
     p->gSB = std::max(1, std::min(nblkN, (256 - std::min(ngrp * C, 128)) / (p->gPT * C)));
