@@ -24,7 +24,7 @@ import os
 RECORDS = []
 
 LOOSE = {"logp_rel": 1e-3, "grad_relnorm": 2e-4, "grad_elem": 2e-3, "grad_norm_rel": 2e-4, "pred_elem": 1e-3,
-         "pos_maxabs": 1e-4, "mom_maxabs": 1e-4, "mean_rel_l2": 1e-4}
+         "pos_maxabs": 1e-4, "mom_maxabs": 1e-4, "mean_rel_l2": 1e-4, "grad_relnorm_uncentred": 2e-3}
 
 # (test function, quantity) -> bound: 4x the maximum measured on the MI355X in round 5 (profiles/r05_parity_errors.json,
 # the calibration run r05b), rounded up to one significant digit
@@ -100,6 +100,10 @@ BOUNDS = {
     ('test_split_loadprior_small_closures', 'grad_relnorm'): 3e-07,   # max 6.13e-08 over 2
     ('test_split_loadprior_small_closures', 'logp_rel'): 2e-07,   # max 0 over 2 (floor: one fp32 ulp-level difference allowed)
     ('test_split_shards_small_rows_on_concurrent_streams', 'logp_rel'): 4e-06,   # max 8.57e-07 over 2
+    # round 6 (r06aa): 16 chains 0.02 N(0, 1) off the goldens (fits far worse than the centre's), against the residual
+    # form -- the uncentred form has no cancellation at such fits, the centred one carries terms of the size of dB Gt
+    ('test_uncentred_gram_16_chains_vs_residual', 'grad_relnorm_uncentred'): 4e-06,   # max 8.40e-07 over 1
+    ('test_uncentred_gram_16_chains_vs_residual', 'grad_relnorm'): 2e-05,   # max 4.90e-06 over 1
 }
 
 

@@ -506,3 +506,23 @@ def test_gram_pair2_with_guarded_chains(cuda_device):
         res.append(g.cpu())
         eng.close()
     assert torch.equal(res[0], res[1])
+
+
+def test_uncentred_gram_16_chains_vs_residual(cuda_device):
+    """The uncentred Gram form (gram_center = 0) at 16 distinct chains -- the Gram-t tiles folded into the T_b units
+    (4 row groups) and the Gram-b units cut to the centred form's slab length (two slabs at 16 chains) -- against the
+    residual form, and the centred form on the same chains (each within its recorded bound)."""
+    c = deeponet_case("deeponet_burgers")
+    C = 16
+    base = np.stack([c.thetas[i % len(c.thetas)] for i in range(C)]).astype(np.float32)
+    rng = np.random.default_rng(31)
+    th = torch.tensor(base + 0.02 * rng.standard_normal(base.shape, dtype=np.float32), device=cuda_device)
+    eng = engine_for(c, C, cuda_device)
+    _, gr = eng.logp_grad(th)
+    gr = gr.cpu().numpy()
+    for center in (0, 1):
+        eng.option("gram_center", center)
+        g = eng.grad(th).cpu().numpy()
+        assert eng.get_option("gram") & 2 and eng.get_option("gram_chains") == C
+        worst = max(rel_norm(g[i], gr[i]) for i in range(C))
+        parity.check("grad_relnorm" if center else "grad_relnorm_uncentred", worst, f"gram_center = {center}")
