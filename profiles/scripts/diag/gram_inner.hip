@@ -103,6 +103,72 @@ __global__ __launch_bounds__(NW * 64, 1) void k_inner(const bf16x8* src, float* 
     }
 }
 
+// RT row tiles per wave (RT = 4: 64 rows, each B fragment feeds four row tiles), NWG workgroups per CU via the grid
+template <int RT, int NW>
+__global__ __launch_bounds__(NW * 64) void k_inner_rt(const bf16x8* src, float* out, unsigned long long* clk) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds[BLK];
+    const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lg = lane >> 4;
+    for (int i = tid; i < BLK / 16; i += NW * 64) reinterpret_cast<bf16x8*>(lds)[i] = src[i % 4096];
+    bf16x8 a[RT][3];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[rt][pl] = src[(tid + 64 * (rt * 3 + pl)) % 4096];
+    __syncthreads();
+    const int tro = (4 * lg + (lr >> 2)) * PITCH + 8 * (lr & 3);
+    f32x4 acc[RT][7];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < ITERS * 2 / RT; ++it) {
+        bf16x8 b[2][3];
+        load_b(lds, tro, 0, b[0]);
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            if (t < 6) load_b(lds, tro, t + 1, b[(t + 1) & 1]);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) acc[rt][t] = six(a[rt], b[t & 1], acc[rt][t]);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    float s = 0.f;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int t = 0; t < 7; ++t) s += acc[rt][t][0] + acc[rt][t][1] + acc[rt][t][2] + acc[rt][t][3];
+    out[blockIdx.x * NW * 64 + tid] = s;
+    if (tid == 0) {
+        clk[2 * blockIdx.x] = t1 - t0;
+        clk[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
+// same MFMA count per SIMD as run<0, 8>: (waves per SIMD) x (ITERS x 2 / RT blocks) x (RT x 7 x 6 MFMAs)
+template <int RT, int NW>
+void run_rt(const char* name, const bf16x8* src, float* out, unsigned long long* clk, int nblk, int wg_per_cu) {
+    hipLaunchKernelGGL((k_inner_rt<RT, NW>), dim3(nblk), dim3(NW * 64), 0, 0, src, out, clk);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL((k_inner_rt<RT, NW>), dim3(nblk), dim3(NW * 64), 0, 0, src, out, clk);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    std::vector<unsigned long long> h(2 * nblk);
+    hipMemcpy(h.data(), clk, h.size() * 8, hipMemcpyDeviceToHost);
+    double cyc = 0, rt = 0;
+    for (int b = 0; b < nblk; ++b) cyc += h[2 * b], rt += h[2 * b + 1];
+    const double mhz = cyc / rt * 100.0;
+    const double mfma_per_simd = (NW / 4.0) * wg_per_cu * (ITERS * 2.0 / RT) * RT * 42.0;
+    const double us_floor = mfma_per_simd * 16.0 / mhz;
+    printf("%-34s %8.1f us  clock %6.0f MHz  MFMA busy (wall, at that clock) %.3f\n", name, ms * 1e3, mhz,
+           us_floor / (ms * 1e3));
+}
+
 template <int V, int NW>
 void run(const char* name, const bf16x8* src, float* out, unsigned long long* clk, int nblk) {
     hipLaunchKernelGGL((k_inner<V, NW>), dim3(nblk), dim3(NW * 64), 0, 0, src, out, clk);   // warm
@@ -146,5 +212,14 @@ int main() {
     run<0, 4>("v3 shipped, 4 waves", src, out, clk, nblk);
     run<0, 12>("v4 shipped, 12 waves", src, out, clk, nblk);
     run<1, 4>("v5 B in registers, 4 waves", src, out, clk, nblk);
+    // row tiles per wave: RT = 2 (shipped, 8 waves per CU) vs RT = 4 (4-wave workgroups, two per CU: 512 blocks)
+    hipFree(out);
+    hipFree(clk);
+    hipMalloc(&out, 2 * nblk * 12 * 64 * 4);
+    hipMalloc(&clk, 2 * nblk * 2 * 8);
+    run_rt<2, 8>("rt2 8 waves, 1 wg/CU", src, out, clk, nblk, 1);
+    run_rt<4, 4>("rt4 4 waves, 2 wg/CU", src, out, clk, 2 * nblk, 2);
+    run_rt<2, 8>("rt2 8 waves, 1 wg/CU (again)", src, out, clk, nblk, 1);
+    run_rt<4, 4>("rt4 4 waves, 2 wg/CU (again)", src, out, clk, 2 * nblk, 2);
     return 0;
 }
